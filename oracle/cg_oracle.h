@@ -1,0 +1,117 @@
+/*
+ * cg_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's two pixel-loop hot paths
+ * (fznsakib/Computer-Graphics: raytracer/Source/skeleton.cpp and
+ * rasteriser/Source/skeleton.cpp), written from scratch in plain C with the
+ * reference's exact IEEE operation order (GLM 0.9.7.2 association, no FMA,
+ * FP64 islands where the reference promotes to double).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / CPU baseline.  The product
+ * path (include/cg_render.h, computer-graphics_amd/) never links it.
+ *
+ * Pinning: the RT restatement is pinned bit-exactly by the reference's own
+ * golden image raytracer/screenshot.bmp (tests/golden/rt_screenshot_320x256.bmp).
+ * The RAST restatement is pinned by the reference's first-party
+ * ComputePolygonRows KAT (rasteriser/Source/skeleton.cpp:183-199) and by the
+ * frame fingerprints recorded in SURVEY.md section 8c.
+ */
+#ifndef CG_ORACLE_H
+#define CG_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { float x, y, z; } cgo_v3;
+typedef struct { float x, y, z, w; } cgo_v4;
+
+/* raytracer/Source/TestModelH.h:80-115 (76 bytes, same field order). */
+typedef struct { cgo_v4 v0, v1, v2, normal; cgo_v3 color; } cgo_rt_tri;
+/* raytracer/Source/TestModelH.h:14-22 (44 bytes, same field order). */
+typedef struct { float radius, radiusSquared; cgo_v3 centre, color, normal; } cgo_sphere;
+/* raytracer/Source/skeleton.cpp:40-45 */
+typedef struct { cgo_v4 position; float distance; int triangleIndex; int sphereIndex; } cgo_isect;
+/* raytracer/Source/skeleton.cpp:47-50 */
+typedef struct { cgo_v4 position; cgo_v3 colour; } cgo_light;
+
+/* Frame parameters = the reference's RT globals (skeleton.cpp:56-60). */
+typedef struct {
+    int width, height;
+    float focal;
+    cgo_v4 camera;
+    float R[16];        /* glm::mat4, column-major: R[c*4+r] = m[c][r] */
+    float indirect;     /* skeleton.cpp:110, 0.5 */
+    int n_lights;
+    cgo_light lights[4];
+} cgo_rt_params;
+
+/* Work counters. */
+typedef struct {
+    uint64_t n_ray, n_t, n_uv, n_sph, n_dl;
+} cgo_rt_counters;
+
+int  cgo_rt_load_scene(cgo_rt_tri *tris, int cap, cgo_sphere *sph);
+void cgo_rt_default_params(cgo_rt_params *p, int width, int height);
+int  cgo_rt_closest(cgo_v4 start, cgo_v4 dir, const cgo_rt_tri *tris, int n_tris,
+                    const cgo_sphere *sph, int n_sph, cgo_isect *out, cgo_rt_counters *cnt);
+cgo_v3 cgo_rt_direct_light(const cgo_isect *i, const cgo_rt_tri *tris, int n_tris,
+                           const cgo_sphere *sph, int n_sph, const cgo_light *light,
+                           cgo_rt_counters *cnt);
+int  cgo_sphere_solve_quadratic(float a, float b, float c, float *x0, float *x1);
+int  cgo_sphere_intersect(const cgo_sphere *s, cgo_v3 start, cgo_v3 dir, float *t);
+uint32_t cgo_put_pixel(cgo_v3 colour);
+/* Render rows [row0,row1) of the frame into argb (full W*H buffer, row-major). */
+void cgo_rt_draw(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                 const cgo_sphere *sph, int n_sph, uint32_t *argb, int row0, int row1,
+                 cgo_rt_counters *cnt);
+/* Same, multithreaded by rows (pthreads); returns threads used. */
+int  cgo_rt_draw_mt(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                    const cgo_sphere *sph, int n_sph, uint32_t *argb, int row0, int row1,
+                    int n_threads);
+
+/* ------------------------------- RAST --------------------------------- */
+
+/* rasteriser/Source/TestModelH.h:13-42 (84 bytes). */
+typedef struct { cgo_v4 v0, v1, v2, normal; cgo_v3 color; int texture; int index; } cgo_rast_tri;
+/* rasteriser/Source/skeleton.cpp:88-94 */
+typedef struct { int x, y; float zinv; cgo_v4 pos3d; } cgo_pixel;
+
+typedef struct {
+    int width, height;
+    float focal;
+    cgo_v4 camera;
+    float R[16];
+    cgo_v4 light_scene;       /* sceneCoordinatesLightPos, skeleton.cpp:52 */
+    cgo_v3 light_power;       /* skeleton.cpp:53 */
+    float indirect_first;     /* value of indirectLightPowerPerArea at frame start (0.15 first frame, 0.2 after) */
+} cgo_rast_params;
+
+typedef struct {
+    uint64_t n_tris, n_spans, n_frags, n_shaded, n_shadow;
+} cgo_rast_counters;
+
+int  cgo_rast_load_scene(cgo_rast_tri *room, int *n_room, cgo_rast_tri *boxes, int *n_boxes);
+void cgo_rast_default_params(cgo_rast_params *p, int width, int height);
+/* Host geometry of Draw (skeleton.cpp:205-241): returns number of clipped
+ * triangles written to out (cap entries), light position (camera space,
+ * rotated) to *light_out. */
+int  cgo_rast_geometry(const cgo_rast_params *p, cgo_rast_tri *out, int cap, cgo_v4 *light_out);
+int  cgo_rast_clip(const cgo_rast_tri *in, int n, int plane, const cgo_rast_params *p,
+                   cgo_rast_tri *out, int cap);
+void cgo_rast_vertex_shader(const cgo_rast_params *p, cgo_v4 v, cgo_pixel *px);
+void cgo_rast_interpolate(cgo_pixel a, cgo_pixel b, cgo_pixel *result, int n);
+/* Returns rows; left/right must hold >= rows entries (pass NULL to query). */
+int  cgo_rast_polygon_rows(const cgo_pixel *vp, cgo_pixel *left, cgo_pixel *right, int cap);
+/* Full RAST frame. Any output pointer may be NULL. Buffers W*H. screen/low/high
+ * are float[3*W*H]. */
+void cgo_rast_draw(const cgo_rast_params *p, uint32_t *argb, float *depth, int32_t *shadow,
+                   float *screen_buf, float *low_buf, float *high_buf, cgo_rast_counters *cnt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
