@@ -1,0 +1,294 @@
+"""ctypes binding of the MI355X renderer's C-ABI (include/cg_render.h).
+
+This is harness plumbing for tests/ and bench.py; the product host surface is
+the C++ in host/ (the reference's Draw(screen*) shape).  Loading fails loudly
+when libcgamd.so is missing: there is no CPU fallback anywhere on the product
+path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libcgamd.so")
+
+CG_OK, CG_E_INVALID, CG_E_NODEVICE, CG_E_HIP, CG_E_NOSCENE, CG_E_CAPACITY = 0, -1, -2, -3, -4, -5
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Vec4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class Tri(C.Structure):        # raytracer Triangle, 76 B
+    _fields_ = [("v0", Vec4), ("v1", Vec4), ("v2", Vec4), ("normal", Vec4), ("color", Vec3)]
+
+
+class Sphere(C.Structure):     # 44 B
+    _fields_ = [("radius", C.c_float), ("radiusSquared", C.c_float), ("centre", Vec3),
+                ("color", Vec3), ("normal", Vec3)]
+
+
+class Light(C.Structure):      # 28 B
+    _fields_ = [("position", Vec4), ("colour", Vec3)]
+
+
+class Isect(C.Structure):      # Intersection, 28 B
+    _fields_ = [("position", Vec4), ("distance", C.c_float), ("triangleIndex", C.c_int),
+                ("sphereIndex", C.c_int)]
+
+
+class RtCamera(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", Vec4),
+                ("R", C.c_float * 16), ("indirect", C.c_float)]
+
+
+class RtShard(C.Structure):
+    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("stripe_h", C.c_int)]
+
+
+class RTri(C.Structure):       # rasteriser Triangle, 84 B
+    _fields_ = [("v0", Vec4), ("v1", Vec4), ("v2", Vec4), ("normal", Vec4), ("color", Vec3),
+                ("texture", C.c_int), ("index", C.c_int)]
+
+
+class RastParams(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", Vec4),
+                ("R", C.c_float * 16), ("light_scene", Vec4), ("light_power", Vec3),
+                ("indirect_first", C.c_float)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double), ("total_ms", C.c_double), ("n_tris", C.c_int),
+                ("n_spans", C.c_int)]
+
+
+assert C.sizeof(Tri) == 76 and C.sizeof(Sphere) == 44 and C.sizeof(Light) == 28
+assert C.sizeof(Isect) == 28 and C.sizeof(RTri) == 84
+
+P = C.c_void_p
+_SIGS = {
+    "cg_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "cg_destroy": (None, [P]),
+    "cg_last_error": (C.c_char_p, [P]),
+    "cg_device_count": (C.c_int, []),
+    "cg_rt_load_test_model": (C.c_int, [C.POINTER(Tri), C.c_int, C.POINTER(Sphere)]),
+    "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
+    "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
+    "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
+                                      C.POINTER(RtShard), P, P]),
+    "cg_rt_shard_rows": (C.c_int, [C.c_int, C.POINTER(RtShard)]),
+    "cg_rt_unstripe_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "cg_rt_probe_closest": (C.c_int, [P, C.POINTER(Vec4), C.POINTER(Vec4), C.c_int,
+                                      C.POINTER(Isect), C.POINTER(C.c_int)]),
+    "cg_rt_probe_direct_light": (C.c_int, [P, C.POINTER(Isect), C.POINTER(Light), C.c_int,
+                                           C.POINTER(Vec3)]),
+    "cg_rast_load_test_model": (C.c_int, [C.POINTER(RTri), C.c_int, C.POINTER(C.c_int),
+                                          C.POINTER(RTri), C.c_int, C.POINTER(C.c_int)]),
+    "cg_rast_prepare": (C.c_int, [C.POINTER(RastParams), C.POINTER(RTri), C.c_int, C.POINTER(RTri),
+                                  C.c_int, C.POINTER(RTri), C.c_int, C.POINTER(Vec4)]),
+    "cg_rast_render": (C.c_int, [P, C.POINTER(RTri), C.c_int, C.POINTER(RastParams), Vec4, P, P, P,
+                                 C.POINTER(Stats)]),
+    "cg_rast_render_device": (C.c_int, [P, P, C.c_int, C.POINTER(RastParams), Vec4, P, P, P, P]),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libcgamd.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libcgamd.so not built at {path}; run __graft_entry__.build()")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def identity16():
+    return (C.c_float * 16)(*[1.0 if k % 5 == 0 else 0.0 for k in range(16)])
+
+
+def yaw_matrix(yaw: float):
+    """R for a yaw angle exactly as Update() sets it (RT skeleton.cpp:236-238):
+    R[0][0]=cos R[0][2]=-sin R[2][0]=sin R[2][2]=cos, float32 cos/sin."""
+    y = np.float32(yaw)
+    c, s = np.cos(y, dtype=np.float32), np.sin(y, dtype=np.float32)
+    m = [1.0 if k % 5 == 0 else 0.0 for k in range(16)]
+    m[0 * 4 + 0], m[0 * 4 + 2] = float(c), float(-s)
+    m[2 * 4 + 0], m[2 * 4 + 2] = float(s), float(c)
+    return (C.c_float * 16)(*m)
+
+
+def rt_camera(width, height, focal=256.0, cam=(0.0, 0.0, -3.0, 1.0), R=None, indirect=0.5):
+    c = RtCamera()
+    c.width, c.height, c.focal = width, height, focal
+    c.camera = Vec4(*cam)
+    c.R = R if R is not None else identity16()
+    c.indirect = indirect
+    return c
+
+
+def default_lights():
+    """skeleton.cpp:86-89: one light at (0,-0.5,-0.7), colour 14*(1,1,1)."""
+    arr = (Light * 1)()
+    arr[0].position = Vec4(0.0, -0.5, -0.7, 1.0)
+    f = float(np.float32(14.0) * np.float32(1.0))
+    arr[0].colour = Vec3(f, f, f)
+    return arr
+
+
+def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
+                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2):
+    p = RastParams()
+    p.width, p.height, p.focal = width, height, focal
+    p.camera = Vec4(*cam)
+    p.R = R if R is not None else identity16()
+    p.light_scene = Vec4(*light)
+    f = float(np.float32(20.0) * np.float32(1.0))
+    p.light_power = Vec3(f, f, f)
+    p.indirect_first = indirect_first
+    return p
+
+
+def rt_scene():
+    lib = load()
+    tris = (Tri * 64)()
+    sph = Sphere()
+    n = lib.cg_rt_load_test_model(tris, 64, C.byref(sph))
+    if n < 0:
+        raise RuntimeError(f"cg_rt_load_test_model failed: {n}")
+    return tris, n, sph
+
+
+def rast_scene():
+    lib = load()
+    room, boxes = (RTri * 16)(), (RTri * 32)()
+    nr, nb = C.c_int(), C.c_int()
+    rc = lib.cg_rast_load_test_model(room, 16, C.byref(nr), boxes, 32, C.byref(nb))
+    if rc < 0:
+        raise RuntimeError(f"cg_rast_load_test_model failed: {rc}")
+    return room, nr.value, boxes, nb.value
+
+
+def rast_prepare(params, room=None, nr=None, boxes=None, nb=None):
+    """Host geometry (clip etc.): returns (clipped RTri array, n, light Vec4)."""
+    lib = load()
+    if room is None:
+        room, nr, boxes, nb = rast_scene()
+    light = Vec4()
+    n = lib.cg_rast_prepare(C.byref(params), room, nr, boxes, nb, None, 0, C.byref(light))
+    if n < 0:
+        raise RuntimeError(f"cg_rast_prepare failed: {n}")
+    out = (RTri * max(n, 1))()
+    n = lib.cg_rast_prepare(C.byref(params), room, nr, boxes, nb, out, n, C.byref(light))
+    return out, n, light
+
+
+class Context:
+    """One GPU context (cg_create/cg_destroy)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = P()
+        rc = self.lib.cg_create(device, C.byref(h))
+        if rc != CG_OK:
+            raise RuntimeError(f"cg_create({device}) failed with {rc} (no usable HIP device?)")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cg_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != CG_OK:
+            msg = self.lib.cg_last_error(self.h)
+            raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    # -- RT --
+    def rt_set_scene(self, tris, n, sph=None, n_sph=1):
+        sp = C.byref(sph) if sph is not None else None
+        self._check(self.lib.cg_rt_set_scene(self.h, tris, n, sp, n_sph if sph is not None else 0),
+                    "cg_rt_set_scene")
+
+    def rt_render(self, cam, lights=None, n_lights=None):
+        lights = default_lights() if lights is None else lights
+        n_lights = len(lights) if n_lights is None else n_lights
+        out = np.zeros(cam.width * cam.height, np.uint32)
+        st = Stats()
+        self._check(self.lib.cg_rt_render(self.h, lights, n_lights, C.byref(cam),
+                                          out.ctypes.data_as(P), C.byref(st)), "cg_rt_render")
+        return out, st
+
+    def rt_render_device(self, cam, d_out, shard=None, stream=None, lights=None):
+        lights = default_lights() if lights is None else lights
+        sh = C.byref(shard) if shard is not None else None
+        self._check(self.lib.cg_rt_render_device(self.h, lights, len(lights), C.byref(cam), sh,
+                                                 P(d_out), P(stream) if stream else None),
+                    "cg_rt_render_device")
+
+    def rt_unstripe_device(self, d_gathered, width, height, nranks, stripe_h, d_frame, stream=None):
+        self._check(self.lib.cg_rt_unstripe_device(self.h, P(d_gathered), width, height, nranks,
+                                                   stripe_h, P(d_frame), P(stream) if stream else None),
+                    "cg_rt_unstripe_device")
+
+    def rt_probe_closest(self, starts, dirs):
+        n = len(starts)
+        S, D = (Vec4 * n)(*[Vec4(*s) for s in starts]), (Vec4 * n)(*[Vec4(*d) for d in dirs])
+        out, hit = (Isect * n)(), (C.c_int * n)()
+        self._check(self.lib.cg_rt_probe_closest(self.h, S, D, n, out, hit), "cg_rt_probe_closest")
+        return out, list(hit)
+
+    def rt_probe_direct_light(self, isects, light):
+        n = len(isects)
+        arr = (Isect * n)(*isects)
+        out = (Vec3 * n)()
+        self._check(self.lib.cg_rt_probe_direct_light(self.h, arr, C.byref(light), n, out),
+                    "cg_rt_probe_direct_light")
+        return out
+
+    # -- RAST --
+    def rast_render(self, tris, n, params, light, want_depth=True, want_shadow=True):
+        npx = params.width * params.height
+        argb = np.zeros(npx, np.uint32)
+        depth = np.zeros(npx, np.float32) if want_depth else None
+        shadow = np.zeros(npx, np.int32) if want_shadow else None
+        st = Stats()
+        self._check(self.lib.cg_rast_render(
+            self.h, tris, n, C.byref(params), light, argb.ctypes.data_as(P),
+            depth.ctypes.data_as(P) if depth is not None else None,
+            shadow.ctypes.data_as(P) if shadow is not None else None, C.byref(st)), "cg_rast_render")
+        return argb, depth, shadow, st
+
+    def rast_render_device(self, d_tris, n, params, light, d_argb, d_depth=None, d_shadow=None,
+                           stream=None):
+        self._check(self.lib.cg_rast_render_device(
+            self.h, P(d_tris), n, C.byref(params), light, P(d_argb),
+            P(d_depth) if d_depth else None, P(d_shadow) if d_shadow else None,
+            P(stream) if stream else None), "cg_rast_render_device")

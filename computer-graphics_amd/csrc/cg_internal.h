@@ -1,0 +1,77 @@
+// cg_internal.h -- device-side data layouts shared by the shim and kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cg_render.h"
+#include "cg_math.h"
+
+namespace cg {
+
+constexpr int kMaxLights = 8;
+constexpr int kRtTileW = 32;   // RT workgroup: 4 waves, each an 8x8 pixel tile
+constexpr int kRtTileH = 8;
+constexpr int kRtThreads = 256;
+
+// Per-frame, per-triangle constants of ClosestIntersection for rays that
+// start at the camera (skeleton.cpp:279-306).  Every field is computed with
+// exactly the reference's float ops, so reusing it across rays is exact:
+//   e1 = v1 - v0, e2 = v2 - v0 (:283-284), s = cameraPos - v0 (:296-297),
+//   K1 = e1.y*e2.z - e2.y*e1.z   (first cofactor of det(-d, e1, e2))
+//   K2 = s.y*e2.z - e2.y*s.z     (first cofactor of det(-d, s, e2))
+//   K3 = e1.y*s.z - s.y*e1.z     (first cofactor of det(-d, e1, s))
+//   detT = det(s, e1, e2) = (s.x*K1 - e1.x*K2) + e2.x*(s.y*e1.z - e1.y*s.z)
+// 64 B per triangle: one s_load_dwordx16 per loop iteration.
+struct alignas(16) RtTri {
+    float e1x, e1y, e1z, e2x, e2y, e2z;
+    float sx, sy, sz, detT;
+    float K1, K2, K3;
+    float v0x, v0y, v0z;
+};
+static_assert(sizeof(RtTri) == 64, "RtTri must be 64 B");
+
+// Shading attributes, read only on a hit.
+struct alignas(16) RtShade {
+    float nx, ny, nz, nw;   // Triangle::normal (w = 1)
+    float cr, cg, cb, pad;  // Triangle::color
+};
+
+struct RtSphere {
+    float cx, cy, cz, r2;   // centre, radiusSquared
+    float cr, cg, cb, pad;  // color
+};
+
+// Frame arguments, passed by value (kernarg -> SGPRs).
+struct RtFrame {
+    int W, H;
+    float focal, indirect;
+    float cam[4];
+    float R[16];
+    int n_tris, n_sph, n_lights;
+    int rank, nranks, stripe_h, rows_out;
+    float lpos[kMaxLights][4];
+    float lcol[kMaxLights][3];
+};
+
+// ---- RAST --------------------------------------------------------------
+constexpr int kRastMaxH = 8192;
+
+// Row span of one triangle (output of ComputePolygonRows, skeleton.cpp:433-498),
+// already reduced to what Interpolate (:524-551) needs for DrawPolygonRows:
+//   x_i = lx + i, zinv_i = lz + sz*i, X_i = (lX + sX*i)/zinv_i, Y_i likewise,
+//   shaded for i in [0, rx - lx).
+struct alignas(16) RastSpan {
+    int lx, rx;
+    float lz, sz;      // left zinv, step_z
+    float lX, sX;      // left pos3d.x * zinv, step
+    float lY, sY;
+};
+
+struct RastTriHdr {
+    int ymin, rows;      // rows of this triangle (VertexShader y's), span base offset below
+    int span0;           // first span index in the span array
+    int pad;
+};
+
+}  // namespace cg

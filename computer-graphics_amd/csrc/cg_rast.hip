@@ -1,0 +1,461 @@
+// cg_rast.hip -- rasteriser fill + post-pass for gfx950 (MI355X).
+//
+// Reference: rasteriser/Source/skeleton.cpp, texture mode 0 / colour mode 0.
+// Four launches per frame, all order-exact (no atomics touch colour/depth):
+//   1. rast_setup_kernel   (one workgroup per clipped triangle)
+//        VertexShader (:510-522) x3, then ComputePolygonRows (:433-498):
+//        every edge sample of Interpolate (:524-551) is reduced into its row
+//        with a 64-bit LDS min/max whose key is (x, sample sequence), which
+//        reproduces the reference's `<=` / `>=` "later sample wins ties"
+//        updates exactly; each visible row becomes a RastSpan holding what
+//        DrawPolygonRows' Interpolate needs.
+//   2. rast_rowlist_kernel (one wave per screen row)
+//        ordered list of the triangles whose spans cover the row (ballot +
+//        popcount compaction, triangle order preserved).
+//   3. rast_fill_kernel    (one wave per 64-pixel row segment)
+//        walks its row's list in triangle order -- the reference's ordered
+//        z-buffer (`>=` for colour, `>` for shadow marks, :574/:668) with
+//        depth/shadow/shade state held in registers; PixelShader +
+//        calculateIllumination (:559-586, :664-688).
+//   4. rast_post_kernel    (one thread per pixel)
+//        the in-place raster-order post-pass (:283-307): a pixel's up/left
+//        neighbours are seen darkened and down/right ones not, which is
+//        recomputed per pixel from the shadow buffer, then antiAliasing
+//        (:1736-1753) and PutPixelSDL.  Border pixels stay 0x00000000.
+#include <float.h>
+#include <limits.h>
+
+#include "cg_internal.h"
+
+namespace cg {
+
+void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e);
+int ctx_fail(cg_ctx *c, hipError_t e, const char *what);
+void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b);
+
+constexpr int kSetupThreads = 256;
+constexpr int kRastMaxRows = 4096;   // LDS rows per triangle in span setup (H <= 4096)
+
+struct RastArgs {
+    int W, H, n;
+    float focal;
+    float light[3];
+    float lp[3];            // lightPower
+    float ind_first;        // indirectLightPowerPerArea at frame start
+    int want_first;         // ind_first differs from the steady-state 0.2
+};
+
+struct RastHdr {
+    int ylo, yhi;           // visible rows [ylo, yhi] (ylo > yhi: none)
+    int fy, fx;             // first shadeable fragment (if want_first), fy = INT_MAX none
+};
+
+struct Pix {                // rasteriser Pixel (:88-94) minus w
+    int x, y;
+    float zinv, X, Y;
+};
+
+__device__ __forceinline__ Pix vertex_shader(const RastArgs &A, cg_vec4 v)
+{
+    // :512-521
+    float x = (A.focal * (v.x / v.z)) + (float)(A.W / 2);
+    float y = (A.focal * (v.y / v.z)) + (float)(A.H / 2);
+    Pix p;
+    p.x = f2i_x86(x);
+    p.y = f2i_x86(y);
+    p.zinv = 1 / v.z;
+    p.X = v.x;
+    p.Y = v.y;
+    return p;
+}
+
+// Interpolate (:524-551) prepared for one edge a -> b with N samples.
+struct Edge {
+    float ax, ay, az, aX, aY;     // a.x, a.y as float; a.zinv; a.pos3d.xy * a.zinv
+    float stx, sty, stz, sX, sY;
+    int n;
+};
+
+__device__ __forceinline__ Edge make_edge(Pix a, Pix b)
+{
+    Edge e;
+    float aX = a.X * a.zinv, aY = a.Y * a.zinv;   // :526-527
+    float bX = b.X * b.zinv, bY = b.Y * b.zinv;   // :529-530
+    int dx = a.x - b.x, dy = a.y - b.y;
+    dx = dx < 0 ? -dx : dx;
+    dy = dy < 0 ? -dy : dy;
+    e.n = (dx > dy ? dx : dy) + 1;                // :473-475
+    float den = (float)(e.n - 1 > 1 ? e.n - 1 : 1);
+    e.ax = (float)a.x;
+    e.ay = (float)a.y;
+    e.az = a.zinv;
+    e.aX = aX;
+    e.aY = aY;
+    e.stx = (float)(b.x - a.x) / den;             // :533-538
+    e.sty = (float)(b.y - a.y) / den;
+    e.stz = (b.zinv - a.zinv) / den;
+    e.sX = (bX - aX) / den;
+    e.sY = (bY - aY) / den;
+    return e;
+}
+
+__device__ __forceinline__ int edge_x(const Edge &e, int j) { return f2i_x86(floorf(e.ax + (e.stx * (float)j))); }
+__device__ __forceinline__ int edge_y(const Edge &e, int j) { return f2i_x86(floorf(e.ay + (e.sty * (float)j))); }
+
+// sample j's zinv and pos3d.xy (:543-548)
+__device__ __forceinline__ void edge_attr(const Edge &e, int j, float &zinv, float &X, float &Y)
+{
+    float fj = (float)j;
+    zinv = e.az + (e.stz * fj);
+    X = (e.aX + (e.sX * fj)) / zinv;
+    Y = (e.aY + (e.sY * fj)) / zinv;
+}
+
+__device__ __forceinline__ unsigned long long key_left(int x, unsigned seq)
+{
+    return ((unsigned long long)((unsigned)x ^ 0x80000000u) << 32) | (unsigned long long)(~seq);
+}
+__device__ __forceinline__ unsigned long long key_right(int x, unsigned seq)
+{
+    return ((unsigned long long)((unsigned)x ^ 0x80000000u) << 32) | (unsigned long long)seq;
+}
+
+__global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
+    const cg_rtri *__restrict__ tris, RastArgs A, RastSpan *__restrict__ spans,
+    RastHdr *__restrict__ hdr, int *__restrict__ first_tri)
+{
+    __shared__ unsigned long long lkey[kRastMaxRows];
+    __shared__ unsigned long long rkey[kRastMaxRows];
+    __shared__ unsigned long long fkey;
+    const int t = blockIdx.x;
+    const cg_rtri T = tris[t];
+    Pix vp[3] = {vertex_shader(A, T.v0), vertex_shader(A, T.v1), vertex_shader(A, T.v2)};
+    int mx = -INT_MAX, mn = INT_MAX;                        // :434-447
+    for (int i = 0; i < 3; ++i) {
+        if (vp[i].y > mx) mx = vp[i].y;
+        if (vp[i].y < mn) mn = vp[i].y;
+    }
+    long long rows = (long long)mx - (long long)mn + 1;     // :448
+    int ylo = mn > 0 ? mn : 0;
+    int yhi = mx < A.H - 1 ? mx : A.H - 1;
+    RastHdr h;
+    h.ylo = ylo;
+    h.yhi = yhi;
+    h.fy = INT_MAX;
+    h.fx = INT_MAX;
+    if (rows <= 0 || ylo > yhi) {
+        if (threadIdx.x == 0) {
+            h.ylo = 1;
+            h.yhi = 0;
+            hdr[t] = h;
+        }
+        return;
+    }
+    const int nv = yhi - ylo + 1;
+    for (int k = threadIdx.x; k < nv; k += kSetupThreads) {
+        lkey[k] = ~0ull;
+        rkey[k] = 0ull;
+    }
+    if (threadIdx.x == 0) fkey = ~0ull;
+    __syncthreads();
+    // Edge samples -> rows (:466-497).  Rows outside the screen never shade.
+    for (int ei = 0; ei < 3; ++ei) {
+        Edge e = make_edge(vp[ei], vp[ei == 2 ? 0 : ei + 1]);
+        for (int j = threadIdx.x; j < e.n; j += kSetupThreads) {
+            int y = edge_y(e, j);
+            if (y < ylo || y > yhi) continue;               // also covers :485's y - min >= 0
+            int x = edge_x(e, j);
+            unsigned seq = ((unsigned)ei << 30) | (unsigned)j;
+            atomicMin(&lkey[y - ylo], key_left(x, seq));
+            atomicMax(&rkey[y - ylo], key_right(x, seq));
+        }
+    }
+    __syncthreads();
+    const bool shade_tri = A.want_first && T.color.x >= 0;
+    for (int k = threadIdx.x; k < nv; k += kSetupThreads) {
+        RastSpan s;
+        unsigned long long lk = lkey[k], rk = rkey[k];
+        if (lk == ~0ull) {                                  // untouched row: shades nothing
+            s.lx = 1; s.rx = 0;
+            s.lz = s.sz = s.lX = s.sX = s.lY = s.sY = 0.f;
+        } else {
+            unsigned ls = ~(unsigned)(lk & 0xffffffffu), rs = (unsigned)(rk & 0xffffffffu);
+            int le = (int)(ls >> 30), lj = (int)(ls & 0x3fffffffu);
+            int re = (int)(rs >> 30), rj = (int)(rs & 0x3fffffffu);
+            Edge el = make_edge(vp[le], vp[le == 2 ? 0 : le + 1]);
+            Edge er = make_edge(vp[re], vp[re == 2 ? 0 : re + 1]);
+            int lx = edge_x(el, lj), rx = edge_x(er, rj);
+            float lz, lX, lY, rz, rX, rY;
+            edge_attr(el, lj, lz, lX, lY);
+            edge_attr(er, rj, rz, rX, rY);
+            // DrawPolygonRows' Interpolate(left, right, N = rx - lx + 1) (:502-503, :524-538)
+            long long span = (long long)rx - (long long)lx;
+            if (span < 0 || span > (1 << 24)) {              // reference would not survive this row
+                s.lx = 1; s.rx = 0;
+                s.lz = s.sz = s.lX = s.sX = s.lY = s.sY = 0.f;
+            } else {
+                int N = (int)span + 1;
+                float den = (float)(N - 1 > 1 ? N - 1 : 1);
+                float aX = lX * lz, aY = lY * lz, bX = rX * rz, bY = rY * rz;
+                s.lx = lx;
+                s.rx = rx;
+                s.lz = lz;
+                s.sz = (rz - lz) / den;
+                s.lX = aX;
+                s.sX = (bX - aX) / den;
+                s.lY = aY;
+                s.sY = (bY - aY) / den;
+                if (shade_tri) {
+                    // first fragment of this row that PixelShader would shade on an empty z-buffer
+                    int y = ylo + k;
+                    for (int i = 0; i < N - 1; ++i) {
+                        int x = lx + i;
+                        if (x >= A.W) break;
+                        if (x < 0) continue;
+                        float zi = s.lz + (s.sz * (float)i);
+                        if (zi >= 0.0f) {
+                            atomicMin(&fkey, ((unsigned long long)(unsigned)y << 32) | (unsigned)x);
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        spans[(size_t)t * A.H + ylo + k] = s;
+    }
+    if (shade_tri) {
+        __syncthreads();
+        if (threadIdx.x == 0 && fkey != ~0ull) {
+            h.fy = (int)(fkey >> 32);
+            h.fx = (int)(fkey & 0xffffffffu);
+            atomicMin(first_tri, t);
+        }
+    }
+    if (threadIdx.x == 0) hdr[t] = h;
+}
+
+// Ordered per-row triangle lists (one wave per row).
+__global__ __launch_bounds__(256) void rast_rowlist_kernel(const RastHdr *__restrict__ hdr, int n,
+                                                          int H, int *__restrict__ list,
+                                                          int *__restrict__ count)
+{
+    const int y = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (y >= H) return;
+    int c = 0;
+    for (int base = 0; base < n; base += 64) {
+        int t = base + lane;
+        bool cov = false;
+        if (t < n) {
+            RastHdr h = hdr[t];
+            cov = h.ylo <= y && y <= h.yhi;
+        }
+        unsigned long long m = __ballot(cov);
+        unsigned long long below = lane ? (m & ((1ull << lane) - 1)) : 0ull;
+        if (cov) list[(size_t)y * n + c + __popcll(below)] = t;
+        c += __popcll(m);
+    }
+    if (lane == 0) count[y] = c;
+}
+
+// calculateIllumination's direct term D (:674-683); the post-pass rebuilds
+// screen/low/high = colour * (D + indirect) from it with the same ops.
+__device__ __forceinline__ vec3 illum_D(const RastArgs &A, float zinv, float X, float Y, vec3 N)
+{
+    // Interpolate pos3d (:546-548)
+    float pz = 1 / zinv;
+    float px = X / zinv;
+    float py = Y / zinv;
+    vec3 r = v3(A.light[0] - px, A.light[1] - py, A.light[2] - pz);               // :675
+    double a = (double)r.x * (double)r.x, b = (double)r.y * (double)r.y,
+           c = (double)r.z * (double)r.z;
+    float r2 = (float)((a + b) + c);                                              // :677
+    float vp = dot(r, N);                                                         // :681
+    float m = gmax(vp, 0.0f);
+    float area = (float)((double)4.0f * M_PI * (double)r2);                       // :682
+    return v3((A.lp[0] * m) / area, (A.lp[1] * m) / area, (A.lp[2] * m) / area);
+}
+
+// Per-pixel shade state between fill and post: .x = triangle index (as bits;
+// -1 none; bit 30 = shaded by the frame's first fragment), .yzw = D.
+__global__ __launch_bounds__(256) void rast_fill_kernel(
+    const cg_rtri *__restrict__ tris, RastArgs A, const RastSpan *__restrict__ spans,
+    const RastHdr *__restrict__ hdr, const int *__restrict__ list, const int *__restrict__ count,
+    const int *__restrict__ first_tri, float4 *__restrict__ state, float *__restrict__ depth_out,
+    int32_t *__restrict__ shadow_out)
+{
+    const int segs = (A.W + 63) >> 6;
+    const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int y = seg / segs;
+    if (y >= A.H) return;
+    const int x0 = (seg - y * segs) * 64;
+    const int x = x0 + lane;
+    const int ft = A.want_first ? *first_tri : INT_MAX;
+    float depth = 0.0f;                                    // :247
+    int shadow = 0;                                        // :259
+    int tri = -1;
+    vec3 D = v3(0.f, 0.f, 0.f);
+    const int cnt = count[y];
+    const int *lst = list + (size_t)y * A.n;
+    for (int q = 0; q < cnt; ++q) {
+        const int t = lst[q];
+        const RastSpan s = spans[(size_t)t * A.H + y];
+        if (s.rx - 1 < x0 || s.lx > x0 + 63) continue;    // no fragment in this segment
+        const int i = x - s.lx;
+        if (!(x < A.W && i >= 0 && x < s.rx)) continue;   // :504, :573
+        const float zinv = s.lz + (s.sz * (float)i);      // :543
+        const cg_rtri T = tris[t];
+        if (T.color.x >= 0) {
+            if (zinv >= depth) {                          // :574
+                float X = s.lX + (s.sX * (float)i);
+                float Y = s.lY + (s.sY * (float)i);
+                D = illum_D(A, zinv, X, Y, v3(T.normal.x, T.normal.y, T.normal.z));
+                tri = t;
+                if (t == ft) {
+                    RastHdr h = hdr[t];
+                    if (h.fy == y && h.fx == x) tri |= 1 << 30;
+                }
+                depth = zinv;                             // :665
+            }
+        } else if (zinv > depth) {                        // :668-669
+            shadow = 1;
+        }
+    }
+    if (x < A.W) {
+        size_t o = (size_t)y * A.W + x;
+        state[o] = make_float4(__int_as_float(tri), D.x, D.y, D.z);
+        if (depth_out) depth_out[o] = depth;
+        shadow_out[o] = shadow;
+    }
+}
+
+// shade buffers of one pixel, as they stand after the fill.
+__device__ __forceinline__ void shade3(const cg_rtri *__restrict__ tris, const RastArgs &A, float4 st,
+                                       vec3 &sc, vec3 &lo, vec3 &hi)
+{
+    int tb = __float_as_int(st.x);
+    if (tb < 0) {
+        sc = lo = hi = v3(0.f, 0.f, 0.f);
+        return;
+    }
+    int t = tb & ~(1 << 30);
+    float ind = (tb & (1 << 30)) ? A.ind_first : 0.2f * 1;
+    cg_rtri T = tris[t];
+    vec3 c = v3(T.color.x, T.color.y, T.color.z);
+    vec3 D = v3(st.y, st.z, st.w);
+    sc = c * (D + v3(ind, ind, ind));                      // :580
+    lo = c * (D + v3(0.0f * 1, 0.0f * 1, 0.0f * 1));       // :582
+    hi = c * (D + v3(0.4f * 1, 0.4f * 1, 0.4f * 1));       // :584
+}
+
+// soft-shadow darkening amount for interior pixel o, 0 if not shadowed (:286-303, :1725-1733)
+__device__ __forceinline__ float darken(const int32_t *__restrict__ sh, int W, size_t o)
+{
+    if (sh[o] != 1) return 0.0f;
+    int k = sh[o] + sh[o - W] + sh[o - W - 1] + sh[o - W + 1] + sh[o + W - 1] + sh[o + W] +
+            sh[o + W - 1] + sh[o - 1] + sh[o + 1];
+    float val = (float)k;
+    val /= 9.0f;
+    if ((double)val < 0.6) return 0.05f;
+    if ((double)val < 0.7) return 0.08f;
+    if ((double)val < 0.8) return 0.1f;
+    if ((double)val < 0.9) return 0.12f;
+    return 0.3f;
+}
+
+__global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
+                                                       const float4 *__restrict__ state,
+                                                       const int32_t *__restrict__ sh,
+                                                       uint32_t *__restrict__ argb)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= A.W || y >= A.H) return;
+    const int W = A.W;
+    const size_t o = (size_t)y * W + x;
+    if (x < 1 || y < 1 || x >= W - 1 || y >= A.H - 1) {   // :283-284 border never written
+        argb[o] = 0u;
+        return;
+    }
+    vec3 s[5], l[5], h[5];
+    const size_t taps[5] = {o, o - W, o + W, o - 1, o + 1};   // centre, up, down, left, right
+#pragma unroll
+    for (int k = 0; k < 5; ++k) shade3(tris, A, state[taps[k]], s[k], l[k], h[k]);
+    // darkened before the AA of this pixel: itself, the pixel above and the one
+    // to the left (both interior-only, raster order)
+    float d0 = darken(sh, W, o);
+    float dU = (y - 1 >= 1) ? darken(sh, W, o - W) : 0.0f;
+    float dL = (x - 1 >= 1) ? darken(sh, W, o - 1) : 0.0f;
+    if (sh[o] == 1) s[0] = s[0] - v3(d0, d0, d0);
+    if (y - 1 >= 1 && sh[o - W] == 1) s[1] = s[1] - v3(dU, dU, dU);
+    if (x - 1 >= 1 && sh[o - 1] == 1) s[3] = s[3] - v3(dL, dL, dL);
+    // antiAliasing (:1741-1750)
+    vec3 val = ((((s[0] + s[1]) + s[2]) + s[3]) + s[4]) / 5.0f;
+    vec3 val1 = ((((l[0] + l[1]) + l[2]) + l[3]) + l[4]) / 5.0f;
+    vec3 val2 = ((((h[0] + h[1]) + h[2]) + h[3]) + h[4]) / 5.0f;
+    val = ((val + val1) + val2) / 3.0f;
+    argb[o] = put_pixel(val);
+}
+
+int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_params *p, cg_vec4 light,
+                       uint32_t *d_argb, float *d_depth, int32_t *d_shadow, hipStream_t st,
+                       cg_stats *stats)
+{
+    if (p->width <= 2 || p->height <= 2 || p->height > kRastMaxRows) return CG_E_INVALID;
+    const int W = p->width, H = p->height;
+    const size_t npx = (size_t)W * H;
+    const int nn = n > 0 ? n : 1;
+    hipError_t e;
+    RastSpan *spans = (RastSpan *)ctx_buf(c, 2, (size_t)nn * H * sizeof(RastSpan), &e);
+    if (!spans) return ctx_fail(c, e, "alloc spans");
+    RastHdr *hdr = (RastHdr *)ctx_buf(c, 1, (size_t)nn * sizeof(RastHdr), &e);
+    if (!hdr) return ctx_fail(c, e, "alloc hdr");
+    float4 *state = (float4 *)ctx_buf(c, 3, npx * sizeof(float4), &e);
+    if (!state) return ctx_fail(c, e, "alloc state");
+    // count[H] | first_tri | list[H*n]
+    int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16 + (size_t)H * nn) * sizeof(int), &e);
+    if (!misc) return ctx_fail(c, e, "alloc lists");
+    int *count = misc, *first_tri = misc + H, *list = misc + H + 16;
+    int32_t *shadow = d_shadow;
+    if (!shadow) {
+        shadow = (int32_t *)ctx_buf(c, 6, npx * sizeof(int32_t), &e);
+        if (!shadow) return ctx_fail(c, e, "alloc shadow");
+    }
+    RastArgs A;
+    A.W = W;
+    A.H = H;
+    A.n = n;
+    A.focal = p->focal;
+    A.light[0] = light.x; A.light[1] = light.y; A.light[2] = light.z;
+    A.lp[0] = p->light_power.x; A.lp[1] = p->light_power.y; A.lp[2] = p->light_power.z;
+    A.ind_first = p->indirect_first;
+    A.want_first = p->indirect_first != 0.2f * 1;
+    hipEvent_t e0, e1;
+    ctx_events(c, &e0, &e1);
+    if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
+    if (A.want_first && (e = hipMemsetAsync(first_tri, 0x7f, sizeof(int), st)) != hipSuccess)
+        return ctx_fail(c, e, "memset");
+    if (n > 0) {
+        hipLaunchKernelGGL(rast_setup_kernel, dim3(n), dim3(kSetupThreads), 0, st, d_tris, A, spans,
+                           hdr, first_tri);
+        if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
+    }
+    hipLaunchKernelGGL(rast_rowlist_kernel, dim3((H + 3) / 4), dim3(256), 0, st, hdr, n, H, list, count);
+    if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rowlist launch");
+    const int segs = (W + 63) / 64;
+    hipLaunchKernelGGL(rast_fill_kernel, dim3((segs * H + 3) / 4), dim3(256), 0, st, d_tris, A, spans,
+                       hdr, list, count, first_tri, state, d_depth, shadow);
+    if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
+    hipLaunchKernelGGL(rast_post_kernel, dim3(segs, (H + 3) / 4), dim3(256), 0, st, d_tris, A, state,
+                       shadow, d_argb);
+    if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");
+    if (stats && (e = hipEventRecord(e1, st)) != hipSuccess) return ctx_fail(c, e, "event");
+    if (stats) {
+        stats->n_tris = n;
+        stats->n_spans = 0;
+    }
+    return CG_OK;
+}
+
+}  // namespace cg

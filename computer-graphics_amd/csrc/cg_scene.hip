@@ -1,0 +1,144 @@
+// cg_scene.hip -- LoadTestModel for both hot paths (host code).
+//   raytracer/Source/TestModelH.h:121-279  (28 triangles + 1 sphere)
+//   rasteriser/Source/TestModelH.h:48-312  (room 10 + boxes 20, setting = settingBoxes = 0)
+// Vertex scaling and normals use the reference's float ops exactly.
+#include <cstring>
+
+#include "cg_internal.h"
+
+using namespace cg;
+
+namespace {
+
+struct P4 { float x, y, z, w; };
+
+// Triangle::ComputeNormal (both TestModelH.h files)
+template <class T>
+void compute_normal(T &t)
+{
+    vec3 e1 = v3(t.v1.x - t.v0.x, t.v1.y - t.v0.y, t.v1.z - t.v0.z);
+    vec3 e2 = v3(t.v2.x - t.v0.x, t.v2.y - t.v0.y, t.v2.z - t.v0.z);
+    vec3 n = normalize(cross(e2, e1));
+    t.normal = cg_vec4{n.x, n.y, n.z, 1.0f};
+}
+
+// `v *= 2/L; v -= (1,1,1,1); v.x *= -1; v.y *= -1; v.w = 1` (RT :246-269, RAST :266-310)
+cg_vec4 scale_vertex(cg_vec4 v, float L)
+{
+    float s = 2 / L;
+    vec4 r = v4(v.x, v.y, v.z, v.w) * s;
+    r = r - v4(1, 1, 1, 1);
+    r.x *= -1;
+    r.y *= -1;
+    r.w = 1.0f;
+    return cg_vec4{r.x, r.y, r.z, r.w};
+}
+
+struct Box { cg_vec4 A, B, C, D, E, F, G, H; };
+
+Box box(float ax, float az, float bx, float bz, float cx, float cz, float dx, float dz, float h)
+{
+    Box b;
+    b.A = cg_vec4{ax, 0, az, 1}; b.B = cg_vec4{bx, 0, bz, 1};
+    b.C = cg_vec4{cx, 0, cz, 1}; b.D = cg_vec4{dx, 0, dz, 1};
+    b.E = cg_vec4{ax, h, az, 1}; b.F = cg_vec4{bx, h, bz, 1};
+    b.G = cg_vec4{cx, h, cz, 1}; b.H = cg_vec4{dx, h, dz, 1};
+    return b;
+}
+
+const cg_vec3 kRed{0.75f, 0.15f, 0.15f}, kYellow{0.75f, 0.75f, 0.15f}, kGreen{0.15f, 0.75f, 0.15f},
+    kCyan{0.15f, 0.75f, 0.75f}, kBlue{0.15f, 0.15f, 0.75f}, kPurple{0.75f, 0.15f, 0.75f},
+    kWhite{0.75f, 0.75f, 0.75f};
+
+}  // namespace
+
+extern "C" int cg_rt_load_test_model(cg_tri *tris, int cap, cg_sphere *sphere)
+{
+    if (!tris || cap < 28) return CG_E_CAPACITY;
+    const float L = 555;
+    int n = 0;
+    auto add = [&](cg_vec4 a, cg_vec4 b, cg_vec4 c, cg_vec3 col) {
+        cg_tri &t = tris[n++];
+        t.v0 = a; t.v1 = b; t.v2 = c; t.color = col;
+        compute_normal(t);
+    };
+    Box r = box(L, 0, 0, 0, L, L, 0, L, L);   // room corners A..H (TestModelH.h:145-153)
+    add(r.C, r.B, r.A, kGreen);  add(r.C, r.D, r.B, kGreen);     // floor
+    add(r.A, r.E, r.C, kPurple); add(r.C, r.E, r.G, kPurple);    // left wall
+    add(r.F, r.B, r.D, kYellow); add(r.H, r.F, r.D, kYellow);    // right wall
+    add(r.E, r.F, r.G, kCyan);   add(r.F, r.H, r.G, kCyan);      // ceiling
+    add(r.G, r.D, r.C, kWhite);  add(r.G, r.H, r.D, kWhite);     // back wall
+    Box s = box(290, 114, 130, 65, 240, 272, 82, 225, 165);      // short block (:178-206)
+    add(s.E, s.B, s.A, kRed); add(s.E, s.F, s.B, kRed);
+    add(s.F, s.D, s.B, kRed); add(s.F, s.H, s.D, kRed);
+    add(s.H, s.C, s.D, kRed); add(s.H, s.G, s.C, kRed);
+    add(s.G, s.E, s.C, kRed); add(s.E, s.A, s.C, kRed);
+    add(s.G, s.F, s.E, kRed); add(s.G, s.H, s.F, kRed);
+    Box t = box(423, 247, 265, 296, 472, 406, 314, 456, 330);    // tall block (:212-240), no back face
+    add(t.E, t.B, t.A, kBlue); add(t.E, t.F, t.B, kBlue);
+    add(t.F, t.D, t.B, kBlue); add(t.F, t.H, t.D, kBlue);
+    add(t.G, t.E, t.C, kBlue); add(t.E, t.A, t.C, kBlue);
+    add(t.G, t.F, t.E, kBlue); add(t.G, t.H, t.F, kBlue);
+    for (int i = 0; i < n; ++i) {
+        tris[i].v0 = scale_vertex(tris[i].v0, L);
+        tris[i].v1 = scale_vertex(tris[i].v1, L);
+        tris[i].v2 = scale_vertex(tris[i].v2, L);
+        compute_normal(tris[i]);
+    }
+    if (sphere) {                                                // :275-277, Sphere ctor :17-18
+        float rad = 0.3f;
+        sphere->radius = rad;
+        sphere->radiusSquared = rad * rad;
+        sphere->centre = cg_vec3{-0.45f, 0.6f, -0.6f};
+        sphere->color = kWhite;
+        sphere->normal = cg_vec3{0, 0, 0};
+    }
+    return n;
+}
+
+extern "C" int cg_rast_load_test_model(cg_rtri *room, int room_cap, int *n_room, cg_rtri *boxes,
+                                       int boxes_cap, int *n_boxes)
+{
+    if (!room || !boxes || !n_room || !n_boxes || room_cap < 10 || boxes_cap < 20) return CG_E_CAPACITY;
+    const float L = 555;
+    int nr = 0, nb = 0;
+    auto add = [&](cg_rtri *arr, int &n, cg_vec4 a, cg_vec4 b, cg_vec4 c, cg_vec3 col, int index) {
+        cg_rtri &t = arr[n++];
+        t.v0 = a; t.v1 = b; t.v2 = c; t.color = col;
+        t.texture = 0;                                           // setting = settingBoxes = 0
+        t.index = index;
+        compute_normal(t);
+    };
+    const cg_vec3 back{0.03529f, 0.7843f, 0.8078f};
+    Box r = box(L, 0, 0, 0, L, L, 0, L, L);
+    add(room, nr, r.C, r.B, r.A, kGreen, 2);  add(room, nr, r.C, r.D, r.B, kGreen, 2);
+    add(room, nr, r.A, r.E, r.C, kPurple, 3); add(room, nr, r.C, r.E, r.G, kPurple, 3);
+    add(room, nr, r.F, r.B, r.D, kYellow, 4); add(room, nr, r.H, r.F, r.D, kYellow, 4);
+    add(room, nr, r.E, r.F, r.G, kCyan, 1);   add(room, nr, r.F, r.H, r.G, kCyan, 1);
+    add(room, nr, r.G, r.D, r.C, back, 0);    add(room, nr, r.G, r.H, r.D, back, 0);
+    Box s = box(290, 114, 130, 65, 240, 272, 82, 225, 165);
+    add(boxes, nb, s.E, s.B, s.A, kRed, 0); add(boxes, nb, s.E, s.F, s.B, kRed, 0);
+    add(boxes, nb, s.F, s.D, s.B, kRed, 4); add(boxes, nb, s.F, s.H, s.D, kRed, 4);
+    add(boxes, nb, s.H, s.C, s.D, kRed, 0); add(boxes, nb, s.H, s.G, s.C, kRed, 0);
+    add(boxes, nb, s.G, s.E, s.C, kRed, 3); add(boxes, nb, s.E, s.A, s.C, kRed, 3);
+    add(boxes, nb, s.G, s.F, s.E, kRed, 1); add(boxes, nb, s.G, s.H, s.F, kRed, 1);
+    Box t = box(423, 247, 265, 296, 472, 406, 314, 456, 330);    // tall block incl. back face
+    add(boxes, nb, t.E, t.B, t.A, kBlue, 0); add(boxes, nb, t.E, t.F, t.B, kBlue, 0);
+    add(boxes, nb, t.F, t.D, t.B, kBlue, 4); add(boxes, nb, t.F, t.H, t.D, kBlue, 4);
+    add(boxes, nb, t.H, t.C, t.D, kBlue, 0); add(boxes, nb, t.H, t.G, t.C, kBlue, 0);
+    add(boxes, nb, t.G, t.E, t.C, kBlue, 3); add(boxes, nb, t.E, t.A, t.C, kBlue, 3);
+    add(boxes, nb, t.G, t.F, t.E, kBlue, 1); add(boxes, nb, t.G, t.H, t.F, kBlue, -1); // :256 uninitialised
+    for (int pass = 0; pass < 2; ++pass) {
+        cg_rtri *arr = pass ? boxes : room;
+        int n = pass ? nb : nr;
+        for (int i = 0; i < n; ++i) {
+            arr[i].v0 = scale_vertex(arr[i].v0, L);
+            arr[i].v1 = scale_vertex(arr[i].v1, L);
+            arr[i].v2 = scale_vertex(arr[i].v2, L);
+            compute_normal(arr[i]);
+        }
+    }
+    *n_room = nr;
+    *n_boxes = nb;
+    return nr + nb;
+}

@@ -1,0 +1,404 @@
+// cg_shim.hip -- the extern "C" boundary (include/cg_render.h): context,
+// device-resident scene, launches, error mapping.  Nothing here throws
+// across the ABI; HIP failures become CG_E_HIP with the HIP message kept in
+// the context for cg_last_error().
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cg_internal.h"
+
+namespace cg {
+hipError_t launch_rt_prepare(const cg_tri *, int, const float *, RtTri *, RtShade *, hipStream_t);
+hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
+                            uint32_t *, hipStream_t);
+hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, uint32_t *, hipStream_t);
+hipError_t launch_rt_probe_closest(const RtFrame &, const cg_tri *, const RtSphere *,
+                                   const cg_vec4 *, const cg_vec4 *, int, cg_isect *, int *,
+                                   hipStream_t);
+hipError_t launch_rt_probe_direct_light(const RtFrame &, const RtTri *, const RtShade *,
+                                        const RtSphere *, const cg_isect *, int, cg_vec3 *,
+                                        hipStream_t);
+int rast_render_device(cg_ctx *ctx, const cg_rtri *d_tris, int n, const cg_rast_params *p,
+                       cg_vec4 light, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
+                       hipStream_t st, cg_stats *stats);
+void rast_release(cg_ctx *ctx);
+}  // namespace cg
+
+using namespace cg;
+
+// Grow-only device buffer.
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n)
+    {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct cg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    // RT scene
+    int n_tris = -1, n_sph = 0;
+    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d;
+    // RAST scratch (owned by cg_rast.hip)
+    DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount;
+};
+
+namespace cg {
+// exposed to cg_rast.hip
+void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
+{
+    DevBuf *b = nullptr;
+    switch (which) {
+    case 0: b = &c->rtris; break;
+    case 1: b = &c->rhdr; break;
+    case 2: b = &c->rspan; break;
+    case 3: b = &c->rpix; break;
+    case 4: b = &c->rargb; break;
+    case 5: b = &c->rdepth; break;
+    case 6: b = &c->rshadow; break;
+    case 7: b = &c->rcount; break;
+    default: *e = hipErrorInvalidValue; return nullptr;
+    }
+    *e = b->ensure(bytes);
+    return *e == hipSuccess ? b->p : nullptr;
+}
+hipStream_t ctx_stream(cg_ctx *c) { return c->stream; }
+int ctx_fail(cg_ctx *c, hipError_t e, const char *what)
+{
+    c->err = std::string(what) + ": " + hipGetErrorString(e);
+    return CG_E_HIP;
+}
+void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b)
+{
+    *a = c->ev0;
+    *b = c->ev1;
+}
+void rast_release(cg_ctx *c)
+{
+    c->rtris.release(); c->rhdr.release(); c->rspan.release(); c->rpix.release();
+    c->rargb.release(); c->rdepth.release(); c->rshadow.release(); c->rcount.release();
+}
+}  // namespace cg
+
+#define CG_TRY(ctx, call, what)                       \
+    do {                                              \
+        hipError_t e_ = (call);                       \
+        if (e_ != hipSuccess) return ctx_fail((ctx), e_, (what)); \
+    } while (0)
+
+extern "C" int cg_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int cg_create(int device, cg_ctx **out)
+{
+    if (!out) return CG_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CG_E_NODEVICE;
+    if (device < 0 || device >= n) return CG_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return CG_E_NODEVICE;
+    cg_ctx *c = new (std::nothrow) cg_ctx;
+    if (!c) return CG_E_INVALID;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return CG_E_HIP;
+    }
+    *out = c;
+    return CG_OK;
+}
+
+extern "C" void cg_destroy(cg_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->tris, &c->tc, &c->shade, &c->sph, &c->frame,
+                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d};
+    for (DevBuf *b : bufs) b->release();
+    rast_release(c);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" const char *cg_last_error(const cg_ctx *c) { return c ? c->err.c_str() : "no context"; }
+
+// ---------------------------------------------------------------------------
+// RT
+
+extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const cg_sphere *spheres,
+                               int n_spheres)
+{
+    if (!c || n_tris < 0 || n_spheres < 0 || (n_tris && !tris) || (n_spheres && !spheres))
+        return CG_E_INVALID;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    size_t nt = n_tris > 0 ? (size_t)n_tris : 1;
+    CG_TRY(c, c->tris.ensure(nt * sizeof(cg_tri)), "alloc tris");
+    CG_TRY(c, c->tc.ensure(nt * sizeof(RtTri)), "alloc tri constants");
+    CG_TRY(c, c->shade.ensure(nt * sizeof(RtShade)), "alloc tri shading");
+    CG_TRY(c, c->sph.ensure((size_t)(n_spheres > 0 ? n_spheres : 1) * sizeof(RtSphere)), "alloc spheres");
+    if (n_tris)
+        CG_TRY(c, hipMemcpyAsync(c->tris.p, tris, (size_t)n_tris * sizeof(cg_tri),
+                                 hipMemcpyHostToDevice, c->stream), "upload tris");
+    std::vector<RtSphere> S((size_t)n_spheres);
+    for (int i = 0; i < n_spheres; ++i) {
+        S[i] = RtSphere{spheres[i].centre.x, spheres[i].centre.y, spheres[i].centre.z,
+                        spheres[i].radiusSquared, spheres[i].color.x, spheres[i].color.y,
+                        spheres[i].color.z, 0.f};
+    }
+    if (n_spheres)
+        CG_TRY(c, hipMemcpyAsync(c->sph.p, S.data(), S.size() * sizeof(RtSphere),
+                                 hipMemcpyHostToDevice, c->stream), "upload spheres");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "scene upload");
+    c->n_tris = n_tris;
+    c->n_sph = n_spheres;
+    return CG_OK;
+}
+
+static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                      const cg_rt_shard *shard, RtFrame &F)
+{
+    if (!cam || cam->width <= 0 || cam->height <= 0 || n_lights < 0 || n_lights > kMaxLights ||
+        (n_lights && !lights))
+        return CG_E_INVALID;
+    if (c->n_tris < 0) {
+        c->err = "render before cg_rt_set_scene";
+        return CG_E_NOSCENE;
+    }
+    std::memset(&F, 0, sizeof(F));
+    F.W = cam->width;
+    F.H = cam->height;
+    F.focal = cam->focal;
+    F.indirect = cam->indirect;
+    F.cam[0] = cam->camera.x; F.cam[1] = cam->camera.y; F.cam[2] = cam->camera.z; F.cam[3] = cam->camera.w;
+    std::memcpy(F.R, cam->R, sizeof(F.R));
+    F.n_tris = c->n_tris;
+    F.n_sph = c->n_sph;
+    F.n_lights = n_lights;
+    for (int l = 0; l < n_lights; ++l) {
+        F.lpos[l][0] = lights[l].position.x; F.lpos[l][1] = lights[l].position.y;
+        F.lpos[l][2] = lights[l].position.z; F.lpos[l][3] = lights[l].position.w;
+        F.lcol[l][0] = lights[l].colour.x; F.lcol[l][1] = lights[l].colour.y;
+        F.lcol[l][2] = lights[l].colour.z;
+    }
+    cg_rt_shard one{0, 1, kRtTileH};
+    const cg_rt_shard *s = shard ? shard : &one;
+    if (s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0 ||
+        s->stripe_h % kRtTileH)
+        return CG_E_INVALID;
+    F.rank = s->rank;
+    F.nranks = s->nranks;
+    F.stripe_h = s->stripe_h;
+    F.rows_out = cg_rt_shard_rows(F.H, s);
+    return CG_OK;
+}
+
+extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
+{
+    cg_rt_shard one{0, 1, kRtTileH};
+    const cg_rt_shard *s = shard ? shard : &one;
+    if (height <= 0 || s->nranks < 1 || s->stripe_h <= 0) return CG_E_INVALID;
+    int stripes = (height + s->stripe_h - 1) / s->stripe_h;
+    int per = (stripes + s->nranks - 1) / s->nranks;
+    return per * s->stripe_h;
+}
+
+static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
+{
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, F.cam, (RtTri *)c->tc.p,
+                                (RtShade *)c->shade.p, st), "rt_prepare launch");
+    CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
+                               (const RtSphere *)c->sph.p, d_out, st), "rt_pixel launch");
+    return CG_OK;
+}
+
+extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_lights,
+                                   const cg_rt_camera *cam, const cg_rt_shard *shard,
+                                   uint32_t *d_out, void *stream)
+{
+    if (!c || !d_out) return CG_E_INVALID;
+    RtFrame F;
+    int rc = fill_frame(c, lights, n_lights, cam, shard, F);
+    if (rc) return rc;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    return rt_enqueue(c, F, d_out, stream ? (hipStream_t)stream : c->stream);
+}
+
+extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                            uint32_t *argb, cg_stats *stats)
+{
+    if (!c || !argb) return CG_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    RtFrame F;
+    int rc = fill_frame(c, lights, n_lights, cam, nullptr, F);
+    if (rc) return rc;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    size_t bytes = (size_t)F.rows_out * F.W * sizeof(uint32_t);
+    CG_TRY(c, c->frame.ensure(bytes), "alloc frame");
+    CG_TRY(c, hipEventRecord(c->ev0, c->stream), "event");
+    rc = rt_enqueue(c, F, (uint32_t *)c->frame.p, c->stream);
+    if (rc) return rc;
+    CG_TRY(c, hipEventRecord(c->ev1, c->stream), "event");
+    CG_TRY(c, hipMemcpyAsync(argb, c->frame.p, (size_t)F.H * F.W * sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, c->stream), "download frame");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "rt frame");
+    if (stats) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->n_tris = c->n_tris;
+        stats->n_spans = 0;
+    }
+    return CG_OK;
+}
+
+extern "C" int cg_rt_unstripe_device(cg_ctx *c, const uint32_t *d_gathered, int width, int height,
+                                     int nranks, int stripe_h, uint32_t *d_frame, void *stream)
+{
+    if (!c || !d_gathered || !d_frame || width <= 0 || height <= 0 || nranks < 1 || stripe_h <= 0)
+        return CG_E_INVALID;
+    cg_rt_shard s{0, nranks, stripe_h};
+    int rows = cg_rt_shard_rows(height, &s);
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    CG_TRY(c, launch_rt_unstripe(d_gathered, width, height, nranks, stripe_h, rows, d_frame,
+                                 stream ? (hipStream_t)stream : c->stream), "unstripe launch");
+    return CG_OK;
+}
+
+extern "C" int cg_rt_probe_closest(cg_ctx *c, const cg_vec4 *starts, const cg_vec4 *dirs, int n,
+                                   cg_isect *out, int *hit)
+{
+    if (!c || n < 0 || (n && (!starts || !dirs || !out || !hit))) return CG_E_INVALID;
+    if (c->n_tris < 0) return CG_E_NOSCENE;
+    if (n == 0) return CG_OK;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec4)), "alloc");
+    CG_TRY(c, c->probe_b.ensure((size_t)n * sizeof(cg_vec4)), "alloc");
+    CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
+    CG_TRY(c, c->probe_d.ensure((size_t)n * sizeof(int)), "alloc");
+    CG_TRY(c, hipMemcpyAsync(c->probe_a.p, starts, (size_t)n * sizeof(cg_vec4), hipMemcpyHostToDevice, c->stream), "h2d");
+    CG_TRY(c, hipMemcpyAsync(c->probe_b.p, dirs, (size_t)n * sizeof(cg_vec4), hipMemcpyHostToDevice, c->stream), "h2d");
+    RtFrame F;
+    std::memset(&F, 0, sizeof(F));
+    F.n_tris = c->n_tris;
+    F.n_sph = c->n_sph;
+    CG_TRY(c, launch_rt_probe_closest(F, (const cg_tri *)c->tris.p, (const RtSphere *)c->sph.p,
+                                      (const cg_vec4 *)c->probe_a.p, (const cg_vec4 *)c->probe_b.p, n,
+                                      (cg_isect *)c->probe_c.p, (int *)c->probe_d.p, c->stream), "probe");
+    CG_TRY(c, hipMemcpyAsync(out, c->probe_c.p, (size_t)n * sizeof(cg_isect), hipMemcpyDeviceToHost, c->stream), "d2h");
+    CG_TRY(c, hipMemcpyAsync(hit, c->probe_d.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, c->stream), "d2h");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "probe sync");
+    return CG_OK;
+}
+
+extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const cg_light *light,
+                                        int n, cg_vec3 *out)
+{
+    if (!c || !light || n < 0 || (n && (!isects || !out))) return CG_E_INVALID;
+    if (c->n_tris < 0) return CG_E_NOSCENE;
+    if (n == 0) return CG_OK;
+    for (int i = 0; i < n; ++i) {
+        int ti = isects[i].triangleIndex, si = isects[i].sphereIndex;
+        if (ti != -1 ? (ti < 0 || ti >= c->n_tris) : (si < 0 || si >= c->n_sph)) return CG_E_INVALID;
+    }
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    RtFrame F;
+    std::memset(&F, 0, sizeof(F));
+    F.n_tris = c->n_tris;
+    F.n_sph = c->n_sph;
+    F.n_lights = 1;
+    F.lpos[0][0] = light->position.x; F.lpos[0][1] = light->position.y;
+    F.lpos[0][2] = light->position.z; F.lpos[0][3] = light->position.w;
+    F.lcol[0][0] = light->colour.x; F.lcol[0][1] = light->colour.y; F.lcol[0][2] = light->colour.z;
+    // shadow rays use generic starts: RtTri constants are camera-independent
+    // except s/detT/K2/K3, which the shadow path does not read.
+    float zero[4] = {0, 0, 0, 1};
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, (RtTri *)c->tc.p,
+                                (RtShade *)c->shade.p, c->stream), "prepare");
+    CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
+    CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec3) + 16), "alloc");
+    CG_TRY(c, hipMemcpyAsync(c->probe_c.p, isects, (size_t)n * sizeof(cg_isect), hipMemcpyHostToDevice, c->stream), "h2d");
+    CG_TRY(c, launch_rt_probe_direct_light(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
+                                           (const RtSphere *)c->sph.p, (const cg_isect *)c->probe_c.p,
+                                           n, (cg_vec3 *)c->probe_a.p, c->stream), "probe");
+    CG_TRY(c, hipMemcpyAsync(out, c->probe_a.p, (size_t)n * sizeof(cg_vec3), hipMemcpyDeviceToHost, c->stream), "d2h");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "probe sync");
+    return CG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RAST entry points (kernels in cg_rast.hip)
+
+extern "C" int cg_rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n,
+                                     const cg_rast_params *p, cg_vec4 light, uint32_t *d_argb,
+                                     float *d_depth, int32_t *d_shadow, void *stream)
+{
+    if (!c || !p || !d_argb || n < 0 || (n && !d_tris)) return CG_E_INVALID;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    return rast_render_device(c, d_tris, n, p, light, d_argb, d_depth, d_shadow,
+                              stream ? (hipStream_t)stream : c->stream, nullptr);
+}
+
+extern "C" int cg_rast_render(cg_ctx *c, const cg_rtri *tris, int n, const cg_rast_params *p,
+                              cg_vec4 light, uint32_t *argb, float *depth, int32_t *shadow,
+                              cg_stats *stats)
+{
+    if (!c || !p || !argb || n < 0 || (n && !tris) || p->width <= 2 || p->height <= 2 ||
+        p->height > kRastMaxH)
+        return CG_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    size_t npx = (size_t)p->width * p->height;
+    hipError_t e;
+    cg_rtri *d_tris = (cg_rtri *)ctx_buf(c, 0, (size_t)(n > 0 ? n : 1) * sizeof(cg_rtri), &e);
+    if (!d_tris) return ctx_fail(c, e, "alloc rast tris");
+    uint32_t *d_argb = (uint32_t *)ctx_buf(c, 4, npx * 4, &e);
+    if (!d_argb) return ctx_fail(c, e, "alloc argb");
+    float *d_depth = (float *)ctx_buf(c, 5, npx * 4, &e);
+    if (!d_depth) return ctx_fail(c, e, "alloc depth");
+    int32_t *d_shadow = (int32_t *)ctx_buf(c, 6, npx * 4, &e);
+    if (!d_shadow) return ctx_fail(c, e, "alloc shadow");
+    if (n) CG_TRY(c, hipMemcpyAsync(d_tris, tris, (size_t)n * sizeof(cg_rtri), hipMemcpyHostToDevice, c->stream), "upload tris");
+    int rc = rast_render_device(c, d_tris, n, p, light, d_argb, d_depth, d_shadow, c->stream, stats);
+    if (rc) return rc;
+    CG_TRY(c, hipMemcpyAsync(argb, d_argb, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h argb");
+    if (depth) CG_TRY(c, hipMemcpyAsync(depth, d_depth, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h depth");
+    if (shadow) CG_TRY(c, hipMemcpyAsync(shadow, d_shadow, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h shadow");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "rast frame");
+    if (stats) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->n_tris = n;
+    }
+    return CG_OK;
+}

@@ -1,0 +1,138 @@
+// rasteriser.cpp -- headless drop-in for rasteriser/Source/skeleton.cpp
+// (texture mode 0, colour mode 0).
+//
+// Same globals (focalLength, cameraPos, yaw, R, sceneCoordinatesLightPos,
+// lightPower, indirectLightPowerPerArea, originalroom/originalbox), same
+// main loop and Draw(screen*) -> screen->buffer, same screenshot.bmp.  The
+// host geometry (camera space, shadow volumes, clipping) runs on the host as
+// in the reference (cg_rast_prepare); the fill and post-pass run on the GPU
+// (cg_rast_render).  Scripted keys as in Update() (:311-417): w s a d q e =
+// light, 1 2 = indirect, U D L R z x = camera, n m = yaw, f g = focal,
+// ESC = 'X'.
+//
+//   rasteriser [--width W] [--height H] [--focal F] [--keys KEYS] [--out FILE]
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "SDLauxiliary.h"
+#include "TestModelH.h"
+#include "cg_render.h"
+
+using namespace std;
+using glm::mat4;
+using glm::vec3;
+using glm::vec4;
+
+int SCREEN_WIDTH = 900, SCREEN_HEIGHT = 720;                 // :21-22
+float focalLength = 512;                                      // :30
+vec4 cameraPos(0, 0, -3.001, 1);                              // :31
+float yaw = 0.0;                                              // :34
+mat4 R(1.0f);                                                 // :35
+vec4 sceneCoordinatesLightPos(0, -0.5, 0, 1);                 // :52
+vec3 lightPower = 20.0f * vec3(1, 1, 1);                      // :53
+vec3 indirectLightPowerPerArea = 0.15f * vec3(1, 1, 1);       // :54
+vector<rast::Triangle> originalroom;                          // :84
+vector<rast::Triangle> originalbox;                           // :85
+vector<rast::Triangle> clippedTriangles;                      // :86
+
+static cg_ctx *g_ctx = nullptr;
+static string g_keys;
+static size_t g_frame = 0;
+
+static void die(int rc, const char *what)
+{
+    cerr << what << " failed (" << rc << "): " << (g_ctx ? cg_last_error(g_ctx) : "") << endl;
+    exit(1);
+}
+
+// skeleton.cpp:203-308
+void Draw(screen *screen)
+{
+    cg_rast_params p;
+    p.width = screen->width;
+    p.height = screen->height;
+    p.focal = focalLength;
+    p.camera = cg_vec4{cameraPos.x, cameraPos.y, cameraPos.z, cameraPos.w};
+    memcpy(p.R, R.data(), sizeof(p.R));
+    p.light_scene = cg_vec4{sceneCoordinatesLightPos.x, sceneCoordinatesLightPos.y,
+                            sceneCoordinatesLightPos.z, sceneCoordinatesLightPos.w};
+    p.light_power = cg_vec3{lightPower.x, lightPower.y, lightPower.z};
+    p.indirect_first = indirectLightPowerPerArea.x;
+    const cg_rtri *room = reinterpret_cast<const cg_rtri *>(originalroom.data());
+    const cg_rtri *box = reinterpret_cast<const cg_rtri *>(originalbox.data());
+    cg_vec4 light;
+    int n = cg_rast_prepare(&p, room, (int)originalroom.size(), box, (int)originalbox.size(),
+                            nullptr, 0, &light);
+    if (n < 0) die(n, "cg_rast_prepare");
+    clippedTriangles.resize(n);
+    n = cg_rast_prepare(&p, room, (int)originalroom.size(), box, (int)originalbox.size(),
+                        reinterpret_cast<cg_rtri *>(clippedTriangles.data()), n, &light);
+    int rc = cg_rast_render(g_ctx, reinterpret_cast<const cg_rtri *>(clippedTriangles.data()), n, &p,
+                            light, screen->buffer, nullptr, nullptr, nullptr);
+    if (rc) die(rc, "cg_rast_render");
+    // PixelShader leaves the global at 0.2 after the first shaded fragment (:585)
+    if (n > 0) indirectLightPowerPerArea = 0.2f * vec3(1, 1, 1);
+}
+
+// skeleton.cpp:311-417 with scripted keys
+bool Update()
+{
+    if (g_frame >= g_keys.size()) return g_frame++ == 0;
+    char key = g_keys[g_frame++];
+    switch (key) {
+    case 'w': sceneCoordinatesLightPos += vec4(0, 0, 0.1, 0); break;
+    case 's': sceneCoordinatesLightPos += vec4(0, 0, -0.1, 0); break;
+    case 'a': sceneCoordinatesLightPos += vec4(-0.1, 0, 0, 0); break;
+    case 'd': sceneCoordinatesLightPos += vec4(0.1, 0, 0, 0); break;
+    case 'q': sceneCoordinatesLightPos += vec4(0, -0.1, 0, 0); break;
+    case 'e': sceneCoordinatesLightPos += vec4(0, 0.1, 0, 0); break;
+    case '1': indirectLightPowerPerArea -= vec3(0.005f, 0.005f, 0.005f); break;
+    case '2': indirectLightPowerPerArea += vec3(0.005f, 0.005f, 0.005f); break;
+    case 'U': cameraPos += vec4(0, 0, 0.1, 0); break;
+    case 'D': cameraPos += vec4(0, 0, -0.1, 0); break;
+    case 'L': cameraPos += vec4(-0.1, 0, 0, 0); break;
+    case 'R': cameraPos += vec4(0.1, 0, 0, 0); break;
+    case 'z': cameraPos += vec4(0, -0.1, 0, 0); break;
+    case 'x': cameraPos += vec4(0, 0.1, 0, 0); break;
+    case 'n':
+    case 'm':
+        if (key == 'n') yaw -= 0.174533;
+        else yaw += 0.174533;
+        R[0][0] = cos(yaw); R[0][1] = 0; R[0][2] = -sin(yaw);
+        R[1][0] = 0;        R[1][1] = 1; R[1][2] = 0;
+        R[2][0] = sin(yaw); R[2][1] = 0; R[2][2] = cos(yaw);
+        break;
+    case 'f': focalLength += 5; break;
+    case 'g': focalLength -= 5; break;
+    case 'X': return false;
+    default: break;
+    }
+    return true;
+}
+
+int main(int argc, char *argv[])
+{
+    string out = "screenshot.bmp";
+    for (int i = 1; i + 1 < argc; i += 2) {
+        string a = argv[i];
+        if (a == "--width") SCREEN_WIDTH = atoi(argv[i + 1]);
+        else if (a == "--height") SCREEN_HEIGHT = atoi(argv[i + 1]);
+        else if (a == "--focal") focalLength = (float)atof(argv[i + 1]);
+        else if (a == "--keys") g_keys = argv[i + 1];
+        else if (a == "--out") out = argv[i + 1];
+    }
+    int rc = cg_create(0, &g_ctx);
+    if (rc) die(rc, "cg_create");
+    screen *screen = InitializeSDL(SCREEN_WIDTH, SCREEN_HEIGHT, false);
+    rast::LoadTestModel(originalroom, originalbox);          // :131
+    while (Update()) {
+        Draw(screen);
+        SDL_Renderframe(screen);
+    }
+    SDL_SaveImage(screen, out.c_str());
+    KillSDL(screen);
+    cg_destroy(g_ctx);
+    return 0;
+}

@@ -1,0 +1,160 @@
+/*
+ * cg_render.h -- C-ABI of the MI355X-native renderer (gfx950 HIP kernels).
+ *
+ * This is the drop-in boundary for the two pixel-loop hot paths of
+ * fznsakib/Computer-Graphics.  The reference has no plugin/FFI API: its hot
+ * paths sit behind `void Draw(screen*)`, which reads mutable globals and
+ * writes ARGB pixels into the caller-owned `screen->buffer`.
+ * The host surface in computer-graphics_amd/host/ keeps that exact shape
+ * (same Draw(screen*), same globals, same Triangle/Sphere/Intersection/Light
+ * structs, same PutPixelSDL pixel layout) and calls the entry points below.
+ *
+ * Conventions: plain pointers and sizes only; POD structs with the
+ * reference's field order; every call returns 0 (CG_OK) or a negative
+ * CG_E* code and never throws across the ABI.  A context is bound to one
+ * GPU and is not thread-safe (one host thread per context, like the
+ * reference's single main thread).  Host buffers are caller-owned; device
+ * buffers are context-owned unless a *_device entry point is given a
+ * caller-owned device pointer.  `stream` arguments are hipStream_t values
+ * (NULL = the context's own stream).
+ */
+#ifndef CG_RENDER_H
+#define CG_RENDER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CG_OK 0
+#define CG_E_INVALID (-1)     /* bad argument / shape */
+#define CG_E_NODEVICE (-2)    /* no HIP device / HIP init failed */
+#define CG_E_HIP (-3)         /* HIP runtime error (see cg_last_error) */
+#define CG_E_NOSCENE (-4)     /* render before cg_rt_set_scene */
+#define CG_E_CAPACITY (-5)    /* output capacity too small */
+
+typedef struct cg_ctx cg_ctx;
+
+typedef struct { float x, y, z; } cg_vec3;
+typedef struct { float x, y, z, w; } cg_vec4;
+
+/* raytracer/Source/TestModelH.h:80-115 `Triangle` (76 B: v0@0 v1@16 v2@32 normal@48 color@64). */
+typedef struct { cg_vec4 v0, v1, v2, normal; cg_vec3 color; } cg_tri;
+/* raytracer/Source/TestModelH.h:14-22 `Sphere` (44 B). */
+typedef struct { float radius, radiusSquared; cg_vec3 centre, color, normal; } cg_sphere;
+/* raytracer/Source/skeleton.cpp:47-50 `Light` (28 B). */
+typedef struct { cg_vec4 position; cg_vec3 colour; } cg_light;
+/* raytracer/Source/skeleton.cpp:40-45 `Intersection` (28 B). */
+typedef struct { cg_vec4 position; float distance; int triangleIndex; int sphereIndex; } cg_isect;
+
+/* The RT globals Draw reads (raytracer/Source/skeleton.cpp:56-60, :110). */
+typedef struct {
+    int width, height;     /* SCREEN_WIDTH / SCREEN_HEIGHT (:19-20) */
+    float focal;           /* focalLength (:56) */
+    cg_vec4 camera;        /* cameraPos (:57) */
+    float R[16];           /* R (:60), glm::mat4 column-major: R[c*4+r] */
+    float indirect;        /* indirectLight scale (:110), 0.5 */
+} cg_rt_camera;
+
+/* Row sharding for the multi-GPU path: stripes of `stripe_h` rows are dealt
+ * round-robin over `nranks`; this rank renders stripes k with
+ * k % nranks == rank, packed in order into its output. */
+typedef struct { int rank, nranks, stripe_h; } cg_rt_shard;
+
+/* rasteriser/Source/TestModelH.h:13-42 `Triangle` (84 B). */
+typedef struct { cg_vec4 v0, v1, v2, normal; cg_vec3 color; int texture; int index; } cg_rtri;
+
+/* The RAST globals Draw reads (rasteriser/Source/skeleton.cpp:30-86). */
+typedef struct {
+    int width, height;        /* SCREEN_WIDTH / SCREEN_HEIGHT (:21-22) */
+    float focal;              /* focalLength (:30) */
+    cg_vec4 camera;           /* cameraPos (:31) */
+    float R[16];              /* R (:35) */
+    cg_vec4 light_scene;      /* sceneCoordinatesLightPos (:52) */
+    cg_vec3 light_power;      /* lightPower (:53) */
+    float indirect_first;     /* indirectLightPowerPerArea at frame start (:54, :581-585):
+                                 0.15 on the very first frame, 0.2 afterwards */
+} cg_rast_params;
+
+typedef struct {
+    double kernel_ms;        /* device time of the frame's kernels (HIP events) */
+    double total_ms;         /* host wall time of the call */
+    int n_tris;              /* triangles rendered (RAST: after clipping) */
+    int n_spans;             /* RAST: row spans produced by span setup */
+} cg_stats;
+
+/* ---- context ---------------------------------------------------------- */
+int  cg_create(int device, cg_ctx **out);
+void cg_destroy(cg_ctx *ctx);
+const char *cg_last_error(const cg_ctx *ctx);
+/* Number of visible HIP devices (0 without a GPU); never fails loudly. */
+int  cg_device_count(void);
+
+/* ---- raytracer -------------------------------------------------------- */
+/* LoadTestModel (raytracer/Source/TestModelH.h:121-279): 28 triangles +
+ * one sphere, scaled to [-1,1]^3.  Returns the triangle count. */
+int cg_rt_load_test_model(cg_tri *tris, int cap, cg_sphere *sphere);
+/* Upload the scene LoadTestModel built (TestModelH.h:121-279); kept device
+ * resident until the next call.  Replaces the per-frame `vector<Triangle>`
+ * the reference rebuilds in Draw (skeleton.cpp:113-116). */
+int cg_rt_set_scene(cg_ctx *ctx, const cg_tri *tris, int n_tris,
+                    const cg_sphere *spheres, int n_spheres);
+/* One frame of raytracer Draw (skeleton.cpp:104-169): per pixel 3x3
+ * sub-rays, ClosestIntersection (:263-363) and DirectLight (:366-415),
+ * PutPixelSDL packing (SDLauxiliary.h:149-161).  Writes W*H ARGB into the
+ * caller-owned host buffer `argb` (row-major, top row first), exactly what
+ * the reference leaves in screen->buffer. */
+int cg_rt_render(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                 uint32_t *argb, cg_stats *stats);
+/* Device-resident form: renders this shard's rows into the caller-owned
+ * device buffer d_out (cg_rt_shard_rows() rows of W pixels), enqueued on
+ * `stream`, no synchronisation.  shard may be NULL (= whole frame). */
+int cg_rt_render_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                        const cg_rt_shard *shard, uint32_t *d_out, void *stream);
+/* Rows a shard renders (including padding rows of its last stripe). */
+int cg_rt_shard_rows(int height, const cg_rt_shard *shard);
+/* Reassemble a frame from gathered shards: d_gathered holds nranks blocks of
+ * cg_rt_shard_rows() rows each, in rank order. */
+int cg_rt_unstripe_device(cg_ctx *ctx, const uint32_t *d_gathered, int width, int height,
+                          int nranks, int stripe_h, uint32_t *d_frame, void *stream);
+/* Single-ray probes for known-answer tests: device evaluation of
+ * ClosestIntersection (:263-363) and DirectLight (:366-415) on n rays. */
+int cg_rt_probe_closest(cg_ctx *ctx, const cg_vec4 *starts, const cg_vec4 *dirs, int n,
+                        cg_isect *out, int *hit);
+int cg_rt_probe_direct_light(cg_ctx *ctx, const cg_isect *isects, const cg_light *light, int n,
+                             cg_vec3 *out);
+
+/* ---- rasteriser ------------------------------------------------------- */
+/* LoadTestModel (rasteriser/Source/TestModelH.h:48-312) with texture
+ * selectors 0: room (10) and boxes (20). Returns n_room + n_boxes. */
+int cg_rast_load_test_model(cg_rtri *room, int room_cap, int *n_room, cg_rtri *boxes,
+                            int boxes_cap, int *n_boxes);
+/* Host geometry of rasteriser Draw (skeleton.cpp:205-241): camera space
+ * (:701-716), createShadowVolume (:1676-1722), rotation by R (:223-228),
+ * clip space w = z/f (:691-699), clip planes 1..6 (:720-1673).  Writes the
+ * ordered clipped triangle list (up to `cap`) and the rotated camera-space
+ * light; returns the triangle count (may exceed cap: CG_E_CAPACITY is not
+ * raised, the caller re-sizes) or a negative error. */
+int cg_rast_prepare(const cg_rast_params *p, const cg_rtri *room, int n_room,
+                    const cg_rtri *boxes, int n_boxes, cg_rtri *out, int cap,
+                    cg_vec4 *light_out);
+/* One frame of the rasteriser fill + post-pass (skeleton.cpp:243-307):
+ * DrawPolygon / VertexShader / ComputePolygonRows / DrawPolygonRows /
+ * Interpolate / PixelShader / calculateIllumination over the ordered list,
+ * then surroundingShadowSum + antiAliasing + PutPixelSDL.  Outputs are
+ * caller-owned host buffers of W*H (any may be NULL except argb):
+ * argb = screen->buffer, depth = depthBuffer, shadow = shadowBuffer. */
+int cg_rast_render(cg_ctx *ctx, const cg_rtri *tris, int n, const cg_rast_params *p,
+                   cg_vec4 light, uint32_t *argb, float *depth, int32_t *shadow,
+                   cg_stats *stats);
+/* Device-resident form: triangles already on the device (d_tris), outputs
+ * into caller-owned device buffers (d_depth / d_shadow may be NULL). */
+int cg_rast_render_device(cg_ctx *ctx, const cg_rtri *d_tris, int n, const cg_rast_params *p,
+                          cg_vec4 light, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
+                          void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CG_RENDER_H */

@@ -1,0 +1,202 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of the CPU restatement.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / CPU baseline.  See
+cg_oracle.h for what it restates and how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libcgoracle.so")
+
+
+class V3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class V4(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("w", C.c_float)]
+
+
+class RtTri(C.Structure):
+    _fields_ = [("v0", V4), ("v1", V4), ("v2", V4), ("normal", V4), ("color", V3)]
+
+
+class Sphere(C.Structure):
+    _fields_ = [("radius", C.c_float), ("radiusSquared", C.c_float), ("centre", V3), ("color", V3),
+                ("normal", V3)]
+
+
+class Isect(C.Structure):
+    _fields_ = [("position", V4), ("distance", C.c_float), ("triangleIndex", C.c_int),
+                ("sphereIndex", C.c_int)]
+
+
+class Light(C.Structure):
+    _fields_ = [("position", V4), ("colour", V3)]
+
+
+class RtParams(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", V4),
+                ("R", C.c_float * 16), ("indirect", C.c_float), ("n_lights", C.c_int),
+                ("lights", Light * 4)]
+
+
+class RtCounters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("n_ray", "n_t", "n_uv", "n_sph", "n_dl")]
+
+
+class RastTri(C.Structure):
+    _fields_ = [("v0", V4), ("v1", V4), ("v2", V4), ("normal", V4), ("color", V3),
+                ("texture", C.c_int), ("index", C.c_int)]
+
+
+class Pixel(C.Structure):
+    _fields_ = [("x", C.c_int), ("y", C.c_int), ("zinv", C.c_float), ("pos3d", V4)]
+
+
+class RastParams(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", V4),
+                ("R", C.c_float * 16), ("light_scene", V4), ("light_power", V3),
+                ("indirect_first", C.c_float)]
+
+
+class RastCounters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("n_tris", "n_spans", "n_frags", "n_shaded", "n_shadow")]
+
+
+_lib = None
+
+
+def build(quiet=True):
+    """Compile the restatement (gcc, -O3, no -march, -ffp-contract=off)."""
+    r = subprocess.run(["make", "-C", HERE], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + r.stdout + r.stderr)
+    if not quiet:
+        print(r.stdout)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    sigs = {
+        "cgo_rt_load_scene": (C.c_int, [C.POINTER(RtTri), C.c_int, C.POINTER(Sphere)]),
+        "cgo_rt_default_params": (None, [C.POINTER(RtParams), C.c_int, C.c_int]),
+        "cgo_rt_draw": (None, [C.POINTER(RtParams), C.POINTER(RtTri), C.c_int, C.POINTER(Sphere),
+                               C.c_int, P, C.c_int, C.c_int, C.POINTER(RtCounters)]),
+        "cgo_rt_draw_mt": (C.c_int, [C.POINTER(RtParams), C.POINTER(RtTri), C.c_int,
+                                     C.POINTER(Sphere), C.c_int, P, C.c_int, C.c_int, C.c_int]),
+        "cgo_rt_closest": (C.c_int, [V4, V4, C.POINTER(RtTri), C.c_int, C.POINTER(Sphere), C.c_int,
+                                     C.POINTER(Isect), C.POINTER(RtCounters)]),
+        "cgo_rt_direct_light": (V3, [C.POINTER(Isect), C.POINTER(RtTri), C.c_int, C.POINTER(Sphere),
+                                     C.c_int, C.POINTER(Light), C.POINTER(RtCounters)]),
+        "cgo_sphere_solve_quadratic": (C.c_int, [C.c_float, C.c_float, C.c_float,
+                                                 C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+        "cgo_put_pixel": (C.c_uint32, [V3]),
+        "cgo_rast_load_scene": (C.c_int, [C.POINTER(RastTri), C.POINTER(C.c_int),
+                                          C.POINTER(RastTri), C.POINTER(C.c_int)]),
+        "cgo_rast_default_params": (None, [C.POINTER(RastParams), C.c_int, C.c_int]),
+        "cgo_rast_geometry": (C.c_int, [C.POINTER(RastParams), C.POINTER(RastTri), C.c_int,
+                                        C.POINTER(V4)]),
+        "cgo_rast_polygon_rows": (C.c_int, [C.POINTER(Pixel), C.POINTER(Pixel), C.POINTER(Pixel),
+                                            C.c_int]),
+        "cgo_rast_interpolate": (None, [Pixel, Pixel, C.POINTER(Pixel), C.c_int]),
+        "cgo_rast_draw": (None, [C.POINTER(RastParams), P, P, P, P, P, P,
+                                 C.POINTER(RastCounters)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def rt_scene():
+    lib = load()
+    tris = (RtTri * 64)()
+    sph = Sphere()
+    n = lib.cgo_rt_load_scene(tris, 64, C.byref(sph))
+    return tris, n, sph
+
+
+def rt_params(width, height, focal=256.0, cam=(0.0, 0.0, -3.0, 1.0), R=None, indirect=0.5,
+              lights=None):
+    lib = load()
+    p = RtParams()
+    lib.cgo_rt_default_params(C.byref(p), width, height)
+    p.focal = focal
+    p.camera = V4(*cam)
+    if R is not None:
+        p.R = (C.c_float * 16)(*list(R))
+    p.indirect = indirect
+    if lights is not None:
+        p.n_lights = len(lights)
+        for i, (pos, col) in enumerate(lights):
+            p.lights[i].position = V4(*pos)
+            p.lights[i].colour = V3(*col)
+    return p
+
+
+def rt_draw(p, rows=None, counters=False, threads=1):
+    """Render rows [r0, r1) of the RT frame (ARGB uint32, W*H, untouched rows 0)."""
+    lib = load()
+    tris, n, sph = rt_scene()
+    out = np.zeros(p.width * p.height, np.uint32)
+    r0, r1 = rows if rows is not None else (0, p.height)
+    cnt = RtCounters()
+    if threads > 1:
+        lib.cgo_rt_draw_mt(C.byref(p), tris, n, C.byref(sph), 1, out.ctypes.data_as(C.c_void_p),
+                           r0, r1, threads)
+    else:
+        lib.cgo_rt_draw(C.byref(p), tris, n, C.byref(sph), 1, out.ctypes.data_as(C.c_void_p), r0, r1,
+                        C.byref(cnt) if counters else None)
+    return (out, cnt) if counters else out
+
+
+def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
+                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2):
+    lib = load()
+    p = RastParams()
+    lib.cgo_rast_default_params(C.byref(p), width, height)
+    p.focal = focal
+    p.camera = V4(*cam)
+    if R is not None:
+        p.R = (C.c_float * 16)(*list(R))
+    p.light_scene = V4(*light)
+    p.indirect_first = indirect_first
+    return p
+
+
+def rast_geometry(p):
+    lib = load()
+    out = (RastTri * 8192)()
+    light = V4()
+    n = lib.cgo_rast_geometry(C.byref(p), out, 8192, C.byref(light))
+    return out, n, light
+
+
+def rast_draw(p, counters=False):
+    """Full RAST frame: (argb uint32, depth float32, shadow int32) planes of W*H."""
+    lib = load()
+    npx = p.width * p.height
+    argb = np.zeros(npx, np.uint32)
+    depth = np.zeros(npx, np.float32)
+    shadow = np.zeros(npx, np.int32)
+    cnt = RastCounters()
+    vp = C.c_void_p
+    lib.cgo_rast_draw(C.byref(p), argb.ctypes.data_as(vp), depth.ctypes.data_as(vp),
+                      shadow.ctypes.data_as(vp), None, None, None, C.byref(cnt))
+    return (argb, depth, shadow, cnt) if counters else (argb, depth, shadow)

@@ -1,0 +1,124 @@
+"""GPU: the raytracer hot path (rt_pixel_kernel via cg_rt_render) against the
+oracle, bit-exact (integer ARGB output: the tolerance is 0), plus the
+reference's own screenshot.bmp and the SURVEY.md 8c fingerprints."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import cgamd
+import cgdist
+import make_golden as mg
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _lights(cfg):
+    arr = (cgamd.Light * len(cfg["lights"]))()
+    for i, (p, c) in enumerate(cfg["lights"]):
+        arr[i].position = cgamd.Vec4(*p)
+        arr[i].colour = cgamd.Vec3(*c)
+    return arr
+
+
+def _cam(cfg):
+    R = (C.c_float * 16)(*cfg["R"]) if cfg["R"] else None
+    return cgamd.rt_camera(cfg["width"], cfg["height"], cfg["focal"], tuple(cfg["cam"]), R)
+
+
+@pytest.fixture(scope="module")
+def rt(ctx):
+    tris, n, sph = cgamd.rt_scene()
+    ctx.rt_set_scene(tris, n, sph, 1)
+    return ctx
+
+
+def test_rt_screenshot_golden(rt):
+    """GPU frame == raytracer/screenshot.bmp, every pixel."""
+    cfg = mg.rt_configs()["rt_320x256_z-2.9"]
+    argb, st = rt.rt_render(_cam(cfg), _lights(cfg))
+    assert int((argb != mg.screenshot_argb()).sum()) == 0
+    assert st.kernel_ms > 0
+
+
+@pytest.mark.parametrize("name", list(mg.rt_configs()))
+def test_rt_configs_match_golden(rt, golden, name):
+    cfg = mg.rt_configs()[name]
+    argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+    h = mg.sha(argb)
+    assert h == golden["rt"][name]["argb_sha256"], name
+    ref = mg.REFERENCE_FINGERPRINTS.get(name)
+    if ref:
+        assert h.startswith(ref["argb"])
+
+
+def test_rt_vs_live_oracle_diff_report(rt):
+    """Independent live oracle run at an odd size; on mismatch report the diff."""
+    p = oracle.rt_params(200, 120, 150.0, (0.05, -0.1, -2.7, 1.0))
+    ref = oracle.rt_draw(p, threads=os.cpu_count() or 8)
+    cam = cgamd.rt_camera(200, 120, 150.0, (0.05, -0.1, -2.7, 1.0))
+    argb, _ = rt.rt_render(cam)
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"{bad.size} pixels differ, first {bad[:8]} gpu {argb[bad[:4]]} ref {ref[bad[:4]]}"
+
+
+def test_rt_probe_closest_and_direct_light(rt, golden):
+    rays = golden["rt_rays"]
+    out, hit = rt.rt_probe_closest([r["start"] for r in rays], [r["dir"] for r in rays])
+    isects = []
+    for r, o, h in zip(rays, out, hit):
+        assert h == r["hit"]
+        if h:
+            e = r["isect"]
+            assert [o.position.x, o.position.y, o.position.z, o.position.w] == e["position"]
+            assert o.distance == e["distance"]
+            assert (o.triangleIndex, o.sphereIndex) == (e["triangleIndex"], e["sphereIndex"])
+            isects.append((o, r["direct_light"]))
+    light = cgamd.Light(cgamd.Vec4(0.0, -0.5, -0.7, 1.0), cgamd.Vec3(14.0, 14.0, 14.0))
+    dl = rt.rt_probe_direct_light([i for i, _ in isects], light)
+    for got, (_, want) in zip(dl, isects):
+        assert [got.x, got.y, got.z] == want
+
+
+def test_rt_sharded_device_path_reassembles(rt):
+    """cg_rt_render_device per shard + cg_rt_unstripe_device == whole frame."""
+    torch = pytest.importorskip("torch")
+    W, H = 320, 256
+    cam = cgamd.rt_camera(W, H)
+    full, _ = rt.rt_render(cam)
+    for n in (2, 3, 8):
+        rows = cgdist.shard_rows(H, n)
+        g = torch.zeros(n * rows * W, dtype=torch.int32, device="cuda")
+        for r in range(n):
+            sh = cgamd.RtShard(r, n, cgdist.DEFAULT_STRIPE)
+            rt.rt_render_device(cam, g.data_ptr() + r * rows * W * 4, sh,
+                                torch.cuda.current_stream().cuda_stream)
+        frame = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        rt.rt_unstripe_device(g.data_ptr(), W, H, n, cgdist.DEFAULT_STRIPE, frame.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy().view(np.uint32), full), n
+
+
+def test_rt_full_1080p_vs_oracle(rt, golden):
+    """North-star config C2 at full size: hash of the reference fingerprint AND
+    a live multithreaded oracle frame, every pixel."""
+    cfg = mg.rt_configs()["rt_1920x1080_f1080"]
+    argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+    assert mg.sha(argb) == golden["rt"]["rt_1920x1080_f1080"]["argb_sha256"]
+
+
+def test_rt_empty_scene_is_black(ctx):
+    """No triangles, no spheres: every pixel is PutPixelSDL(black) = 0x80000000."""
+    ctx.rt_set_scene(None, 0, None, 0)
+    argb, _ = ctx.rt_render(cgamd.rt_camera(64, 32, 64.0))
+    assert np.all(argb == 0x80000000)
+    tris, n, sph = cgamd.rt_scene()
+    ctx.rt_set_scene(tris, n, sph, 1)
+
+
+def test_rt_errors(ctx):
+    with pytest.raises(RuntimeError):
+        ctx.rt_render(cgamd.rt_camera(0, 10))
