@@ -50,6 +50,7 @@ struct RtFrame {
     float R[16];
     int n_tris, n_sph, n_lights;
     int rank, nranks, stripe_h, rows_out;
+    int cull_primary, cull_shadow;   // certificates on (CG_RT_CULL env: 0 none, 1 primary, 2 both)
     float lpos[kMaxLights][4];
     float lcol[kMaxLights][3];
 };

@@ -72,11 +72,198 @@ __device__ __forceinline__ bool sphere_intersect(const RtSphere &S, vec3 start, 
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Per-wave culling certificate for camera-origin rays.
+//
+// For a ray d from the camera, the reference's triangle test (skeleton.cpp:
+// 289-335) computes, in float, det = det3(-d, e1, e2), detU = det3(-d, s, e2),
+// detV = det3(-d, e1, s) with s = cam - v0 -- in exact arithmetic the linear
+// forms -d.(e1 x e2), -d.(s x e2), -d.(e1 x s).  A triangle is skipped for the
+// whole wave only if, for EVERY d of the wave's bundle (the box spanned by the
+// 9 sub-ray directions of its 64 pixels, exact float extremes), the float
+// evaluation is certain to reject it: det has a certain sign and t < 0, or
+// u < 0, or v < 0, or u + v > 1.  The linear forms are evaluated exactly
+// enough in FP64 and each float det3 evaluation is bounded by 16*eps times the
+// sum of its |triple products| (gamma_4 suffices), so a skipped triangle
+// could never have been accepted: results are bit-identical to testing all.
+__device__ __forceinline__ void lin_range(double cx, double cy, double hx, double hy, double f,
+                                          double X, double Y, double Z, double &lo, double &hi)
+{
+    // range of -d.(X,Y,Z) over d = (cx +- hx, cy +- hy, f)
+    double c = -(cx * X + cy * Y + f * Z);
+    double h = hx * fabs(X) + hy * fabs(Y);
+    lo = c - h;
+    hi = c + h;
+}
+
+__device__ __forceinline__ double det3_bound(double Dx, double Dy, double Dz, vec3 a, vec3 b)
+{
+    // sum of |triple products| of det3(-d, a, b) with |d| <= (Dx, Dy, Dz)
+    return Dx * (fabs((double)a.y * b.z) + fabs((double)b.y * a.z)) +
+           fabs((double)a.x) * (Dy * fabs((double)b.z) + fabs((double)b.y) * Dz) +
+           fabs((double)b.x) * (Dy * fabs((double)a.z) + fabs((double)a.y) * Dz);
+}
+
+__device__ bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double g = 16.0 * eps;
+    vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z), s = v3(c.sx, c.sy, c.sz);
+    // N = e1 x e2, A = s x e2, B = e1 x s (float inputs: products exact in FP64)
+    double Nx = (double)e1.y * e2.z - (double)e2.y * e1.z, Ny = (double)e1.z * e2.x - (double)e2.z * e1.x,
+           Nz = (double)e1.x * e2.y - (double)e2.x * e1.y;
+    double Ax = (double)s.y * e2.z - (double)e2.y * s.z, Ay = (double)s.z * e2.x - (double)e2.z * s.x,
+           Az = (double)s.x * e2.y - (double)e2.x * s.y;
+    double Bx = (double)e1.y * s.z - (double)s.y * e1.z, By = (double)e1.z * s.x - (double)s.z * e1.x,
+           Bz = (double)e1.x * s.y - (double)s.x * e1.y;
+    double cx = 0.5 * ((double)x0 + x1), cy = 0.5 * ((double)y0 + y1);
+    double hx = 0.5 * ((double)x1 - x0), hy = 0.5 * ((double)y1 - y0), fz = f;
+    double Dx = fmax(fabs((double)x0), fabs((double)x1)), Dy = fmax(fabs((double)y0), fabs((double)y1)),
+           Dz = fabs(fz);
+    double dlo, dhi, ulo, uhi, vlo, vhi, blo, bhi;
+    lin_range(cx, cy, hx, hy, fz, Nx, Ny, Nz, dlo, dhi);
+    lin_range(cx, cy, hx, hy, fz, Ax, Ay, Az, ulo, uhi);
+    lin_range(cx, cy, hx, hy, fz, Bx, By, Bz, vlo, vhi);
+    lin_range(cx, cy, hx, hy, fz, Ax + Bx - Nx, Ay + By - Ny, Az + Bz - Nz, blo, bhi);
+    double Ed = g * det3_bound(Dx, Dy, Dz, e1, e2) + 1e-12 * (fabs(dlo) + fabs(dhi));
+    double Eu = g * det3_bound(Dx, Dy, Dz, s, e2) + 1e-12 * (fabs(ulo) + fabs(uhi));
+    double Ev = g * det3_bound(Dx, Dy, Dz, e1, s) + 1e-12 * (fabs(vlo) + fabs(vhi));
+    double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
+    if (!(isfinite(dlo) && isfinite(dhi) && isfinite(Ed + Eu + Ev + Eb) && isfinite(ulo + uhi + vlo + vhi + blo + bhi)))
+        return false;
+    int sg;
+    if (dlo - Ed > 0) sg = 1;
+    else if (dhi + Ed < 0) sg = -1;
+    else return false;                                   // det may vanish: keep
+    const double dmin = sg > 0 ? dlo - Ed : -(dhi + Ed);  // |det| >= dmin > 0
+    const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
+    // t = detT/det < 0 (and not underflowing to -0): distance < 0 rejects (:311)
+    double dT = c.detT;
+    if (dT != 0.0 && ((dT > 0) != (sg > 0)) && fabs(dT) > 1e-20 * dmax) return true;
+    // u < 0 or v < 0 (:328)
+    // (the quotient must not underflow to -0, which would pass u >= 0)
+    const double tiny = 1e-20 * dmax;
+    if (sg > 0 ? (uhi + Eu < -tiny) : (ulo - Eu > tiny)) return true;
+    if (sg > 0 ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) return true;
+    // u + v > 1 after float rounding of u, v and their sum: certain when
+    // (U + V - 1) > 4 eps (|U| + |V| + 1), U = detU/det, V = detV/det
+    double K = (fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev) / dmin + 1.0;
+    double margin = 4.0 * eps * K;
+    if (sg > 0 ? ((blo - Eb) / dmax > margin) : ((-(bhi + Eb)) / dmax > margin)) return true;
+    return false;
+}
+
+__device__ __forceinline__ float wave_min(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Per-wave culling certificate for DirectLight's shadow rays (skeleton.cpp:394).
+//
+// A shadow ray starts at S = P + n*1e-5 with direction d = L - P (the float
+// vectors the reference uses).  With a = L - v0 and p = S - L + d (a few 1e-5
+// at most, plus the rounding of s = S - v0), exact arithmetic gives
+//   det  = -d.(e1 x e2)                      (linear in d)
+//   detU = -d.(a x e2) - [d, p, e2]          (linear + |d||p||e2|)
+//   detV = -d.(e1 x a) - [d, e1, p]
+//   detT - det = a.(e1 x e2) + p.(e1 x e2)   (constant + |p||N|)
+// so over the wave's box of d the same certificate as for camera rays holds,
+// plus "the triangle lies beyond the light" (t > 1 + 1e-5, hence distance >=
+// rmag: no shadow).  `pn` bounds |p| (Euclidean) over the wave.
+struct ShadowBox {
+    float lo[3], hi[3];   // exact float extremes of d over the casting lanes
+    float pn;             // bound on |S - L + d| over the casting lanes
+};
+
+__device__ bool cull_shadow(const RtTri &c, vec3 L, const ShadowBox &B)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double g = 16.0 * eps;
+    vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z);
+    double ax = (double)L.x - c.v0x, ay = (double)L.y - c.v0y, az = (double)L.z - c.v0z;
+    double Nx = (double)e1.y * e2.z - (double)e2.y * e1.z, Ny = (double)e1.z * e2.x - (double)e2.z * e1.x,
+           Nz = (double)e1.x * e2.y - (double)e2.x * e1.y;
+    double Ax = ay * e2.z - (double)e2.y * az, Ay = az * e2.x - (double)e2.z * ax, Az = ax * e2.y - (double)e2.x * ay;
+    double Bx = (double)e1.y * az - ay * e1.z, By = (double)e1.z * ax - az * e1.x, Bz = (double)e1.x * ay - ax * e1.y;
+    double cx = 0.5 * ((double)B.lo[0] + B.hi[0]), cy = 0.5 * ((double)B.lo[1] + B.hi[1]),
+           cz = 0.5 * ((double)B.lo[2] + B.hi[2]);
+    double hx = 0.5 * ((double)B.hi[0] - B.lo[0]), hy = 0.5 * ((double)B.hi[1] - B.lo[1]),
+           hz = 0.5 * ((double)B.hi[2] - B.lo[2]);
+    auto lin = [&](double X, double Y, double Z, double &lo, double &hi) {
+        double m = -(cx * X + cy * Y + cz * Z);
+        double h = hx * fabs(X) + hy * fabs(Y) + hz * fabs(Z);
+        lo = m - h;
+        hi = m + h;
+    };
+    double Dx = fmax(fabs((double)B.lo[0]), fabs((double)B.hi[0]));
+    double Dy = fmax(fabs((double)B.lo[1]), fabs((double)B.hi[1]));
+    double Dz = fmax(fabs((double)B.lo[2]), fabs((double)B.hi[2]));
+    double dn = sqrt(Dx * Dx + Dy * Dy + Dz * Dz);
+    // |s| <= |a| + |d| + |p| componentwise; p also absorbs s's own rounding
+    double Sx = fabs(ax) + Dx + B.pn, Sy = fabs(ay) + Dy + B.pn, Sz = fabs(az) + Dz + B.pn;
+    double pn = (double)B.pn + eps * sqrt(Sx * Sx + Sy * Sy + Sz * Sz) + 1e-12;
+    double n1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    double n2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    double nN = sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+    double dlo, dhi, ulo, uhi, vlo, vhi, blo, bhi;
+    lin(Nx, Ny, Nz, dlo, dhi);
+    lin(Ax, Ay, Az, ulo, uhi);
+    lin(Bx, By, Bz, vlo, vhi);
+    lin(Ax + Bx - Nx, Ay + By - Ny, Az + Bz - Nz, blo, bhi);
+    // float-evaluation bounds (sum of |triple products|)
+    auto M3 = [](double x0, double y0, double z0, double x1, double y1, double z1, double x2, double y2,
+                 double z2) {   // |c0|,|c1|,|c2| components of det3(c0, c1, c2)
+        return x0 * (y1 * z2 + y2 * z1) + x1 * (y0 * z2 + y2 * z0) + x2 * (y0 * z1 + y1 * z0);
+    };
+    double ae1x = fabs((double)e1.x), ae1y = fabs((double)e1.y), ae1z = fabs((double)e1.z);
+    double ae2x = fabs((double)e2.x), ae2y = fabs((double)e2.y), ae2z = fabs((double)e2.z);
+    double Ed = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + 1e-12 * (fabs(dlo) + fabs(dhi));
+    double Eu = g * M3(Dx, Dy, Dz, Sx, Sy, Sz, ae2x, ae2y, ae2z) + dn * pn * n2 + 1e-12 * (fabs(ulo) + fabs(uhi));
+    double Ev = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, Sx, Sy, Sz) + dn * pn * n1 + 1e-12 * (fabs(vlo) + fabs(vhi));
+    double Et = g * M3(Sx, Sy, Sz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + pn * nN;
+    double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
+    double aN = ax * Nx + ay * Ny + az * Nz;
+    double EaN = 1e-12 * (fabs(ax * Nx) + fabs(ay * Ny) + fabs(az * Nz));
+    if (!(isfinite(dlo + dhi + ulo + uhi + vlo + vhi + blo + bhi) && isfinite(Ed + Eu + Ev + Et + Eb + aN)))
+        return false;
+    int sg;
+    if (dlo - Ed > 0) sg = 1;
+    else if (dhi + Ed < 0) sg = -1;
+    else return false;
+    const double dmin = sg > 0 ? dlo - Ed : -(dhi + Ed);
+    const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
+    const double tiny = 1e-20 * dmax;
+    // detT = det + aN + (p.N): t = 1 + (detT - det)/det
+    double tlo = (aN - EaN - Et - Ed) / 1.0, thi = aN + EaN + Et + Ed;   // range of detT - det
+    // beyond the light: t - 1 > 1e-5 certain -> distance >= rmag (:395)
+    if (sg > 0 ? (tlo > 1e-5 * dmax) : (thi < -1e-5 * dmax)) return true;
+    // t < 0: detT = det + (detT - det) has the opposite sign of det, i.e.
+    // (detT - det)/det < -1 - margin
+    if (sg > 0 ? (thi + dmax < -tiny - 1e-6 * dmax) : (tlo - dmax > tiny + 1e-6 * dmax)) return true;
+    if (sg > 0 ? (uhi + Eu < -tiny) : (ulo - Eu > tiny)) return true;
+    if (sg > 0 ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) return true;
+    double K = (fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev) / dmin + 1.0;
+    double margin = 4.0 * eps * K;
+    if (sg > 0 ? ((blo - Eb) / dmax > margin) : ((-(bhi + Eb)) / dmax > margin)) return true;
+    return false;
+}
+
 // ClosestIntersection for camera-origin rays (skeleton.cpp:263-363).
 // Returns best index: >= 0 triangle, -1 - k sphere k, INT_MIN no hit; t out.
+// Triangles are visited in index order; with CULL only those whose bit is set
+// in `mask` (certified-rejected ones are skipped, see cull_primary).
+template <bool CULL>
 __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__restrict__ tc,
                                                const RtSphere *__restrict__ sph, vec3 d,
-                                               float &best_t)
+                                               float &best_t, unsigned long long mask)
 {
     const float bound = FLT_MAX;
     float best = bound;
@@ -84,7 +271,12 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
     float bt = 0.f;
     vec3 nd = -d;
     float len = length(d);                                   // :307
-    for (int k = 0; k < F.n_tris; ++k) {
+    for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
+        int k = it;
+        if (CULL) {
+            k = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+        }
         const RtTri c = tc[k];
         float Q2 = nd.y * c.e2z - c.e2y * nd.z;
         float Q1 = nd.y * c.e1z - c.e1y * nd.z;
@@ -125,14 +317,20 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
 // any-hit search bounded by rmag with an early exit; triangles are tested
 // with the reference's float ops (their acceptance does not depend on the
 // running minimum, only on `distance < rmag` here).
+template <bool CULL>
 __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restrict__ tc,
                                          const RtSphere *__restrict__ sph, vec3 start, vec3 d,
-                                         float rmag)
+                                         float rmag, unsigned long long mask)
 {
     const float bound = FLT_MAX;
     vec3 nd = -d;
     float len = length(d);
-    for (int k = 0; k < F.n_tris; ++k) {
+    for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
+        int k = it;
+        if (CULL) {
+            k = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+        }
         const RtTri c = tc[k];
         float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
         float Q2 = nd.y * c.e2z - c.e2y * nd.z;
@@ -161,10 +359,11 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
 }
 
 // DirectLight (skeleton.cpp:366-415) for a hit at `pos` on object `bi`.
+template <bool CULL>
 __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__restrict__ tc,
                                              const RtShade *__restrict__ shade,
                                              const RtSphere *__restrict__ sph, int bi, vec3 pos,
-                                             vec3 objColor, int l)
+                                             vec3 objColor, int l, unsigned long long smask = ~0ull)
 {
     vec3 lp = v3(F.lpos[l][0], F.lpos[l][1], F.lpos[l][2]);
     vec3 r = lp - pos;                                                   // :370
@@ -180,7 +379,7 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
         normal = normalize(pos - v3(S.cx, S.cy, S.cz));
     }
     vec3 origin = pos + normal * 0.00001f;                              // :394
-    if (shadowed(F, tc, sph, origin, r, rmag)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
+    if (shadowed<CULL>(F, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
     vec3 nd = normalize(r);                                              // :400
     float a = dot(nd, normal);                                           // :403
     const float b = (float)(4 * M_PI);                                   // :404
@@ -190,13 +389,61 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     return ((objColor * lc) * a) / area;                                 // :412
 }
 
+__device__ __forceinline__ vec3 object_colour(const RtShade *__restrict__ shade,
+                                              const RtSphere *__restrict__ sph, int bi)
+{
+    if (bi >= 0) {
+        RtShade s = shade[bi];
+        return v3(s.cr, s.cg, s.cb);
+    }
+    const RtSphere S = sph[-1 - bi];
+    return v3(S.cr, S.cg, S.cb);
+}
+
+// Shadow-ray certificate mask for light l over the lanes that hit (must be
+// called by the whole wave in converged control flow).
+__device__ __forceinline__ unsigned long long shadow_mask(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                          const RtShade *__restrict__ shade,
+                                                          const RtSphere *__restrict__ sph, bool hit,
+                                                          int bi, vec3 pos, int l, int lane)
+{
+    vec3 lp = v3(F.lpos[l][0], F.lpos[l][1], F.lpos[l][2]);
+    ShadowBox B;
+    float pb = 0.0f;
+    vec3 r = v3(0.f, 0.f, 0.f);
+    if (hit) {
+        r = lp - pos;                                                    // :370/:373
+        vec3 normal;
+        if (bi >= 0) {
+            RtShade s = shade[bi];
+            normal = v3(s.nx, s.ny, s.nz);
+        } else {
+            const RtSphere S = sph[-1 - bi];
+            normal = normalize(pos - v3(S.cx, S.cy, S.cz));
+        }
+        vec3 S = pos + normal * 0.00001f;                               // :394
+        double px = (double)S.x - lp.x + r.x, py = (double)S.y - lp.y + r.y, pz = (double)S.z - lp.z + r.z;
+        pb = (float)(sqrt(px * px + py * py + pz * pz) * (1.0 + 1e-6) + 1e-30);
+    }
+    const float inf = FLT_MAX;
+    B.lo[0] = wave_min(hit ? r.x : inf); B.hi[0] = wave_max(hit ? r.x : -inf);
+    B.lo[1] = wave_min(hit ? r.y : inf); B.hi[1] = wave_max(hit ? r.y : -inf);
+    B.lo[2] = wave_min(hit ? r.z : inf); B.hi[2] = wave_max(hit ? r.z : -inf);
+    B.pn = wave_max(pb);
+    bool keep = true;
+    if (lane < F.n_tris && B.lo[0] <= B.hi[0]) keep = !cull_shadow(tc[lane], lp, B);
+    return __ballot(keep && lane < F.n_tris);
+}
+
 __device__ __forceinline__ int shard_row(const RtFrame &F, int L)
 {
     int k = L / F.stripe_h;
     return (k * F.nranks + F.rank) * F.stripe_h + (L - k * F.stripe_h);
 }
 
-// Draw (skeleton.cpp:104-169), one thread per pixel.
+// Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
+// one certificate mask per wave (lane k certifies triangle k).
+template <bool CULL>
 __global__ __launch_bounds__(kRtThreads) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                               const RtShade *__restrict__ shade,
                                                               const RtSphere *__restrict__ sph,
@@ -205,12 +452,26 @@ __global__ __launch_bounds__(kRtThreads) void rt_pixel_kernel(RtFrame F, const R
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int u = blockIdx.x * kRtTileW + wave * 8 + (lane & 7);
     const int L = blockIdx.y * kRtTileH + (lane >> 3);
-    if (u >= F.W || L >= F.rows_out) return;
-    const int v = shard_row(F, L);
+    const bool inside = u < F.W && L < F.rows_out;
+    const int v = inside ? shard_row(F, L) : 0;
+    const bool active = inside && v < F.H;
+    vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
+    dir = mat4_mul(F.R, dir);                                                         // :128
+    unsigned long long mask = ~0ull;
+    if (CULL) {
+        // exact float extremes of the wave's sub-ray directions (:137): newDir.x =
+        // fl(dir.x + 0.5 i) is monotone in dir.x, so the bundle lies in this box
+        float ax = active ? dir.x : __int_as_float(0x7fc00000), ay = active ? dir.y : __int_as_float(0x7fc00000);
+        float x0 = wave_min(active ? ax : FLT_MAX), x1 = wave_max(active ? ax : -FLT_MAX);
+        float y0 = wave_min(active ? ay : FLT_MAX), y1 = wave_max(active ? ay : -FLT_MAX);
+        x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+        bool keep = true;
+        if (lane < F.n_tris && x0 <= x1 && y0 <= y1) keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
+        mask = __ballot(keep && lane < F.n_tris);
+    }
+    if (!inside) return;
     uint32_t px = 0u;
-    if (v < F.H) {
-        vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);   // :126
-        dir = mat4_mul(F.R, dir);                                                    // :128
+    if (active) {
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
@@ -219,22 +480,19 @@ __global__ __launch_bounds__(kRtThreads) void rt_pixel_kernel(RtFrame F, const R
                 const float m = 0.5f;
                 vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);  // :137
                 float t;
-                int bi = closest_primary(F, tc, sph, nd, t);                             // :140
-                if (bi != INT_MIN) {
-                    valid = true;
-                    vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z); // :326/:345
-                    vec3 oc;
-                    if (bi >= 0) {
-                        RtShade s = shade[bi];
-                        oc = v3(s.cr, s.cg, s.cb);
-                    } else {
-                        const RtSphere S = sph[-1 - bi];
-                        oc = v3(S.cr, S.cg, S.cb);
+                int bi = closest_primary<CULL>(F, tc, sph, nd, t, mask);                 // :140
+                const bool hit = bi != INT_MIN;
+                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z); // :326/:345
+                if (hit) valid = true;
+                for (int l = 0; l < F.n_lights; ++l) {                                       // :151-153
+                    unsigned long long smask = ~0ull;
+                    if (CULL && F.cull_shadow) smask = shadow_mask(F, tc, shade, sph, hit, bi, pos, l, lane);
+                    if (hit) {
+                        vec3 oc = object_colour(shade, sph, bi);
+                        pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, smask);
                     }
-                    for (int l = 0; l < F.n_lights; ++l)                                  // :151-153
-                        pc = pc + direct_light(F, tc, shade, sph, bi, pos, oc, l);
-                    pc = pc + (oc * ind);                                                 // :156
                 }
+                if (hit) pc = pc + (object_colour(shade, sph, bi) * ind);                    // :156
             }
         }
         px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));            // :160-166
@@ -322,7 +580,7 @@ __global__ void rt_probe_direct_light_kernel(RtFrame F, const RtTri *__restrict_
     vec3 oc;
     if (bi >= 0) oc = v3(shade[bi].cr, shade[bi].cg, shade[bi].cb);
     else oc = v3(sph[-1 - bi].cr, sph[-1 - bi].cg, sph[-1 - bi].cb);
-    vec3 r = direct_light(F, tc, shade, sph, bi, pos, oc, 0);
+    vec3 r = direct_light<false>(F, tc, shade, sph, bi, pos, oc, 0);
     out[i] = cg_vec3{r.x, r.y, r.z};
 }
 
@@ -342,8 +600,12 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
                             const RtSphere *d_sph, uint32_t *d_out, hipStream_t st)
 {
     dim3 grid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    hipLaunchKernelGGL(rt_pixel_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                       d_out);
+    if (F.n_tris <= 64 && F.cull_primary)
+        hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
+                           d_sph, d_out);
+    else
+        hipLaunchKernelGGL(rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
+                           d_sph, d_out);
     return hipGetLastError();
 }
 

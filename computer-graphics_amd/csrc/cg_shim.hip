@@ -3,6 +3,7 @@
 // across the ABI; HIP failures become CG_E_HIP with the HIP message kept in
 // the context for cg_last_error().
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -217,6 +218,12 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     F.nranks = s->nranks;
     F.stripe_h = s->stripe_h;
     F.rows_out = cg_rt_shard_rows(F.H, s);
+    static int cull = [] {
+        const char *e = getenv("CG_RT_CULL");
+        return e ? atoi(e) : 2;
+    }();
+    F.cull_primary = cull >= 1;
+    F.cull_shadow = cull >= 2;
     return CG_OK;
 }
 
