@@ -72,6 +72,28 @@ __device__ __forceinline__ bool sphere_intersect(const RtSphere &S, vec3 start, 
     return true;
 }
 
+__device__ __forceinline__ vec3 object_colour(const RtShade *__restrict__ shade,
+                                              const RtSphere *__restrict__ sph, int bi)
+{
+    if (bi >= 0) {
+        RtShade s = shade[bi];
+        return v3(s.cr, s.cg, s.cb);
+    }
+    const RtSphere S = sph[-1 - bi];
+    return v3(S.cr, S.cg, S.cb);
+}
+
+__device__ __forceinline__ vec3 hit_normal(const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
+                                           int bi, vec3 pos)
+{
+    if (bi >= 0) {                                                       // :377-380
+        RtShade s = shade[bi];
+        return v3(s.nx, s.ny, s.nz);
+    }
+    const RtSphere S = sph[-1 - bi];                                     // :381-387
+    return normalize(pos - v3(S.cx, S.cy, S.cz));
+}
+
 // ---------------------------------------------------------------------------
 // Per-wave culling certificate for camera-origin rays.
 //
@@ -370,14 +392,7 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
            r2 = (double)r.z * (double)r.z;
     float rmag = (float)sqrt((r0 + r1) + r2);                            // :371
-    vec3 normal;
-    if (bi >= 0) {                                                       // :377-380
-        RtShade s = shade[bi];
-        normal = v3(s.nx, s.ny, s.nz);
-    } else {                                                             // :381-387
-        const RtSphere S = sph[-1 - bi];
-        normal = normalize(pos - v3(S.cx, S.cy, S.cz));
-    }
+    vec3 normal = hit_normal(shade, sph, bi, pos);
     vec3 origin = pos + normal * 0.00001f;                              // :394
     if (shadowed<CULL>(F, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
     vec3 nd = normalize(r);                                              // :400
@@ -389,47 +404,41 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     return ((objColor * lc) * a) / area;                                 // :412
 }
 
-__device__ __forceinline__ vec3 object_colour(const RtShade *__restrict__ shade,
-                                              const RtSphere *__restrict__ sph, int bi)
-{
-    if (bi >= 0) {
-        RtShade s = shade[bi];
-        return v3(s.cr, s.cg, s.cb);
+// Shadow-ray certificate for light l: per-lane box of d = L - pos and bound
+// on |S - L + d| over the hits given, reduced over the wave into one mask.
+struct LaneShadowBox {
+    float lo[3], hi[3], pn;
+    __device__ void init()
+    {
+        lo[0] = lo[1] = lo[2] = FLT_MAX;
+        hi[0] = hi[1] = hi[2] = -FLT_MAX;
+        pn = 0.0f;
     }
-    const RtSphere S = sph[-1 - bi];
-    return v3(S.cr, S.cg, S.cb);
+};
+
+__device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lp, vec3 pos, vec3 normal)
+{
+    vec3 r = lp - pos;                                                   // :370/:373
+    vec3 S = pos + normal * 0.00001f;                                    // :394
+    double px = (double)S.x - lp.x + r.x, py = (double)S.y - lp.y + r.y, pz = (double)S.z - lp.z + r.z;
+    float pb = (float)(sqrt(px * px + py * py + pz * pz) * (1.0 + 1e-6) + 1e-30);
+    b.lo[0] = fminf(b.lo[0], r.x); b.hi[0] = fmaxf(b.hi[0], r.x);
+    b.lo[1] = fminf(b.lo[1], r.y); b.hi[1] = fmaxf(b.hi[1], r.y);
+    b.lo[2] = fminf(b.lo[2], r.z); b.hi[2] = fmaxf(b.hi[2], r.z);
+    b.pn = fmaxf(b.pn, pb);
 }
 
-// Shadow-ray certificate mask for light l over the lanes that hit (must be
-// called by the whole wave in converged control flow).
-__device__ __forceinline__ unsigned long long shadow_mask(const RtFrame &F, const RtTri *__restrict__ tc,
-                                                          const RtShade *__restrict__ shade,
-                                                          const RtSphere *__restrict__ sph, bool hit,
-                                                          int bi, vec3 pos, int l, int lane)
+// Whole wave, converged control flow.
+__device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                             const LaneShadowBox &b, vec3 lp, int lane)
 {
-    vec3 lp = v3(F.lpos[l][0], F.lpos[l][1], F.lpos[l][2]);
     ShadowBox B;
-    float pb = 0.0f;
-    vec3 r = v3(0.f, 0.f, 0.f);
-    if (hit) {
-        r = lp - pos;                                                    // :370/:373
-        vec3 normal;
-        if (bi >= 0) {
-            RtShade s = shade[bi];
-            normal = v3(s.nx, s.ny, s.nz);
-        } else {
-            const RtSphere S = sph[-1 - bi];
-            normal = normalize(pos - v3(S.cx, S.cy, S.cz));
-        }
-        vec3 S = pos + normal * 0.00001f;                               // :394
-        double px = (double)S.x - lp.x + r.x, py = (double)S.y - lp.y + r.y, pz = (double)S.z - lp.z + r.z;
-        pb = (float)(sqrt(px * px + py * py + pz * pz) * (1.0 + 1e-6) + 1e-30);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        B.lo[c] = wave_min(b.lo[c]);
+        B.hi[c] = wave_max(b.hi[c]);
     }
-    const float inf = FLT_MAX;
-    B.lo[0] = wave_min(hit ? r.x : inf); B.hi[0] = wave_max(hit ? r.x : -inf);
-    B.lo[1] = wave_min(hit ? r.y : inf); B.hi[1] = wave_max(hit ? r.y : -inf);
-    B.lo[2] = wave_min(hit ? r.z : inf); B.hi[2] = wave_max(hit ? r.z : -inf);
-    B.pn = wave_max(pb);
+    B.pn = wave_max(b.pn);
     bool keep = true;
     if (lane < F.n_tris && B.lo[0] <= B.hi[0]) keep = !cull_shadow(tc[lane], lp, B);
     return __ballot(keep && lane < F.n_tris);
@@ -471,31 +480,49 @@ __global__ __launch_bounds__(kRtThreads) void rt_pixel_kernel(RtFrame F, const R
     }
     if (!inside) return;
     uint32_t px = 0u;
+    // Pass 1: the 9 primary rays (:134-140); hits staged in LDS (bi, t) so the
+    // shadow certificate of light 0 covers the whole wave's hits at once.
+    __shared__ int s_bi[9][kRtThreads];
+    __shared__ float s_t[9][kRtThreads];
+    const float m = 0.5f;
+    LaneShadowBox sb;
+    sb.init();
+    const vec3 lp0 = v3(F.lpos[0][0], F.lpos[0][1], F.lpos[0][2]);
     if (active) {
+        for (int k = 0; k < 9; ++k) {
+            const int i = k / 3 - 1, j = k % 3 - 1;
+            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);       // :137
+            float t;
+            int bi = closest_primary<CULL>(F, tc, sph, nd, t, mask);                     // :140
+            s_bi[k][threadIdx.x] = bi;
+            s_t[k][threadIdx.x] = t;
+            if (CULL && F.cull_shadow && F.n_lights > 0 && bi != INT_MIN) {
+                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+                shadow_box_add(sb, lp0, pos, hit_normal(shade, sph, bi, pos));
+            }
+        }
+    }
+    unsigned long long smask0 = ~0ull;
+    if (CULL && F.cull_shadow && F.n_lights > 0) smask0 = shadow_mask_of(F, tc, sb, lp0, lane);
+    if (active) {
+        // Pass 2: shading in the reference's order (:143-157)
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
-        for (int i = -1; i <= 1; ++i) {
-            for (int j = -1; j <= 1; ++j) {
-                const float m = 0.5f;
-                vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);  // :137
-                float t;
-                int bi = closest_primary<CULL>(F, tc, sph, nd, t, mask);                 // :140
-                const bool hit = bi != INT_MIN;
-                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z); // :326/:345
-                if (hit) valid = true;
-                for (int l = 0; l < F.n_lights; ++l) {                                       // :151-153
-                    unsigned long long smask = ~0ull;
-                    if (CULL && F.cull_shadow) smask = shadow_mask(F, tc, shade, sph, hit, bi, pos, l, lane);
-                    if (hit) {
-                        vec3 oc = object_colour(shade, sph, bi);
-                        pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, smask);
-                    }
-                }
-                if (hit) pc = pc + (object_colour(shade, sph, bi) * ind);                    // :156
-            }
+        for (int k = 0; k < 9; ++k) {
+            const int i = k / 3 - 1, j = k % 3 - 1;
+            const int bi = s_bi[k][threadIdx.x];
+            if (bi == INT_MIN) continue;
+            const float t = s_t[k][threadIdx.x];
+            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+            vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);  // :326/:345
+            valid = true;
+            vec3 oc = object_colour(shade, sph, bi);
+            for (int l = 0; l < F.n_lights; ++l)                                          // :151-153
+                pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, l == 0 ? smask0 : ~0ull);
+            pc = pc + (oc * ind);                                                         // :156
         }
-        px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));            // :160-166
+        px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));             // :160-166
     }
     out[(size_t)L * F.W + u] = px;
 }
