@@ -161,13 +161,39 @@ __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
     // Edge samples -> rows (:466-497).  Rows outside the screen never shade.
     for (int ei = 0; ei < 3; ++ei) {
         Edge e = make_edge(vp[ei], vp[ei == 2 ? 0 : ei + 1]);
-        for (int j = threadIdx.x; j < e.n; j += kSetupThreads) {
-            int y = edge_y(e, j);
-            if (y < ylo || y > yhi) continue;               // also covers :485's y - min >= 0
-            int x = edge_x(e, j);
-            unsigned seq = ((unsigned)ei << 30) | (unsigned)j;
-            atomicMin(&lkey[y - ylo], key_left(x, seq));
-            atomicMax(&rkey[y - ylo], key_right(x, seq));
+        // y is monotone in j, so within a wave the samples of one row are
+        // contiguous lanes: a segmented scan leaves the row's min/max key in
+        // the segment's last lane, which alone touches LDS (a near-horizontal
+        // edge otherwise serialises ~N atomics on one row).
+        const int lane = threadIdx.x & 63;
+        for (int jb = 0; jb < e.n; jb += kSetupThreads) {
+            const int j = jb + (int)threadIdx.x;
+            const bool in = j < e.n;
+            int y = in ? edge_y(e, j) : INT_MIN;
+            const bool vis = in && y >= ylo && y <= yhi;   // also covers :485's y - min >= 0
+            if (!vis) y = INT_MIN + 1 + lane;              // never merges with a real row
+            unsigned long long kl = ~0ull, kr = 0ull;
+            if (vis) {
+                int x = edge_x(e, j);
+                unsigned seq = ((unsigned)ei << 30) | (unsigned)j;
+                kl = key_left(x, seq);
+                kr = key_right(x, seq);
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                int yo = __shfl_up(y, o, 64);
+                unsigned long long lo = __shfl_up(kl, o, 64), ro = __shfl_up(kr, o, 64);
+                if (lane >= o && yo == y) {
+                    kl = lo < kl ? lo : kl;
+                    kr = ro > kr ? ro : kr;
+                }
+            }
+            int yn = __shfl_down(y, 1, 64);
+            bool last = lane == 63 || yn != y;
+            if (vis && last) {
+                atomicMin(&lkey[y - ylo], kl);
+                atomicMax(&rkey[y - ylo], kr);
+            }
         }
     }
     __syncthreads();
@@ -234,25 +260,57 @@ __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
     if (threadIdx.x == 0) hdr[t] = h;
 }
 
-// Ordered per-row triangle lists (one wave per row).
-__global__ __launch_bounds__(256) void rast_rowlist_kernel(const RastHdr *__restrict__ hdr, int n,
-                                                          int H, int *__restrict__ list,
-                                                          int *__restrict__ count)
+// Ordered per-row records (one wave per screen row): for every triangle in
+// order whose span on this row has a fragment on screen, a 64-byte record
+// with everything the fill needs -- one scalar load per record, no
+// dependent loads in the fill loop.
+struct alignas(16) RowRec {
+    int lx, rx;
+    float lz, sz, lX, sX, lY, sY;
+    int t, first_x;          // triangle index; x of the frame's first shaded fragment on this row, else -1
+    int shadow;              // colour.x < 0 (shadow-volume triangle)
+    float nx, ny, nz, pad0, pad1;
+};
+static_assert(sizeof(RowRec) == 64, "RowRec");
+
+__global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
+                                                       const RastSpan *__restrict__ spans,
+                                                       const RastHdr *__restrict__ hdr,
+                                                       const int *__restrict__ first_tri,
+                                                       RowRec *__restrict__ recs, int *__restrict__ count)
 {
-    const int y = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int y = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (y >= H) return;
+    if (y >= A.H) return;
+    const int ft = A.want_first ? *first_tri : INT_MAX;
     int c = 0;
-    for (int base = 0; base < n; base += 64) {
-        int t = base + lane;
-        bool cov = false;
-        if (t < n) {
-            RastHdr h = hdr[t];
-            cov = h.ylo <= y && y <= h.yhi;
+    for (int base = 0; base < A.n; base += 64) {
+        const int t = base + lane;
+        bool keep = false;
+        RastSpan sp;
+        RastHdr h;
+        if (t < A.n) {
+            h = hdr[t];
+            if (h.ylo <= y && y <= h.yhi) {
+                sp = spans[(size_t)t * A.H + y];
+                // fragments x in [lx, rx - 1] (:504) intersecting [0, W)
+                keep = sp.rx > sp.lx && sp.rx - 1 >= 0 && sp.lx <= A.W - 1;
+            }
         }
-        unsigned long long m = __ballot(cov);
+        unsigned long long m = __ballot(keep);
         unsigned long long below = lane ? (m & ((1ull << lane) - 1)) : 0ull;
-        if (cov) list[(size_t)y * n + c + __popcll(below)] = t;
+        if (keep) {
+            const cg_rtri T = tris[t];
+            RowRec r;
+            r.lx = sp.lx; r.rx = sp.rx;
+            r.lz = sp.lz; r.sz = sp.sz; r.lX = sp.lX; r.sX = sp.sX; r.lY = sp.lY; r.sY = sp.sY;
+            r.t = t;
+            r.first_x = (t == ft && h.fy == y) ? h.fx : -1;
+            r.shadow = T.color.x >= 0 ? 0 : 1;
+            r.nx = T.normal.x; r.ny = T.normal.y; r.nz = T.normal.z;
+            r.pad0 = r.pad1 = 0.f;
+            recs[(size_t)y * A.n + c + __popcll(below)] = r;
+        }
         c += __popcll(m);
     }
     if (lane == 0) count[y] = c;
@@ -278,55 +336,98 @@ __device__ __forceinline__ vec3 illum_D(const RastArgs &A, float zinv, float X, 
 
 // Per-pixel shade state between fill and post: .x = triangle index (as bits;
 // -1 none; bit 30 = shaded by the frame's first fragment), .yzw = D.
-__global__ __launch_bounds__(256) void rast_fill_kernel(
-    const cg_rtri *__restrict__ tris, RastArgs A, const RastSpan *__restrict__ spans,
-    const RastHdr *__restrict__ hdr, const int *__restrict__ list, const int *__restrict__ count,
-    const int *__restrict__ first_tri, float4 *__restrict__ state, float *__restrict__ depth_out,
-    int32_t *__restrict__ shadow_out)
+// One wave per kFillPx-pixel row segment, kFillPx/64 pixels per lane, state in
+// registers; records walked in triangle order (the reference's ordered
+// z-buffer), one uniform overlap test per record.
+constexpr int kFillPx = 256;
+constexpr int kFillPerLane = kFillPx / 64;
+
+__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec *__restrict__ recs,
+                                                       const int *__restrict__ count,
+                                                       float4 *__restrict__ state,
+                                                       float *__restrict__ depth_out,
+                                                       int32_t *__restrict__ shadow_out)
 {
-    const int segs = (A.W + 63) >> 6;
-    const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int segs = (A.W + kFillPx - 1) / kFillPx;
+    // wave-uniform by construction; readfirstlane lets the compiler keep the
+    // record walk on the scalar unit (s_load per record, uniform branches)
+    const int seg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int y = seg / segs;
     if (y >= A.H) return;
-    const int x0 = (seg - y * segs) * 64;
-    const int x = x0 + lane;
-    const int ft = A.want_first ? *first_tri : INT_MAX;
-    float depth = 0.0f;                                    // :247
-    int shadow = 0;                                        // :259
-    int tri = -1;
-    vec3 D = v3(0.f, 0.f, 0.f);
+    const int x0 = (seg - y * segs) * kFillPx;
+    float depth[kFillPerLane];
+    int shadow[kFillPerLane], win[kFillPerLane];
+#pragma unroll
+    for (int p = 0; p < kFillPerLane; ++p) {
+        depth[p] = 0.0f;                                  // :247
+        shadow[p] = 0;                                    // :259
+        win[p] = -1;                                      // record of the last shading fragment
+    }
     const int cnt = count[y];
-    const int *lst = list + (size_t)y * A.n;
-    for (int q = 0; q < cnt; ++q) {
-        const int t = lst[q];
-        const RastSpan s = spans[(size_t)t * A.H + y];
-        if (s.rx - 1 < x0 || s.lx > x0 + 63) continue;    // no fragment in this segment
-        const int i = x - s.lx;
-        if (!(x < A.W && i >= 0 && x < s.rx)) continue;   // :504, :573
-        const float zinv = s.lz + (s.sz * (float)i);      // :543
-        const cg_rtri T = tris[t];
-        if (T.color.x >= 0) {
-            if (zinv >= depth) {                          // :574
-                float X = s.lX + (s.sX * (float)i);
-                float Y = s.lY + (s.sY * (float)i);
-                D = illum_D(A, zinv, X, Y, v3(T.normal.x, T.normal.y, T.normal.z));
-                tri = t;
-                if (t == ft) {
-                    RastHdr h = hdr[t];
-                    if (h.fy == y && h.fx == x) tri |= 1 << 30;
+    const RowRec *rr = recs + (size_t)y * A.n;
+    // 64 records per round trip: lane q loads record base+q (coalesced), a
+    // ballot keeps those with a fragment in this segment, and the set bits are
+    // walked in ascending order (= triangle order) with readlane broadcasts.
+    // Shading is deferred: a later shading fragment overwrites every buffer
+    // the earlier one wrote (:580-585, :665), so only the last one per pixel
+    // is evaluated, after the walk -- bit-identical, far less work in the
+    // ordered loop.
+    for (int base = 0; base < cnt; base += 64) {
+        const int q = base + lane;
+        int mlx = 0, mrx = 0, msh = 0;
+        float mlz = 0.f, msz = 0.f;
+        bool ov = false;
+        if (q < cnt) {
+            const RowRec &mr = rr[q];
+            mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = mr.shadow;
+            ov = !(mrx - 1 < x0 || mlx > x0 + kFillPx - 1);
+        }
+        unsigned long long m = __ballot(ov);
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const int lx = __builtin_amdgcn_readlane(mlx, b);
+            const int rx = __builtin_amdgcn_readlane(mrx, b);
+            const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlz), b));
+            const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msz), b));
+            const int shd = __builtin_amdgcn_readlane(msh, b);
+#pragma unroll
+            for (int p = 0; p < kFillPerLane; ++p) {
+                const int x = x0 + lane + 64 * p;
+                const int i = x - lx;
+                if (!(x < A.W && i >= 0 && x < rx)) continue;          // :504, :573
+                const float zinv = lz + (sz * (float)i);               // :543
+                if (!shd) {
+                    if (zinv >= depth[p]) {                            // :574
+                        depth[p] = zinv;                               // :665
+                        win[p] = base + b;
+                    }
+                } else if (zinv > depth[p]) {                          // :668-669
+                    shadow[p] = 1;
                 }
-                depth = zinv;                             // :665
             }
-        } else if (zinv > depth) {                        // :668-669
-            shadow = 1;
         }
     }
-    if (x < A.W) {
-        size_t o = (size_t)y * A.W + x;
-        state[o] = make_float4(__int_as_float(tri), D.x, D.y, D.z);
-        if (depth_out) depth_out[o] = depth;
-        shadow_out[o] = shadow;
+#pragma unroll
+    for (int p = 0; p < kFillPerLane; ++p) {
+        const int x = x0 + lane + 64 * p;
+        if (x < A.W) {
+            int tri = -1;
+            vec3 D = v3(0.f, 0.f, 0.f);
+            if (win[p] >= 0) {
+                const RowRec r = rr[win[p]];
+                const int i = x - r.lx;
+                const float X = r.lX + (r.sX * (float)i);              // :547-548 numerators
+                const float Y = r.lY + (r.sY * (float)i);
+                D = illum_D(A, depth[p], X, Y, v3(r.nx, r.ny, r.nz));  // :580-585
+                tri = r.t | (x == r.first_x ? (1 << 30) : 0);
+            }
+            size_t o = (size_t)y * A.W + x;
+            state[o] = make_float4(__int_as_float(tri), D.x, D.y, D.z);
+            if (depth_out) depth_out[o] = depth[p];
+            shadow_out[o] = shadow[p];
+        }
     }
 }
 
@@ -413,10 +514,12 @@ int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_pa
     if (!hdr) return ctx_fail(c, e, "alloc hdr");
     float4 *state = (float4 *)ctx_buf(c, 3, npx * sizeof(float4), &e);
     if (!state) return ctx_fail(c, e, "alloc state");
-    // count[H] | first_tri | list[H*n]
-    int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16 + (size_t)H * nn) * sizeof(int), &e);
-    if (!misc) return ctx_fail(c, e, "alloc lists");
-    int *count = misc, *first_tri = misc + H, *list = misc + H + 16;
+    // count[H] | first_tri
+    int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16) * sizeof(int), &e);
+    if (!misc) return ctx_fail(c, e, "alloc counts");
+    int *count = misc, *first_tri = misc + H;
+    RowRec *recs = (RowRec *)ctx_buf(c, 0 + 8, (size_t)H * nn * sizeof(RowRec), &e);
+    if (!recs) return ctx_fail(c, e, "alloc row records");
     int32_t *shadow = d_shadow;
     if (!shadow) {
         shadow = (int32_t *)ctx_buf(c, 6, npx * sizeof(int32_t), &e);
@@ -441,12 +544,14 @@ int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_pa
                            hdr, first_tri);
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
     }
-    hipLaunchKernelGGL(rast_rowlist_kernel, dim3((H + 3) / 4), dim3(256), 0, st, hdr, n, H, list, count);
-    if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rowlist launch");
-    const int segs = (W + 63) / 64;
-    hipLaunchKernelGGL(rast_fill_kernel, dim3((segs * H + 3) / 4), dim3(256), 0, st, d_tris, A, spans,
-                       hdr, list, count, first_tri, state, d_depth, shadow);
+    hipLaunchKernelGGL(rast_rows_kernel, dim3((H + 3) / 4), dim3(256), 0, st, d_tris, A, spans, hdr,
+                       first_tri, recs, count);
+    if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rows launch");
+    const int fsegs = (W + kFillPx - 1) / kFillPx;
+    hipLaunchKernelGGL(rast_fill_kernel, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
+                       state, d_depth, shadow);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
+    const int segs = (W + 63) / 64;
     hipLaunchKernelGGL(rast_post_kernel, dim3(segs, (H + 3) / 4), dim3(256), 0, st, d_tris, A, state,
                        shadow, d_argb);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");

@@ -61,7 +61,7 @@ struct cg_ctx {
     int n_tris = -1, n_sph = 0;
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d;
     // RAST scratch (owned by cg_rast.hip)
-    DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount;
+    DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs;
 };
 
 namespace cg {
@@ -78,6 +78,7 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
     case 5: b = &c->rdepth; break;
     case 6: b = &c->rshadow; break;
     case 7: b = &c->rcount; break;
+    case 8: b = &c->rrecs; break;
     default: *e = hipErrorInvalidValue; return nullptr;
     }
     *e = b->ensure(bytes);
@@ -98,6 +99,7 @@ void rast_release(cg_ctx *c)
 {
     c->rtris.release(); c->rhdr.release(); c->rspan.release(); c->rpix.release();
     c->rargb.release(); c->rdepth.release(); c->rshadow.release(); c->rcount.release();
+    c->rrecs.release();
 }
 }  // namespace cg
 
