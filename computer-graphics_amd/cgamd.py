@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libcgamd.so")
+LIB_PATH = os.environ.get("CGAMD_LIB") or os.path.join(HERE, "_build", "libcgamd.so")
 
 CG_OK, CG_E_INVALID, CG_E_NODEVICE, CG_E_HIP, CG_E_NOSCENE, CG_E_CAPACITY = 0, -1, -2, -3, -4, -5
 

@@ -319,6 +319,9 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
         }
     }
     vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+#ifdef CG_ABLATE_SPHERE
+    if (0)
+#endif
     for (int k = 0; k < F.n_sph; ++k) {                       // :341-355
         float t;
         if (sphere_intersect(sph[k], s3, d, t)) {
@@ -373,6 +376,9 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
         float v = detV / det;
         if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) return true;
     }
+#ifdef CG_ABLATE_SPHERE
+    if (0)
+#endif
     for (int k = 0; k < F.n_sph; ++k) {
         float t;
         if (sphere_intersect(sph[k], start, d, t) && t < rmag) return true;
@@ -394,7 +400,9 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     float rmag = (float)sqrt((r0 + r1) + r2);                            // :371
     vec3 normal = hit_normal(shade, sph, bi, pos);
     vec3 origin = pos + normal * 0.00001f;                              // :394
+#ifndef CG_ABLATE_SHADOW
     if (shadowed<CULL>(F, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
+#endif
     vec3 nd = normalize(r);                                              // :400
     float a = dot(nd, normal);                                           // :403
     const float b = (float)(4 * M_PI);                                   // :404
@@ -452,8 +460,11 @@ __device__ __forceinline__ int shard_row(const RtFrame &F, int L)
 
 // Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
 // one certificate mask per wave (lane k certifies triangle k).
+#ifndef CG_RT_MIN_WAVES
+#define CG_RT_MIN_WAVES 5   // 92 VGPRs: 5 waves per SIMD without spills (measured best)
+#endif
 template <bool CULL>
-__global__ __launch_bounds__(kRtThreads) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                               const RtShade *__restrict__ shade,
                                                               const RtSphere *__restrict__ sph,
                                                               uint32_t *__restrict__ out)
