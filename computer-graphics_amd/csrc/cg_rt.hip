@@ -429,7 +429,7 @@ __device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lp, vec3 p
     vec3 r = lp - pos;                                                   // :370/:373
     vec3 S = pos + normal * 0.00001f;                                    // :394
     double px = (double)S.x - lp.x + r.x, py = (double)S.y - lp.y + r.y, pz = (double)S.z - lp.z + r.z;
-    float pb = (float)(sqrt(px * px + py * py + pz * pz) * (1.0 + 1e-6) + 1e-30);
+    float pb = (float)((fabs(px) + fabs(py) + fabs(pz)) * (1.0 + 1e-6) + 1e-30);   // L1 >= L2
     b.lo[0] = fminf(b.lo[0], r.x); b.hi[0] = fmaxf(b.hi[0], r.x);
     b.lo[1] = fminf(b.lo[1], r.y); b.hi[1] = fmaxf(b.hi[1], r.y);
     b.lo[2] = fminf(b.lo[2], r.z); b.hi[2] = fmaxf(b.hi[2], r.z);
