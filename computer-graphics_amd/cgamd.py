@@ -96,6 +96,9 @@ _SIGS = {
     "cg_rast_render": (C.c_int, [P, C.POINTER(RTri), C.c_int, C.POINTER(RastParams), Vec4, P, P, P,
                                  C.POINTER(Stats)]),
     "cg_rast_render_device": (C.c_int, [P, P, C.c_int, C.POINTER(RastParams), Vec4, P, P, P, P]),
+    "cg_rast_set_scene": (C.c_int, [P, C.POINTER(RTri), C.c_int, C.POINTER(RTri), C.c_int]),
+    "cg_rast_draw": (C.c_int, [P, C.POINTER(RastParams), P, P, P, C.POINTER(Stats)]),
+    "cg_rast_draw_device": (C.c_int, [P, C.POINTER(RastParams), P, P, P, P]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -285,6 +288,29 @@ class Context:
             depth.ctypes.data_as(P) if depth is not None else None,
             shadow.ctypes.data_as(P) if shadow is not None else None, C.byref(st)), "cg_rast_render")
         return argb, depth, shadow, st
+
+    def rast_set_scene(self, room=None, nr=None, boxes=None, nb=None):
+        if room is None:
+            room, nr, boxes, nb = rast_scene()
+        self._check(self.lib.cg_rast_set_scene(self.h, room, nr, boxes, nb), "cg_rast_set_scene")
+
+    def rast_draw(self, params, want_depth=True, want_shadow=True):
+        """Whole Draw on the device (geometry + fill + post)."""
+        npx = params.width * params.height
+        argb = np.zeros(npx, np.uint32)
+        depth = np.zeros(npx, np.float32) if want_depth else None
+        shadow = np.zeros(npx, np.int32) if want_shadow else None
+        st = Stats()
+        self._check(self.lib.cg_rast_draw(
+            self.h, C.byref(params), argb.ctypes.data_as(P),
+            depth.ctypes.data_as(P) if depth is not None else None,
+            shadow.ctypes.data_as(P) if shadow is not None else None, C.byref(st)), "cg_rast_draw")
+        return argb, depth, shadow, st
+
+    def rast_draw_device(self, params, d_argb, d_depth=None, d_shadow=None, stream=None):
+        self._check(self.lib.cg_rast_draw_device(self.h, C.byref(params), P(d_argb), P(d_depth) if d_depth else None,
+                                                 P(d_shadow) if d_shadow else None, P(stream) if stream else None),
+                    "cg_rast_draw_device")
 
     def rast_render_device(self, d_tris, n, params, light, d_argb, d_depth=None, d_shadow=None,
                            stream=None):

@@ -43,6 +43,7 @@ struct RastArgs {
     float lp[3];            // lightPower
     float ind_first;        // indirectLightPowerPerArea at frame start
     int want_first;         // ind_first differs from the steady-state 0.2
+    const cg_vec4 *d_light; // if set, the light comes from the device geometry
 };
 
 struct RastHdr {
@@ -120,14 +121,30 @@ __device__ __forceinline__ unsigned long long key_right(int x, unsigned seq)
     return ((unsigned long long)((unsigned)x ^ 0x80000000u) << 32) | (unsigned long long)seq;
 }
 
+__device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs &A, RastSpan *__restrict__ spans,
+                               RastHdr *__restrict__ hdr, int *__restrict__ first_tri, int t,
+                               unsigned long long *lkey, unsigned long long *rkey, unsigned long long &fkey);
+
+// One workgroup per clipped triangle (grid-stride; the count may live on the
+// device when the geometry ran there).
 __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
-    const cg_rtri *__restrict__ tris, RastArgs A, RastSpan *__restrict__ spans,
+    const cg_rtri *__restrict__ tris, RastArgs A, const int *__restrict__ n_dev, RastSpan *__restrict__ spans,
     RastHdr *__restrict__ hdr, int *__restrict__ first_tri)
 {
     __shared__ unsigned long long lkey[kRastMaxRows];
     __shared__ unsigned long long rkey[kRastMaxRows];
     __shared__ unsigned long long fkey;
-    const int t = blockIdx.x;
+    const int n = n_dev ? min(*n_dev, A.n) : A.n;
+    for (int t = blockIdx.x; t < n; t += gridDim.x) {
+        rast_setup_one(tris, A, spans, hdr, first_tri, t, lkey, rkey, fkey);
+        __syncthreads();
+    }
+}
+
+__device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs &A, RastSpan *__restrict__ spans,
+                               RastHdr *__restrict__ hdr, int *__restrict__ first_tri, int t,
+                               unsigned long long *lkey, unsigned long long *rkey, unsigned long long &fkey)
+{
     const cg_rtri T = tris[t];
     Pix vp[3] = {vertex_shader(A, T.v0), vertex_shader(A, T.v1), vertex_shader(A, T.v2)};
     int mx = -INT_MAX, mn = INT_MAX;                        // :434-447
@@ -161,38 +178,27 @@ __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
     // Edge samples -> rows (:466-497).  Rows outside the screen never shade.
     for (int ei = 0; ei < 3; ++ei) {
         Edge e = make_edge(vp[ei], vp[ei == 2 ? 0 : ei + 1]);
-        // y is monotone in j, so within a wave the samples of one row are
-        // contiguous lanes: a segmented scan leaves the row's min/max key in
-        // the segment's last lane, which alone touches LDS (a near-horizontal
-        // edge otherwise serialises ~N atomics on one row).
+        // Only a sample that can still win its row issues an LDS atomic: the
+        // left winner is the minimum x with the latest sequence among equals,
+        // so a sample whose previous same-row neighbour has a smaller x, or
+        // whose next same-row neighbour has a smaller-or-equal x, cannot win
+        // (mirror for the right).  Exact for any order; a near-horizontal
+        // edge then issues a few atomics per wave instead of 64 on one row.
         const int lane = threadIdx.x & 63;
         for (int jb = 0; jb < e.n; jb += kSetupThreads) {
             const int j = jb + (int)threadIdx.x;
             const bool in = j < e.n;
             int y = in ? edge_y(e, j) : INT_MIN;
             const bool vis = in && y >= ylo && y <= yhi;   // also covers :485's y - min >= 0
-            if (!vis) y = INT_MIN + 1 + lane;              // never merges with a real row
-            unsigned long long kl = ~0ull, kr = 0ull;
+            if (!vis) y = INT_MIN + 1 + lane;              // never equals a real row
+            const int x = vis ? edge_x(e, j) : 0;
+            const int yp = __shfl_up(y, 1, 64), xp = __shfl_up(x, 1, 64);
+            const int yn = __shfl_down(y, 1, 64), xn = __shfl_down(x, 1, 64);
+            const bool hp = lane > 0 && yp == y, hn = lane < 63 && yn == y;
             if (vis) {
-                int x = edge_x(e, j);
-                unsigned seq = ((unsigned)ei << 30) | (unsigned)j;
-                kl = key_left(x, seq);
-                kr = key_right(x, seq);
-            }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                int yo = __shfl_up(y, o, 64);
-                unsigned long long lo = __shfl_up(kl, o, 64), ro = __shfl_up(kr, o, 64);
-                if (lane >= o && yo == y) {
-                    kl = lo < kl ? lo : kl;
-                    kr = ro > kr ? ro : kr;
-                }
-            }
-            int yn = __shfl_down(y, 1, 64);
-            bool last = lane == 63 || yn != y;
-            if (vis && last) {
-                atomicMin(&lkey[y - ylo], kl);
-                atomicMax(&rkey[y - ylo], kr);
+                const unsigned seq = ((unsigned)ei << 30) | (unsigned)j;
+                if (!(hp && xp < x) && !(hn && xn <= x)) atomicMin(&lkey[y - ylo], key_left(x, seq));
+                if (!(hp && xp > x) && !(hn && xn >= x)) atomicMax(&rkey[y - ylo], key_right(x, seq));
             }
         }
     }
@@ -274,6 +280,7 @@ struct alignas(16) RowRec {
 static_assert(sizeof(RowRec) == 64, "RowRec");
 
 __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
+                                                       const int *__restrict__ n_dev,
                                                        const RastSpan *__restrict__ spans,
                                                        const RastHdr *__restrict__ hdr,
                                                        const int *__restrict__ first_tri,
@@ -283,13 +290,14 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
     const int lane = threadIdx.x & 63;
     if (y >= A.H) return;
     const int ft = A.want_first ? *first_tri : INT_MAX;
+    const int n = n_dev ? min(*n_dev, A.n) : A.n;
     int c = 0;
-    for (int base = 0; base < A.n; base += 64) {
+    for (int base = 0; base < n; base += 64) {
         const int t = base + lane;
         bool keep = false;
         RastSpan sp;
         RastHdr h;
-        if (t < A.n) {
+        if (t < n) {
             h = hdr[t];
             if (h.ylo <= y && y <= h.yhi) {
                 sp = spans[(size_t)t * A.H + y];
@@ -342,12 +350,17 @@ __device__ __forceinline__ vec3 illum_D(const RastArgs &A, float zinv, float X, 
 constexpr int kFillPx = 256;
 constexpr int kFillPerLane = kFillPx / 64;
 
-__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec *__restrict__ recs,
+__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRec *__restrict__ recs,
                                                        const int *__restrict__ count,
                                                        float4 *__restrict__ state,
                                                        float *__restrict__ depth_out,
                                                        int32_t *__restrict__ shadow_out)
 {
+    RastArgs A = A0;
+    if (A.d_light) {                                      // light from the device geometry (:223)
+        const cg_vec4 L = *A.d_light;
+        A.light[0] = L.x; A.light[1] = L.y; A.light[2] = L.z;
+    }
     const int segs = (A.W + kFillPx - 1) / kFillPx;
     // wave-uniform by construction; readfirstlane lets the compiler keep the
     // record walk on the scalar unit (s_load per record, uniform branches)
@@ -499,9 +512,53 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
     argb[o] = put_pixel(val);
 }
 
+hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
+                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_scr0,
+                                cg_rtri *d_scr1, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st);
+
+// The fill + post pipeline.  Either the triangle count is known on the host
+// (n_dev == nullptr, n = count) or it lives on the device (n_dev, n = capacity,
+// light read from d_light).
+static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_dev, const cg_rast_params *p,
+                         cg_vec4 light, const cg_vec4 *d_light, uint32_t *d_argb, float *d_depth,
+                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open);
+
 int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_params *p, cg_vec4 light,
                        uint32_t *d_argb, float *d_depth, int32_t *d_shadow, hipStream_t st,
                        cg_stats *stats)
+{
+    return rast_pipeline(c, d_tris, n, nullptr, p, light, nullptr, d_argb, d_depth, d_shadow, st, stats, false);
+}
+
+// Whole rasteriser Draw on the device: geometry (shadow volumes + clip) then
+// fill + post.  room/boxes are device pointers (cg_rast_set_scene).
+int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri *d_boxes, int n_boxes,
+                     const cg_rast_params *p, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
+                     hipStream_t st, cg_stats *stats, int **n_out)
+{
+    if (p->width <= 2 || p->height <= 2 || p->height > kRastMaxRows || p->focal == 0.0f) return CG_E_INVALID;
+    const int n_in = n_room + 7 * n_boxes;
+    // planes 1-4 and 6 can each split a triangle in two; plane 5 never does
+    const int cap = n_in > 0 ? 32 * n_in : 1;
+    hipError_t e;
+    cg_rtri *tris = (cg_rtri *)ctx_buf(c, 0, 3 * (size_t)cap * sizeof(cg_rtri), &e);   // out + 2 scratch lists
+    if (!tris) return ctx_fail(c, e, "alloc clipped triangles");
+    int *geo = (int *)ctx_buf(c, 9, 64, &e);               // [0] count, [4..7] light
+    if (!geo) return ctx_fail(c, e, "alloc geometry header");
+    hipEvent_t e0, e1;
+    ctx_events(c, &e0, &e1);
+    if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
+    if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, tris + 2 * (size_t)cap, cap, geo, (cg_vec4 *)(geo + 4), st)) !=
+        hipSuccess)
+        return ctx_fail(c, e, "rast_geometry launch");
+    if (n_out) *n_out = geo;
+    return rast_pipeline(c, tris, cap, geo, p, cg_vec4{0, 0, 0, 1}, (const cg_vec4 *)(geo + 4), d_argb, d_depth,
+                         d_shadow, st, stats, true);
+}
+
+static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_dev, const cg_rast_params *p,
+                         cg_vec4 light, const cg_vec4 *d_light, uint32_t *d_argb, float *d_depth,
+                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open)
 {
     if (p->width <= 2 || p->height <= 2 || p->height > kRastMaxRows) return CG_E_INVALID;
     const int W = p->width, H = p->height;
@@ -514,11 +571,10 @@ int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_pa
     if (!hdr) return ctx_fail(c, e, "alloc hdr");
     float4 *state = (float4 *)ctx_buf(c, 3, npx * sizeof(float4), &e);
     if (!state) return ctx_fail(c, e, "alloc state");
-    // count[H] | first_tri
-    int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16) * sizeof(int), &e);
+    int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16) * sizeof(int), &e);   // count[H] | first_tri
     if (!misc) return ctx_fail(c, e, "alloc counts");
     int *count = misc, *first_tri = misc + H;
-    RowRec *recs = (RowRec *)ctx_buf(c, 0 + 8, (size_t)H * nn * sizeof(RowRec), &e);
+    RowRec *recs = (RowRec *)ctx_buf(c, 8, (size_t)H * nn * sizeof(RowRec), &e);
     if (!recs) return ctx_fail(c, e, "alloc row records");
     int32_t *shadow = d_shadow;
     if (!shadow) {
@@ -534,17 +590,19 @@ int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_pa
     A.lp[0] = p->light_power.x; A.lp[1] = p->light_power.y; A.lp[2] = p->light_power.z;
     A.ind_first = p->indirect_first;
     A.want_first = p->indirect_first != 0.2f * 1;
+    A.d_light = d_light;
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
-    if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
+    if (stats && !events_open && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
     if (A.want_first && (e = hipMemsetAsync(first_tri, 0x7f, sizeof(int), st)) != hipSuccess)
         return ctx_fail(c, e, "memset");
     if (n > 0) {
-        hipLaunchKernelGGL(rast_setup_kernel, dim3(n), dim3(kSetupThreads), 0, st, d_tris, A, spans,
-                           hdr, first_tri);
+        const int grid = n < 512 ? n : 512;                  // 2 workgroups/CU (64 KB LDS each)
+        hipLaunchKernelGGL(rast_setup_kernel, dim3(grid), dim3(kSetupThreads), 0, st, d_tris, A, n_dev, spans, hdr,
+                           first_tri);
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
     }
-    hipLaunchKernelGGL(rast_rows_kernel, dim3((H + 3) / 4), dim3(256), 0, st, d_tris, A, spans, hdr,
+    hipLaunchKernelGGL(rast_rows_kernel, dim3((H + 3) / 4), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,
                        first_tri, recs, count);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rows launch");
     const int fsegs = (W + kFillPx - 1) / kFillPx;
@@ -557,7 +615,7 @@ int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_pa
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");
     if (stats && (e = hipEventRecord(e1, st)) != hipSuccess) return ctx_fail(c, e, "event");
     if (stats) {
-        stats->n_tris = n;
+        stats->n_tris = n_dev ? -1 : n;
         stats->n_spans = 0;
     }
     return CG_OK;

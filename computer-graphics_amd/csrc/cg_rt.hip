@@ -513,7 +513,9 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
             }
         }
     }
-    unsigned long long smask0 = ~0ull;
+    // lights >= 1 test every triangle (the mask walk must stop at n_tris)
+    const unsigned long long all_tris = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
+    unsigned long long smask0 = all_tris;
     if (CULL && F.cull_shadow && F.n_lights > 0) smask0 = shadow_mask_of(F, tc, sb, lp0, lane);
     if (active) {
         // Pass 2: shading in the reference's order (:143-157)
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
             valid = true;
             vec3 oc = object_colour(shade, sph, bi);
             for (int l = 0; l < F.n_lights; ++l)                                          // :151-153
-                pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, l == 0 ? smask0 : ~0ull);
+                pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, l == 0 ? smask0 : all_tris);
             pc = pc + (oc * ind);                                                         // :156
         }
         px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));             // :160-166

@@ -25,6 +25,9 @@ hipError_t launch_rt_probe_direct_light(const RtFrame &, const RtTri *, const Rt
 int rast_render_device(cg_ctx *ctx, const cg_rtri *d_tris, int n, const cg_rast_params *p,
                        cg_vec4 light, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
                        hipStream_t st, cg_stats *stats);
+int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri *d_boxes, int n_boxes,
+                     const cg_rast_params *p, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
+                     hipStream_t st, cg_stats *stats, int **n_out);
 void rast_release(cg_ctx *ctx);
 }  // namespace cg
 
@@ -61,7 +64,8 @@ struct cg_ctx {
     int n_tris = -1, n_sph = 0;
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d;
     // RAST scratch (owned by cg_rast.hip)
-    DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs;
+    DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
+    int n_room = -1, n_boxes = 0;
 };
 
 namespace cg {
@@ -79,6 +83,7 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
     case 6: b = &c->rshadow; break;
     case 7: b = &c->rcount; break;
     case 8: b = &c->rrecs; break;
+    case 9: b = &c->rgeo; break;
     default: *e = hipErrorInvalidValue; return nullptr;
     }
     *e = b->ensure(bytes);
@@ -99,7 +104,7 @@ void rast_release(cg_ctx *c)
 {
     c->rtris.release(); c->rhdr.release(); c->rspan.release(); c->rpix.release();
     c->rargb.release(); c->rdepth.release(); c->rshadow.release(); c->rcount.release();
-    c->rrecs.release();
+    c->rrecs.release(); c->rgeo.release(); c->rroom.release(); c->rboxes.release();
 }
 }  // namespace cg
 
@@ -398,6 +403,74 @@ extern "C" int cg_rast_render(cg_ctx *c, const cg_rtri *tris, int n, const cg_ra
     if (n) CG_TRY(c, hipMemcpyAsync(d_tris, tris, (size_t)n * sizeof(cg_rtri), hipMemcpyHostToDevice, c->stream), "upload tris");
     int rc = rast_render_device(c, d_tris, n, p, light, d_argb, d_depth, d_shadow, c->stream, stats);
     if (rc) return rc;
+    CG_TRY(c, hipMemcpyAsync(argb, d_argb, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h argb");
+    if (depth) CG_TRY(c, hipMemcpyAsync(depth, d_depth, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h depth");
+    if (shadow) CG_TRY(c, hipMemcpyAsync(shadow, d_shadow, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h shadow");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "rast frame");
+    if (stats) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->n_tris = n;
+    }
+    return CG_OK;
+}
+
+extern "C" int cg_rast_set_scene(cg_ctx *c, const cg_rtri *room, int n_room, const cg_rtri *boxes, int n_boxes)
+{
+    if (!c || n_room < 0 || n_boxes < 0 || (n_room && !room) || (n_boxes && !boxes) || n_room + 7 * n_boxes > 4096)
+        return CG_E_INVALID;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    CG_TRY(c, c->rroom.ensure((size_t)(n_room > 0 ? n_room : 1) * sizeof(cg_rtri)), "alloc room");
+    CG_TRY(c, c->rboxes.ensure((size_t)(n_boxes > 0 ? n_boxes : 1) * sizeof(cg_rtri)), "alloc boxes");
+    if (n_room)
+        CG_TRY(c, hipMemcpyAsync(c->rroom.p, room, (size_t)n_room * sizeof(cg_rtri), hipMemcpyHostToDevice, c->stream), "upload room");
+    if (n_boxes)
+        CG_TRY(c, hipMemcpyAsync(c->rboxes.p, boxes, (size_t)n_boxes * sizeof(cg_rtri), hipMemcpyHostToDevice, c->stream), "upload boxes");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "scene upload");
+    c->n_room = n_room;
+    c->n_boxes = n_boxes;
+    return CG_OK;
+}
+
+extern "C" int cg_rast_draw_device(cg_ctx *c, const cg_rast_params *p, uint32_t *d_argb, float *d_depth,
+                                   int32_t *d_shadow, void *stream)
+{
+    if (!c || !p || !d_argb) return CG_E_INVALID;
+    if (c->n_room < 0) {
+        c->err = "draw before cg_rast_set_scene";
+        return CG_E_NOSCENE;
+    }
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    return rast_draw_device(c, (const cg_rtri *)c->rroom.p, c->n_room, (const cg_rtri *)c->rboxes.p, c->n_boxes, p,
+                            d_argb, d_depth, d_shadow, stream ? (hipStream_t)stream : c->stream, nullptr, nullptr);
+}
+
+extern "C" int cg_rast_draw(cg_ctx *c, const cg_rast_params *p, uint32_t *argb, float *depth, int32_t *shadow,
+                            cg_stats *stats)
+{
+    if (!c || !p || !argb || p->width <= 2 || p->height <= 2) return CG_E_INVALID;
+    if (c->n_room < 0) {
+        c->err = "draw before cg_rast_set_scene";
+        return CG_E_NOSCENE;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    size_t npx = (size_t)p->width * p->height;
+    hipError_t e;
+    uint32_t *d_argb = (uint32_t *)ctx_buf(c, 4, npx * 4, &e);
+    if (!d_argb) return ctx_fail(c, e, "alloc argb");
+    float *d_depth = (float *)ctx_buf(c, 5, npx * 4, &e);
+    if (!d_depth) return ctx_fail(c, e, "alloc depth");
+    int32_t *d_shadow = (int32_t *)ctx_buf(c, 6, npx * 4, &e);
+    if (!d_shadow) return ctx_fail(c, e, "alloc shadow");
+    int *d_n = nullptr;
+    int rc = rast_draw_device(c, (const cg_rtri *)c->rroom.p, c->n_room, (const cg_rtri *)c->rboxes.p, c->n_boxes, p,
+                              d_argb, d_depth, d_shadow, c->stream, stats, &d_n);
+    if (rc) return rc;
+    int n = 0;
+    CG_TRY(c, hipMemcpyAsync(&n, d_n, sizeof(int), hipMemcpyDeviceToHost, c->stream), "d2h count");
     CG_TRY(c, hipMemcpyAsync(argb, d_argb, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h argb");
     if (depth) CG_TRY(c, hipMemcpyAsync(depth, d_depth, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h depth");
     if (shadow) CG_TRY(c, hipMemcpyAsync(shadow, d_shadow, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h shadow");

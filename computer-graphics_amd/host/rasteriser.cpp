@@ -4,9 +4,10 @@
 // Same globals (focalLength, cameraPos, yaw, R, sceneCoordinatesLightPos,
 // lightPower, indirectLightPowerPerArea, originalroom/originalbox), same
 // main loop and Draw(screen*) -> screen->buffer, same screenshot.bmp.  The
-// host geometry (camera space, shadow volumes, clipping) runs on the host as
-// in the reference (cg_rast_prepare); the fill and post-pass run on the GPU
-// (cg_rast_render).  Scripted keys as in Update() (:311-417): w s a d q e =
+// whole Draw runs on the GPU (cg_rast_draw): geometry (camera space, shadow
+// volumes, clipping), span setup, ordered fill and post-pass.  (cg_rast_prepare
+// + cg_rast_render keep the host-geometry split available.)  Scripted keys as
+// in Update() (:311-417): w s a d q e =
 // light, 1 2 = indirect, U D L R z x = camera, n m = yaw, f g = focal,
 // ESC = 'X'.
 //
@@ -35,7 +36,6 @@ vec3 lightPower = 20.0f * vec3(1, 1, 1);                      // :53
 vec3 indirectLightPowerPerArea = 0.15f * vec3(1, 1, 1);       // :54
 vector<rast::Triangle> originalroom;                          // :84
 vector<rast::Triangle> originalbox;                           // :85
-vector<rast::Triangle> clippedTriangles;                      // :86
 
 static cg_ctx *g_ctx = nullptr;
 static string g_keys;
@@ -60,20 +60,12 @@ void Draw(screen *screen)
                             sceneCoordinatesLightPos.z, sceneCoordinatesLightPos.w};
     p.light_power = cg_vec3{lightPower.x, lightPower.y, lightPower.z};
     p.indirect_first = indirectLightPowerPerArea.x;
-    const cg_rtri *room = reinterpret_cast<const cg_rtri *>(originalroom.data());
-    const cg_rtri *box = reinterpret_cast<const cg_rtri *>(originalbox.data());
-    cg_vec4 light;
-    int n = cg_rast_prepare(&p, room, (int)originalroom.size(), box, (int)originalbox.size(),
-                            nullptr, 0, &light);
-    if (n < 0) die(n, "cg_rast_prepare");
-    clippedTriangles.resize(n);
-    n = cg_rast_prepare(&p, room, (int)originalroom.size(), box, (int)originalbox.size(),
-                        reinterpret_cast<cg_rtri *>(clippedTriangles.data()), n, &light);
-    int rc = cg_rast_render(g_ctx, reinterpret_cast<const cg_rtri *>(clippedTriangles.data()), n, &p,
-                            light, screen->buffer, nullptr, nullptr, nullptr);
-    if (rc) die(rc, "cg_rast_render");
+    // geometry (shadow volumes + clip), fill and post-pass all on the GPU
+    cg_stats st;
+    int rc = cg_rast_draw(g_ctx, &p, screen->buffer, nullptr, nullptr, &st);
+    if (rc) die(rc, "cg_rast_draw");
     // PixelShader leaves the global at 0.2 after the first shaded fragment (:585)
-    if (n > 0) indirectLightPowerPerArea = 0.2f * vec3(1, 1, 1);
+    if (st.n_tris > 0) indirectLightPowerPerArea = 0.2f * vec3(1, 1, 1);
 }
 
 // skeleton.cpp:311-417 with scripted keys
@@ -127,6 +119,9 @@ int main(int argc, char *argv[])
     if (rc) die(rc, "cg_create");
     screen *screen = InitializeSDL(SCREEN_WIDTH, SCREEN_HEIGHT, false);
     rast::LoadTestModel(originalroom, originalbox);          // :131
+    rc = cg_rast_set_scene(g_ctx, reinterpret_cast<const cg_rtri *>(originalroom.data()), (int)originalroom.size(),
+                           reinterpret_cast<const cg_rtri *>(originalbox.data()), (int)originalbox.size());
+    if (rc) die(rc, "cg_rast_set_scene");
     while (Update()) {
         Draw(screen);
         SDL_Renderframe(screen);

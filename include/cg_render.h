@@ -154,6 +154,16 @@ int cg_rast_render_device(cg_ctx *ctx, const cg_rtri *d_tris, int n, const cg_ra
                           cg_vec4 light, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
                           void *stream);
 
+/* Whole rasteriser Draw on the device (skeleton.cpp:203-308): upload the
+ * LoadTestModel room/boxes once, then each frame runs the geometry
+ * (shadow volumes, rotation, clip) AND the fill + post-pass on the GPU --
+ * the same lists cg_rast_prepare builds on the host. */
+int cg_rast_set_scene(cg_ctx *ctx, const cg_rtri *room, int n_room, const cg_rtri *boxes, int n_boxes);
+int cg_rast_draw(cg_ctx *ctx, const cg_rast_params *p, uint32_t *argb, float *depth, int32_t *shadow,
+                 cg_stats *stats);
+int cg_rast_draw_device(cg_ctx *ctx, const cg_rast_params *p, uint32_t *d_argb, float *d_depth,
+                        int32_t *d_shadow, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,3 +53,16 @@ def test_rast_empty_list(ctx):
     img = argb.reshape(48, 64)
     assert np.all(img[1:-1, 1:-1] == 0x80000000) and not img[0].any()
     assert not depth.any() and not shadow.any()
+
+
+@pytest.mark.parametrize("name", list(mg.rast_configs()))
+def test_rast_device_geometry_draw_matches_golden(ctx, golden, name):
+    """cg_rast_draw: geometry (shadow volumes + clip) on the GPU too."""
+    cfg = mg.rast_configs()[name]
+    ctx.rast_set_scene()
+    argb, depth, shadow, st = ctx.rast_draw(_params(cfg))
+    e = golden["rast"][name]
+    assert st.n_tris == e["counters"]["n_tris"]
+    assert mg.sha(shadow) == e["shadow_sha256"], "shadow plane"
+    assert mg.sha(depth) == e["depth_sha256"], "depth plane"
+    assert mg.sha(argb) == e["argb_sha256"], "colour plane"
