@@ -79,6 +79,8 @@ _SIGS = {
     "cg_last_error": (C.c_char_p, [P]),
     "cg_device_count": (C.c_int, []),
     "cg_rt_load_test_model": (C.c_int, [C.POINTER(Tri), C.c_int, C.POINTER(Sphere)]),
+    "cg_rt_area_lights": (C.c_int, [C.POINTER(Light), C.c_float, C.c_int, C.POINTER(Light), C.c_int]),
+    "cg_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(Tri)]),
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
@@ -152,6 +154,28 @@ def default_lights():
     f = float(np.float32(14.0) * np.float32(1.0))
     arr[0].colour = Vec3(f, f, f)
     return arr
+
+
+def area_lights(centre=None, side=0.1, n=8):
+    """C4 soft-shadow light set (cg_rt_area_lights): n*n lights, default around
+    the reference light (skeleton.cpp:86-89)."""
+    lib = load()
+    c = default_lights()[0] if centre is None else centre
+    out = (Light * (n * n))()
+    k = lib.cg_rt_area_lights(C.byref(c), side, n, out, n * n)
+    if k != n * n:
+        raise RuntimeError(f"cg_rt_area_lights failed: {k}")
+    return out
+
+
+def random_scene(n, seed=0x5EED):
+    """C5 random triangles (cg_rt_random_scene): ctypes Tri array of n."""
+    lib = load()
+    tris = (Tri * max(n, 1))()
+    k = lib.cg_rt_random_scene(seed, n, tris)
+    if k != n:
+        raise RuntimeError(f"cg_rt_random_scene failed: {k}")
+    return tris
 
 
 def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,

@@ -9,7 +9,7 @@
 
 namespace cg {
 
-constexpr int kMaxLights = 8;
+constexpr int kMaxLights = 4096;   // lights live in a device buffer (scalar loads)
 constexpr int kRtTileW = 32;   // RT workgroup: 4 waves, each an 8x8 pixel tile
 constexpr int kRtTileH = 8;
 constexpr int kRtThreads = 256;
@@ -37,6 +37,12 @@ struct alignas(16) RtShade {
     float cr, cg, cb, pad;  // Triangle::color
 };
 
+// Light (skeleton.cpp:47-50), 32 B.
+struct alignas(16) RtLight {
+    float x, y, z, w;
+    float r, g, b, pad;
+};
+
 struct RtSphere {
     float cx, cy, cz, r2;   // centre, radiusSquared
     float cr, cg, cb, pad;  // color
@@ -51,8 +57,11 @@ struct RtFrame {
     int n_tris, n_sph, n_lights;
     int rank, nranks, stripe_h, rows_out;
     int cull_primary, cull_shadow;   // certificates on (CG_RT_CULL env: 0 none, 1 primary, 2 both)
-    float lpos[kMaxLights][4];
-    float lcol[kMaxLights][3];
+    const RtLight *lights;           // n_lights entries, device memory
+    // The light set as the shadow certificate sees it: componentwise min/max
+    // of the positions, a centre lc and rho >= max_k |L_k - lc| (FP64, rounded up).
+    float lmin[3], lmax[3], lc[3];
+    double lrho;
 };
 
 // ---- RAST --------------------------------------------------------------

@@ -205,7 +205,7 @@ struct ShadowBox {
     float pn;             // bound on |S - L + d| over the casting lanes
 };
 
-__device__ bool cull_shadow(const RtTri &c, vec3 L, const ShadowBox &B)
+__device__ bool cull_shadow(const RtTri &c, vec3 L, double rho, const ShadowBox &B)
 {
     const double eps = 5.9604644775390625e-8;   // 2^-24
     const double g = 16.0 * eps;
@@ -230,7 +230,7 @@ __device__ bool cull_shadow(const RtTri &c, vec3 L, const ShadowBox &B)
     double Dz = fmax(fabs((double)B.lo[2]), fabs((double)B.hi[2]));
     double dn = sqrt(Dx * Dx + Dy * Dy + Dz * Dz);
     // |s| <= |a| + |d| + |p| componentwise; p also absorbs s's own rounding
-    double Sx = fabs(ax) + Dx + B.pn, Sy = fabs(ay) + Dy + B.pn, Sz = fabs(az) + Dz + B.pn;
+    double Sx = fabs(ax) + rho + Dx + B.pn, Sy = fabs(ay) + rho + Dy + B.pn, Sz = fabs(az) + rho + Dz + B.pn;
     double pn = (double)B.pn + eps * sqrt(Sx * Sx + Sy * Sy + Sz * Sz) + 1e-12;
     double n1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
     double n2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
@@ -248,9 +248,9 @@ __device__ bool cull_shadow(const RtTri &c, vec3 L, const ShadowBox &B)
     double ae1x = fabs((double)e1.x), ae1y = fabs((double)e1.y), ae1z = fabs((double)e1.z);
     double ae2x = fabs((double)e2.x), ae2y = fabs((double)e2.y), ae2z = fabs((double)e2.z);
     double Ed = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + 1e-12 * (fabs(dlo) + fabs(dhi));
-    double Eu = g * M3(Dx, Dy, Dz, Sx, Sy, Sz, ae2x, ae2y, ae2z) + dn * pn * n2 + 1e-12 * (fabs(ulo) + fabs(uhi));
-    double Ev = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, Sx, Sy, Sz) + dn * pn * n1 + 1e-12 * (fabs(vlo) + fabs(vhi));
-    double Et = g * M3(Sx, Sy, Sz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + pn * nN;
+    double Eu = g * M3(Dx, Dy, Dz, Sx, Sy, Sz, ae2x, ae2y, ae2z) + dn * (pn + rho) * n2 + 1e-12 * (fabs(ulo) + fabs(uhi));
+    double Ev = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, Sx, Sy, Sz) + dn * (pn + rho) * n1 + 1e-12 * (fabs(vlo) + fabs(vhi));
+    double Et = g * M3(Sx, Sy, Sz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + (pn + rho) * nN;
     double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
     double aN = ax * Nx + ay * Ny + az * Nz;
     double EaN = 1e-12 * (fabs(ax * Nx) + fabs(ay * Ny) + fabs(az * Nz));
@@ -393,7 +393,8 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
                                              const RtSphere *__restrict__ sph, int bi, vec3 pos,
                                              vec3 objColor, int l, unsigned long long smask = ~0ull)
 {
-    vec3 lp = v3(F.lpos[l][0], F.lpos[l][1], F.lpos[l][2]);
+    const RtLight Lt = F.lights[l];                                      // uniform: scalar loads
+    vec3 lp = v3(Lt.x, Lt.y, Lt.z);
     vec3 r = lp - pos;                                                   // :370
     double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
            r2 = (double)r.z * (double)r.z;
@@ -408,7 +409,7 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     const float b = (float)(4 * M_PI);                                   // :404
     float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
     if (a <= 0) a = 0.f;                                                 // :409
-    vec3 lc = v3(F.lcol[l][0], F.lcol[l][1], F.lcol[l][2]);
+    vec3 lc = v3(Lt.r, Lt.g, Lt.b);
     return ((objColor * lc) * a) / area;                                 // :412
 }
 
@@ -424,21 +425,26 @@ struct LaneShadowBox {
     }
 };
 
-__device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lp, vec3 pos, vec3 normal)
+__device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lmin, vec3 lmax, vec3 pos, vec3 normal)
 {
-    vec3 r = lp - pos;                                                   // :370/:373
+    // d_k = fl(L_k - pos) (:370/:373) is monotone in L_k, so every light's
+    // direction lies in [fl(lmin - pos), fl(lmax - pos)] componentwise.
+    vec3 rlo = lmin - pos, rhi = lmax - pos;
     vec3 S = pos + normal * 0.00001f;                                    // :394
-    double px = (double)S.x - lp.x + r.x, py = (double)S.y - lp.y + r.y, pz = (double)S.z - lp.z + r.z;
-    float pb = (float)((fabs(px) + fabs(py) + fabs(pz)) * (1.0 + 1e-6) + 1e-30);   // L1 >= L2
-    b.lo[0] = fminf(b.lo[0], r.x); b.hi[0] = fmaxf(b.hi[0], r.x);
-    b.lo[1] = fminf(b.lo[1], r.y); b.hi[1] = fmaxf(b.hi[1], r.y);
-    b.lo[2] = fminf(b.lo[2], r.z); b.hi[2] = fmaxf(b.hi[2], r.z);
+    // p_k = S - L_k + d_k = (S - pos) + rounding(d_k): |p_k| <= |S - pos|_1 + 2^-24 |d|_1
+    double sp = fabs((double)S.x - pos.x) + fabs((double)S.y - pos.y) + fabs((double)S.z - pos.z);
+    double dr = fmax(fabs((double)rlo.x), fabs((double)rhi.x)) + fmax(fabs((double)rlo.y), fabs((double)rhi.y)) +
+                fmax(fabs((double)rlo.z), fabs((double)rhi.z));
+    float pb = (float)((sp + 5.9604644775390625e-8 * dr) * (1.0 + 1e-6) + 1e-30);
+    b.lo[0] = fminf(b.lo[0], rlo.x); b.hi[0] = fmaxf(b.hi[0], rhi.x);
+    b.lo[1] = fminf(b.lo[1], rlo.y); b.hi[1] = fmaxf(b.hi[1], rhi.y);
+    b.lo[2] = fminf(b.lo[2], rlo.z); b.hi[2] = fmaxf(b.hi[2], rhi.z);
     b.pn = fmaxf(b.pn, pb);
 }
 
 // Whole wave, converged control flow.
 __device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, const RtTri *__restrict__ tc,
-                                                             const LaneShadowBox &b, vec3 lp, int lane)
+                                                             const LaneShadowBox &b, int lane)
 {
     ShadowBox B;
 #pragma unroll
@@ -448,7 +454,8 @@ __device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, c
     }
     B.pn = wave_max(b.pn);
     bool keep = true;
-    if (lane < F.n_tris && B.lo[0] <= B.hi[0]) keep = !cull_shadow(tc[lane], lp, B);
+    if (lane < F.n_tris && B.lo[0] <= B.hi[0])
+        keep = !cull_shadow(tc[lane], v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, B);
     return __ballot(keep && lane < F.n_tris);
 }
 
@@ -498,7 +505,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
     const float m = 0.5f;
     LaneShadowBox sb;
     sb.init();
-    const vec3 lp0 = v3(F.lpos[0][0], F.lpos[0][1], F.lpos[0][2]);
+    const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
     if (active) {
         for (int k = 0; k < 9; ++k) {
             const int i = k / 3 - 1, j = k % 3 - 1;
@@ -509,14 +516,13 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
             s_t[k][threadIdx.x] = t;
             if (CULL && F.cull_shadow && F.n_lights > 0 && bi != INT_MIN) {
                 vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
-                shadow_box_add(sb, lp0, pos, hit_normal(shade, sph, bi, pos));
+                shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, bi, pos));
             }
         }
     }
-    // lights >= 1 test every triangle (the mask walk must stop at n_tris)
-    const unsigned long long all_tris = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
-    unsigned long long smask0 = all_tris;
-    if (CULL && F.cull_shadow && F.n_lights > 0) smask0 = shadow_mask_of(F, tc, sb, lp0, lane);
+    // one mask for every light of the set (the mask walk must stop at n_tris)
+    unsigned long long smask = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
+    if (CULL && F.cull_shadow && F.n_lights > 0) smask = shadow_mask_of(F, tc, sb, lane);
     if (active) {
         // Pass 2: shading in the reference's order (:143-157)
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
             valid = true;
             vec3 oc = object_colour(shade, sph, bi);
             for (int l = 0; l < F.n_lights; ++l)                                          // :151-153
-                pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, l == 0 ? smask0 : all_tris);
+                pc = pc + direct_light<CULL>(F, tc, shade, sph, bi, pos, oc, l, smask);
             pc = pc + (oc * ind);                                                         // :156
         }
         px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));             // :160-166

@@ -142,3 +142,71 @@ extern "C" int cg_rast_load_test_model(cg_rtri *room, int room_cap, int *n_room,
     *n_boxes = nb;
     return nr + nb;
 }
+
+// ---------------------------------------------------------------------------
+// Build-defined workloads (not in the reference).
+
+// C4 area light: n x n point lights at the cell centres of a square of side
+// `side` in the xz-plane centred on the given light, each carrying 1/(n*n) of
+// its colour; light (i, j) is out[j*n + i].
+extern "C" int cg_rt_area_lights(const cg_light *centre, float side, int n, cg_light *out, int cap)
+{
+    if (!centre || n <= 0 || n > 64 || !(side >= 0.0f)) return CG_E_INVALID;
+    if (!out || cap < n * n) return CG_E_CAPACITY;
+    const float fn = (float)n, inv = 1.0f / (float)(n * n);
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) {
+            cg_light &l = out[j * n + i];
+            l.position = centre->position;
+            l.position.x = centre->position.x + side * (((float)i + 0.5f) / fn - 0.5f);
+            l.position.z = centre->position.z + side * (((float)j + 0.5f) / fn - 0.5f);
+            l.colour = cg_vec3{centre->colour.x * inv, centre->colour.y * inv, centre->colour.z * inv};
+        }
+    return n * n;
+}
+
+namespace {
+// PCG32 (pcg32_random_r, XSH-RR 64/32), seeded like pcg32_srandom_r(seed, seq).
+struct Pcg32 {
+    uint64_t state = 0, inc = 0;
+    Pcg32(uint64_t seed, uint64_t seq)
+    {
+        inc = (seq << 1u) | 1u;
+        next();
+        state += seed;
+        next();
+    }
+    uint32_t next()
+    {
+        uint64_t old = state;
+        state = old * 6364136223846793005ull + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((0u - rot) & 31u));
+    }
+    // a + (b - a) * u, u = top 24 bits / 2^24 in [0, 1) (all float ops exact but the last two)
+    float uniform(float a, float b) { return a + (b - a) * ((float)(next() >> 8) * 5.9604644775390625e-8f); }
+};
+}  // namespace
+
+// C5 random scene: triangle k draws centroid (x, y, z) ~ U[-1,1], then
+// v0, v1, v2 = centroid + U[-0.02,0.02]^3 each (x, y, z order), then colour
+// ~ U[0.15,0.75]^3; w = 1; normal by ComputeNormal.  Stream seq 54.
+extern "C" int cg_rt_random_scene(uint64_t seed, int n, cg_tri *out)
+{
+    if (n < 0 || (n && !out)) return CG_E_INVALID;
+    Pcg32 g(seed, 54u);
+    for (int k = 0; k < n; ++k) {
+        cg_tri &t = out[k];
+        float cx = g.uniform(-1.f, 1.f), cy = g.uniform(-1.f, 1.f), cz = g.uniform(-1.f, 1.f);
+        cg_vec4 *v[3] = {&t.v0, &t.v1, &t.v2};
+        for (cg_vec4 *p : v) {
+            float dx = g.uniform(-0.02f, 0.02f), dy = g.uniform(-0.02f, 0.02f), dz = g.uniform(-0.02f, 0.02f);
+            *p = cg_vec4{cx + dx, cy + dy, cz + dz, 1.0f};
+        }
+        float r = g.uniform(0.15f, 0.75f), gg = g.uniform(0.15f, 0.75f), b = g.uniform(0.15f, 0.75f);
+        t.color = cg_vec3{r, gg, b};
+        compute_normal(t);
+    }
+    return n;
+}

@@ -2,7 +2,9 @@
 // device-resident scene, launches, error mapping.  Nothing here throws
 // across the ABI; HIP failures become CG_E_HIP with the HIP message kept in
 // the context for cg_last_error().
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -62,7 +64,8 @@ struct cg_ctx {
     std::string err;
     // RT scene
     int n_tris = -1, n_sph = 0;
-    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d;
+    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights;
+    std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
     int n_room = -1, n_boxes = 0;
@@ -147,7 +150,7 @@ extern "C" void cg_destroy(cg_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->tris, &c->tc, &c->shade, &c->sph, &c->frame,
-                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d};
+                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights};
     for (DevBuf *b : bufs) b->release();
     rast_release(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -190,8 +193,46 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     return CG_OK;
 }
 
+// Lights to the device buffer (ordered on `st`; skipped when unchanged) and
+// the light-set summary the shadow certificate uses.
+static int set_lights(cg_ctx *c, const cg_light *lights, int n, hipStream_t st, RtFrame &F)
+{
+    std::vector<RtLight> L((size_t)n);
+    for (int l = 0; l < n; ++l)
+        L[l] = RtLight{lights[l].position.x, lights[l].position.y, lights[l].position.z, lights[l].position.w,
+                       lights[l].colour.x,   lights[l].colour.y,   lights[l].colour.z,   0.f};
+    F.n_lights = n;
+    for (int k = 0; k < 3; ++k) F.lmin[k] = F.lmax[k] = F.lc[k] = 0.f;
+    F.lrho = 0.0;
+    if (n > 0) {
+        for (int k = 0; k < 3; ++k) F.lmin[k] = F.lmax[k] = (&L[0].x)[k];
+        for (const RtLight &q : L)
+            for (int k = 0; k < 3; ++k) {
+                F.lmin[k] = std::min(F.lmin[k], (&q.x)[k]);
+                F.lmax[k] = std::max(F.lmax[k], (&q.x)[k]);
+            }
+        for (int k = 0; k < 3; ++k) F.lc[k] = 0.5f * F.lmin[k] + 0.5f * F.lmax[k];
+        double rho = 0.0;
+        for (const RtLight &q : L) {
+            double dx = (double)q.x - F.lc[0], dy = (double)q.y - F.lc[1], dz = (double)q.z - F.lc[2];
+            rho = std::max(rho, std::sqrt(dx * dx + dy * dy + dz * dz));
+        }
+        F.lrho = rho > 0.0 ? rho * (1.0 + 1e-9) + 1e-12 : 0.0;
+    }
+    const bool same = L.size() == c->lights_host.size() &&
+                      (L.empty() || std::memcmp(L.data(), c->lights_host.data(), L.size() * sizeof(RtLight)) == 0);
+    CG_TRY(c, c->lights.ensure(std::max<size_t>(L.size(), 1) * sizeof(RtLight)), "alloc lights");
+    if (!same && n > 0) {
+        c->lights_host = L;
+        CG_TRY(c, hipMemcpyAsync(c->lights.p, c->lights_host.data(), L.size() * sizeof(RtLight),
+                                 hipMemcpyHostToDevice, st), "upload lights");
+    }
+    F.lights = (const RtLight *)c->lights.p;
+    return CG_OK;
+}
+
 static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
-                      const cg_rt_shard *shard, RtFrame &F)
+                      const cg_rt_shard *shard, hipStream_t st, RtFrame &F)
 {
     if (!cam || cam->width <= 0 || cam->height <= 0 || n_lights < 0 || n_lights > kMaxLights ||
         (n_lights && !lights))
@@ -209,13 +250,6 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     std::memcpy(F.R, cam->R, sizeof(F.R));
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
-    F.n_lights = n_lights;
-    for (int l = 0; l < n_lights; ++l) {
-        F.lpos[l][0] = lights[l].position.x; F.lpos[l][1] = lights[l].position.y;
-        F.lpos[l][2] = lights[l].position.z; F.lpos[l][3] = lights[l].position.w;
-        F.lcol[l][0] = lights[l].colour.x; F.lcol[l][1] = lights[l].colour.y;
-        F.lcol[l][2] = lights[l].colour.z;
-    }
     cg_rt_shard one{0, 1, kRtTileH};
     const cg_rt_shard *s = shard ? shard : &one;
     if (s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0 ||
@@ -231,7 +265,8 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     }();
     F.cull_primary = cull >= 1;
     F.cull_shadow = cull >= 2;
-    return CG_OK;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    return set_lights(c, lights, n_lights, st, F);
 }
 
 extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
@@ -259,10 +294,10 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 {
     if (!c || !d_out) return CG_E_INVALID;
     RtFrame F;
-    int rc = fill_frame(c, lights, n_lights, cam, shard, F);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int rc = fill_frame(c, lights, n_lights, cam, shard, st, F);
     if (rc) return rc;
-    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    return rt_enqueue(c, F, d_out, stream ? (hipStream_t)stream : c->stream);
+    return rt_enqueue(c, F, d_out, st);
 }
 
 extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
@@ -271,9 +306,8 @@ extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, con
     if (!c || !argb) return CG_E_INVALID;
     auto t0 = std::chrono::steady_clock::now();
     RtFrame F;
-    int rc = fill_frame(c, lights, n_lights, cam, nullptr, F);
+    int rc = fill_frame(c, lights, n_lights, cam, nullptr, c->stream, F);
     if (rc) return rc;
-    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     size_t bytes = (size_t)F.rows_out * F.W * sizeof(uint32_t);
     CG_TRY(c, c->frame.ensure(bytes), "alloc frame");
     CG_TRY(c, hipEventRecord(c->ev0, c->stream), "event");
@@ -348,10 +382,8 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     std::memset(&F, 0, sizeof(F));
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
-    F.n_lights = 1;
-    F.lpos[0][0] = light->position.x; F.lpos[0][1] = light->position.y;
-    F.lpos[0][2] = light->position.z; F.lpos[0][3] = light->position.w;
-    F.lcol[0][0] = light->colour.x; F.lcol[0][1] = light->colour.y; F.lcol[0][2] = light->colour.z;
+    int rc = set_lights(c, light, 1, c->stream, F);
+    if (rc) return rc;
     // shadow rays use generic starts: RtTri constants are camera-independent
     // except s/detT/K2/K3, which the shadow path does not read.
     float zero[4] = {0, 0, 0, 1};

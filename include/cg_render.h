@@ -95,6 +95,16 @@ int  cg_device_count(void);
 /* LoadTestModel (raytracer/Source/TestModelH.h:121-279): 28 triangles +
  * one sphere, scaled to [-1,1]^3.  Returns the triangle count. */
 int cg_rt_load_test_model(cg_tri *tris, int cap, cg_sphere *sphere);
+/* Build-defined workloads of SURVEY.md 8d (not in the reference; host-only,
+ * no device work).  C4: n x n point lights at the cell centres of a square of
+ * side `side` in the xz-plane centred on *centre, each with colour/(n*n);
+ * light (i, j) -> out[j*n + i], x = c.x + side*(((float)i + 0.5f)/n - 0.5f),
+ * z likewise with j.  Returns n*n.  C5: n random triangles from PCG32
+ * (seed, stream 54): centroid ~ U[-1,1]^3, each vertex = centroid +
+ * U[-0.02,0.02]^3, colour ~ U[0.15,0.75]^3, w = 1, normal by ComputeNormal
+ * (TestModelH.h:96-105).  Returns n. */
+int cg_rt_area_lights(const cg_light *centre, float side, int n, cg_light *out, int cap);
+int cg_rt_random_scene(uint64_t seed, int n, cg_tri *out);
 /* Upload the scene LoadTestModel built (TestModelH.h:121-279); kept device
  * resident until the next call.  Replaces the per-frame `vector<Triangle>`
  * the reference rebuilds in Draw (skeleton.cpp:113-116). */
@@ -106,7 +116,7 @@ int cg_rt_set_scene(cg_ctx *ctx, const cg_tri *tris, int n_tris,
  * caller-owned host buffer `argb` (row-major, top row first), exactly what
  * the reference leaves in screen->buffer. */
 int cg_rt_render(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
-                 uint32_t *argb, cg_stats *stats);
+                 uint32_t *argb, cg_stats *stats);   /* 0 <= n_lights <= 4096 */
 /* Device-resident form: renders this shard's rows into the caller-owned
  * device buffer d_out (cg_rt_shard_rows() rows of W pixels), enqueued on
  * `stream`, no synchronisation.  shard may be NULL (= whole frame). */

@@ -38,6 +38,8 @@ typedef struct { cgo_v4 position; float distance; int triangleIndex; int sphereI
 /* raytracer/Source/skeleton.cpp:47-50 */
 typedef struct { cgo_v4 position; cgo_v3 colour; } cgo_light;
 
+#define CGO_MAX_LIGHTS 64   /* C4's 8x8 area light */
+
 /* Frame parameters = the reference's RT globals (skeleton.cpp:56-60). */
 typedef struct {
     int width, height;
@@ -46,7 +48,7 @@ typedef struct {
     float R[16];        /* glm::mat4, column-major: R[c*4+r] = m[c][r] */
     float indirect;     /* skeleton.cpp:110, 0.5 */
     int n_lights;
-    cgo_light lights[4];
+    cgo_light lights[CGO_MAX_LIGHTS];
 } cgo_rt_params;
 
 /* Work counters. */
@@ -68,6 +70,18 @@ uint32_t cgo_put_pixel(cgo_v3 colour);
 void cgo_rt_draw(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
                  const cgo_sphere *sph, int n_sph, uint32_t *argb, int row0, int row1,
                  cgo_rt_counters *cnt);
+/* One pixel of Draw (skeleton.cpp:120-166). */
+uint32_t cgo_rt_pixel(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                      const cgo_sphere *sph, int n_sph, int u, int v, cgo_rt_counters *cnt);
+/* Pixels (xy[2k], xy[2k+1]) into out[k], k < n, over n_threads pthreads. */
+void cgo_rt_draw_pixels(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                        const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
+                        int n_threads);
+/* Build-defined workloads, restated from their definition in
+ * include/cg_render.h: C4 area light (n x n lights, colour/(n*n)) and the C5
+ * PCG32 random scene. */
+int cgo_rt_area_lights(cgo_light centre, float side, int n, cgo_light *out);
+int cgo_rt_random_scene(uint64_t seed, int n, cgo_rt_tri *out);
 /* Same, multithreaded by rows (pthreads); returns threads used. */
 int  cgo_rt_draw_mt(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
                     const cgo_sphere *sph, int n_sph, uint32_t *argb, int row0, int row1,

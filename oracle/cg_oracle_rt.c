@@ -303,43 +303,134 @@ uint32_t cgo_put_pixel(cgo_v3 c)
     return (128u << 24) + (r << 16) + (g << 8) + b;
 }
 
+/* raytracer/Source/skeleton.cpp:120-166: one pixel of Draw */
+uint32_t cgo_rt_pixel(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                      const cgo_sphere *sph, int n_sph, int u, int v, cgo_rt_counters *cnt)
+{
+    const int W = p->width, H = p->height;
+    cgo_v3 indirectLight = v3(p->indirect, p->indirect, p->indirect);
+    cgo_v4 dir = v4((float)(u - W / 2), (float)(v - H / 2), p->focal, 1.0f); /* :126 */
+    dir = mat4_mul(p->R, dir);                                              /* :128 */
+    cgo_v3 pixelColour = v3(0.0f, 0.0f, 0.0f);
+    int validRay = 0;
+    for (int i = -1; i <= 1; ++i) {
+        for (int j = -1; j <= 1; ++j) {
+            float multiplier = 0.5f;
+            cgo_v4 newDir = v4(dir.x + (multiplier * (float)i),
+                               dir.y + (multiplier * (float)j), p->focal, 1.0f); /* :137 */
+            cgo_isect is;
+            if (cgo_rt_closest(p->camera, newDir, tris, n_tris, sph, n_sph, &is, cnt)) {
+                validRay = 1;
+                cgo_v3 objectColor = is.triangleIndex != -1 ? tris[is.triangleIndex].color
+                                                            : sph[is.sphereIndex].color;
+                for (int l = 0; l < p->n_lights; ++l)
+                    pixelColour = v3_add(pixelColour,
+                                         cgo_rt_direct_light(&is, tris, n_tris, sph, n_sph,
+                                                             &p->lights[l], cnt));
+                pixelColour = v3_add(pixelColour, v3_mul(objectColor, indirectLight)); /* :156 */
+            }
+        }
+    }
+    if (validRay) return cgo_put_pixel(v3_divs(pixelColour, 9.0f));   /* :160-163 */
+    return cgo_put_pixel(v3(0.0f, 0.0f, 0.0f));                       /* :165 */
+}
+
 /* raytracer/Source/skeleton.cpp:104-169 */
 void cgo_rt_draw(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
                  const cgo_sphere *sph, int n_sph, uint32_t *argb, int row0, int row1,
                  cgo_rt_counters *cnt)
 {
     const int W = p->width, H = p->height;
-    cgo_v3 indirectLight = v3(p->indirect, p->indirect, p->indirect);
-    for (int v = row0; v < row1 && v < H; v++) {
-        for (int u = 0; u < W; u++) {
-            cgo_v4 dir = v4((float)(u - W / 2), (float)(v - H / 2), p->focal, 1.0f); /* :126 */
-            dir = mat4_mul(p->R, dir);                                              /* :128 */
-            cgo_v3 pixelColour = v3(0.0f, 0.0f, 0.0f);
-            int validRay = 0;
-            for (int i = -1; i <= 1; ++i) {
-                for (int j = -1; j <= 1; ++j) {
-                    float multiplier = 0.5f;
-                    cgo_v4 newDir = v4(dir.x + (multiplier * (float)i),
-                                       dir.y + (multiplier * (float)j), p->focal, 1.0f); /* :137 */
-                    cgo_isect is;
-                    if (cgo_rt_closest(p->camera, newDir, tris, n_tris, sph, n_sph, &is, cnt)) {
-                        validRay = 1;
-                        cgo_v3 objectColor = is.triangleIndex != -1 ? tris[is.triangleIndex].color
-                                                                    : sph[is.sphereIndex].color;
-                        for (int l = 0; l < p->n_lights; ++l)
-                            pixelColour = v3_add(pixelColour,
-                                                 cgo_rt_direct_light(&is, tris, n_tris, sph, n_sph,
-                                                                     &p->lights[l], cnt));
-                        pixelColour = v3_add(pixelColour, v3_mul(objectColor, indirectLight)); /* :156 */
-                    }
-                }
-            }
-            uint32_t px;
-            if (validRay) px = cgo_put_pixel(v3_divs(pixelColour, 9.0f));   /* :160-163 */
-            else px = cgo_put_pixel(v3(0.0f, 0.0f, 0.0f));                    /* :165 */
-            argb[(size_t)v * W + u] = px;
+    for (int v = row0; v < row1 && v < H; v++)
+        for (int u = 0; u < W; u++)
+            argb[(size_t)v * W + u] = cgo_rt_pixel(p, tris, n_tris, sph, n_sph, u, v, cnt);
+}
+
+typedef struct {
+    const cgo_rt_params *p; const cgo_rt_tri *tris; int n_tris;
+    const cgo_sphere *sph; int n_sph; const int *xy; int n; uint32_t *out; int stride, k;
+} px_job;
+
+static void *px_worker(void *arg)
+{
+    px_job *j = (px_job *)arg;
+    for (int i = j->k; i < j->n; i += j->stride)
+        j->out[i] = cgo_rt_pixel(j->p, j->tris, j->n_tris, j->sph, j->n_sph, j->xy[2 * i], j->xy[2 * i + 1], 0);
+    return 0;
+}
+
+void cgo_rt_draw_pixels(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                        const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
+                        int n_threads)
+{
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    px_job jobs[256];
+    for (int k = 0; k < n_threads; ++k) {
+        jobs[k] = (px_job){p, tris, n_tris, sph, n_sph, xy, n, out, n_threads, k};
+        if (k) pthread_create(&th[k], 0, px_worker, &jobs[k]);
+    }
+    px_worker(&jobs[0]);
+    for (int k = 1; k < n_threads; ++k) pthread_join(th[k], 0);
+}
+
+/* ---- build-defined workloads ---- */
+
+/* C4: cell centres of an n x n grid over a side x side square in the xz-plane */
+int cgo_rt_area_lights(cgo_light centre, float side, int n, cgo_light *out)
+{
+    if (n <= 0 || n * n > CGO_MAX_LIGHTS) return -1;
+    float share = 1.0f / (float)(n * n);
+    for (int j = 0; j < n; ++j) {
+        for (int i = 0; i < n; ++i) {
+            float fx = ((float)i + 0.5f) / (float)n - 0.5f;
+            float fz = ((float)j + 0.5f) / (float)n - 0.5f;
+            cgo_light *l = &out[j * n + i];
+            l->position = centre.position;
+            l->position.x = centre.position.x + side * fx;
+            l->position.z = centre.position.z + side * fz;
+            l->colour = v3_muls(centre.colour, share);
         }
     }
+    return n * n;
+}
+
+/* C5: PCG32 XSH-RR (O'Neill's pcg32_random_r / pcg32_srandom_r) */
+typedef struct { uint64_t s, inc; } pcg_t;
+static uint32_t pcg_step(pcg_t *g)
+{
+    uint64_t x = g->s;
+    g->s = x * 6364136223846793005ull + g->inc;
+    uint32_t sh = (uint32_t)(((x >> 18) ^ x) >> 27), r = (uint32_t)(x >> 59);
+    return (sh >> r) | (sh << ((32u - r) & 31u));
+}
+static float pcg_unif(pcg_t *g, float lo, float hi)
+{
+    float u = (float)(pcg_step(g) >> 8) / 16777216.0f;
+    return lo + (hi - lo) * u;
+}
+int cgo_rt_random_scene(uint64_t seed, int n, cgo_rt_tri *out)
+{
+    pcg_t g = {0u, (54u << 1) | 1u};
+    pcg_step(&g);
+    g.s += seed;
+    pcg_step(&g);
+    for (int k = 0; k < n; ++k) {
+        float c[3];
+        for (int a = 0; a < 3; ++a) c[a] = pcg_unif(&g, -1.0f, 1.0f);
+        cgo_v4 *vs[3] = {&out[k].v0, &out[k].v1, &out[k].v2};
+        for (int q = 0; q < 3; ++q) {
+            float o[3];
+            for (int a = 0; a < 3; ++a) o[a] = pcg_unif(&g, -0.02f, 0.02f);
+            *vs[q] = v4(c[0] + o[0], c[1] + o[1], c[2] + o[2], 1.0f);
+        }
+        float col[3];
+        for (int a = 0; a < 3; ++a) col[a] = pcg_unif(&g, 0.15f, 0.75f);
+        out[k].color = v3(col[0], col[1], col[2]);
+        compute_normal(&out[k]);
+    }
+    return n;
 }
 
 typedef struct {

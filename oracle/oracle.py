@@ -45,7 +45,7 @@ class Light(C.Structure):
 class RtParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", V4),
                 ("R", C.c_float * 16), ("indirect", C.c_float), ("n_lights", C.c_int),
-                ("lights", Light * 4)]
+                ("lights", Light * 64)]   # CGO_MAX_LIGHTS
 
 
 class RtCounters(C.Structure):
@@ -105,6 +105,10 @@ def load():
         "cgo_sphere_solve_quadratic": (C.c_int, [C.c_float, C.c_float, C.c_float,
                                                  C.POINTER(C.c_float), C.POINTER(C.c_float)]),
         "cgo_put_pixel": (C.c_uint32, [V3]),
+        "cgo_rt_draw_pixels": (None, [C.POINTER(RtParams), C.POINTER(RtTri), C.c_int, C.POINTER(Sphere),
+                                      C.c_int, P, C.c_int, P, C.c_int]),
+        "cgo_rt_area_lights": (C.c_int, [Light, C.c_float, C.c_int, C.POINTER(Light)]),
+        "cgo_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(RtTri)]),
         "cgo_rast_load_scene": (C.c_int, [C.POINTER(RastTri), C.POINTER(C.c_int),
                                           C.POINTER(RastTri), C.POINTER(C.c_int)]),
         "cgo_rast_default_params": (None, [C.POINTER(RastParams), C.c_int, C.c_int]),
@@ -150,20 +154,56 @@ def rt_params(width, height, focal=256.0, cam=(0.0, 0.0, -3.0, 1.0), R=None, ind
     return p
 
 
-def rt_draw(p, rows=None, counters=False, threads=1):
-    """Render rows [r0, r1) of the RT frame (ARGB uint32, W*H, untouched rows 0)."""
+def rt_draw(p, rows=None, counters=False, threads=1, scene=None):
+    """Render rows [r0, r1) of the RT frame (ARGB uint32, W*H, untouched rows 0).
+    scene = (tris, n, sphere pointer or None, n_sph); default LoadTestModel."""
     lib = load()
-    tris, n, sph = rt_scene()
+    if scene is None:
+        tris, n, sph1 = rt_scene()
+        scene = (tris, n, C.pointer(sph1), 1)
+    tris, n, sph, n_sph = scene
     out = np.zeros(p.width * p.height, np.uint32)
     r0, r1 = rows if rows is not None else (0, p.height)
     cnt = RtCounters()
     if threads > 1:
-        lib.cgo_rt_draw_mt(C.byref(p), tris, n, C.byref(sph), 1, out.ctypes.data_as(C.c_void_p),
+        lib.cgo_rt_draw_mt(C.byref(p), tris, n, sph, n_sph, out.ctypes.data_as(C.c_void_p),
                            r0, r1, threads)
     else:
-        lib.cgo_rt_draw(C.byref(p), tris, n, C.byref(sph), 1, out.ctypes.data_as(C.c_void_p), r0, r1,
+        lib.cgo_rt_draw(C.byref(p), tris, n, sph, n_sph, out.ctypes.data_as(C.c_void_p), r0, r1,
                         C.byref(cnt) if counters else None)
     return (out, cnt) if counters else out
+
+
+def rt_area_lights(pos, colour, side, n):
+    """C4 area light (build-defined, see cg_oracle.h): list of (pos, colour) tuples."""
+    lib = load()
+    out = (Light * (n * n))()
+    k = lib.cgo_rt_area_lights(Light(V4(*pos), V3(*colour)), side, n, out)
+    assert k == n * n
+    return [((l.position.x, l.position.y, l.position.z, l.position.w),
+             (l.colour.x, l.colour.y, l.colour.z)) for l in out]
+
+
+def rt_random_scene(seed, n):
+    """C5 random scene (build-defined, see cg_oracle.h): ctypes RtTri array."""
+    lib = load()
+    tris = (RtTri * max(n, 1))()
+    assert lib.cgo_rt_random_scene(seed, n, tris) == n
+    return tris
+
+
+def rt_draw_pixels(p, xy, scene=None, threads=1):
+    """Pixels xy (int array (k, 2) of (u, v)) of the RT frame; scene as in rt_draw."""
+    lib = load()
+    if scene is None:
+        tris1, n1, sph1 = rt_scene()
+        scene = (tris1, n1, C.pointer(sph1), 1)
+    tris, n_tris, sph, n_sph = scene
+    xy = np.ascontiguousarray(np.asarray(xy, np.int32).reshape(-1, 2))
+    out = np.zeros(len(xy), np.uint32)
+    lib.cgo_rt_draw_pixels(C.byref(p), tris, n_tris, sph, n_sph, xy.ctypes.data_as(C.c_void_p),
+                           len(xy), out.ctypes.data_as(C.c_void_p), threads)
+    return out
 
 
 def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,

@@ -79,6 +79,11 @@ def rt_configs():
                                        lights=[[[f32(0.1), f32(-0.6), f32(-0.6), 1.0], [14.0, 14.0, 14.0]]]),
         "rt_256x192_2lights": dict(width=256, height=192, focal=200.0, cam=[0, 0, -3.0, 1], R=None,
                                    lights=[L0, [[0.3, -0.8, -0.2, 1.0], [6.0, 3.0, 9.0]]]),
+        # build-defined workloads, small sizes of C4 and C5
+        "rt_c4_480x270_soft8x8": dict(width=480, height=270, focal=270.0, cam=[0, 0, -3.0, 1], R=None,
+                                      lights=[L0], area=dict(side=0.1, n=8)),
+        "rt_c5_256x144_rand2000": dict(width=256, height=144, focal=144.0, cam=[0, 0, -3.0, 1], R=None,
+                                       lights=[L0], scene=dict(random=2000, seed=0x5EED)),
     }
 
 
@@ -98,9 +103,26 @@ def rast_configs():
     }
 
 
+def rt_lights_of(cfg):
+    """Light list of a config: explicit, or the C4 area light around lights[0]."""
+    if "area" in cfg:
+        (p, c), a = cfg["lights"][0], cfg["area"]
+        return oracle.rt_area_lights(tuple(p), tuple(c), a["side"], a["n"])
+    return [(tuple(p), tuple(c)) for p, c in cfg["lights"]]
+
+
 def rt_params_of(cfg):
     return oracle.rt_params(cfg["width"], cfg["height"], cfg["focal"], tuple(cfg["cam"]), cfg["R"], 0.5,
-                            [(tuple(p), tuple(c)) for p, c in cfg["lights"]])
+                            rt_lights_of(cfg))
+
+
+def rt_oracle_scene(cfg):
+    """(tris, n, sph pointer or None, n_sph) for oracle.rt_draw*: LoadTestModel or the C5 scene."""
+    if "scene" in cfg:
+        sc = cfg["scene"]
+        return oracle.rt_random_scene(sc["seed"], sc["random"]), sc["random"], None, 0
+    tris, n, sph = oracle.rt_scene()
+    return tris, n, C.pointer(sph), 1
 
 
 def rast_params_of(cfg):
@@ -129,8 +151,10 @@ def main():
     shot = screenshot_argb()
     for name, cfg in rt_configs().items():
         p = rt_params_of(cfg)
-        argb, cnt = oracle.rt_draw(p, counters=True, threads=1) if cfg["width"] <= 320 else \
-            (oracle.rt_draw(p, threads=os.cpu_count() or 8), None)
+        scene = rt_oracle_scene(cfg)
+        small = cfg["width"] <= 320 and "area" not in cfg and "scene" not in cfg
+        argb, cnt = oracle.rt_draw(p, counters=True, threads=1) if small else \
+            (oracle.rt_draw(p, threads=os.cpu_count() or 8, scene=scene), None)
         e = {"config": cfg, "argb_sha256": sha(argb)}
         if cnt is not None:
             e["counters"] = {k: int(getattr(cnt, k)) for k in ("n_ray", "n_t", "n_uv", "n_sph", "n_dl")}
@@ -138,6 +162,8 @@ def main():
         if ref:
             assert e["argb_sha256"].startswith(ref["argb"]), (name, e["argb_sha256"])
             e["pinned_by"] = "SURVEY.md 8c reference fingerprint"
+        elif "area" in cfg or "scene" in cfg:
+            e["pinned_by"] = "build-defined workload (SURVEY.md 8d C4/C5, not in the reference): restatement only"
         else:
             e["pinned_by"] = "restatement only (parity unpinned beyond the oracle)"
         if name == "rt_320x256_z-2.9":

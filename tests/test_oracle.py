@@ -35,7 +35,7 @@ def test_rt_golden_hashes_small(golden):
         cfg = e["config"]
         if cfg["width"] * cfg["height"] > 320 * 256:
             continue
-        argb = oracle.rt_draw(mg.rt_params_of(cfg))
+        argb = oracle.rt_draw(mg.rt_params_of(cfg), scene=mg.rt_oracle_scene(cfg), threads=8)
         assert mg.sha(argb) == e["argb_sha256"], name
 
 

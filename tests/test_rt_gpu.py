@@ -20,7 +20,18 @@ def _lights(cfg):
     for i, (p, c) in enumerate(cfg["lights"]):
         arr[i].position = cgamd.Vec4(*p)
         arr[i].colour = cgamd.Vec3(*c)
+    if "area" in cfg:   # C4: the library's own area-light expansion
+        return cgamd.area_lights(arr[0], cfg["area"]["side"], cfg["area"]["n"])
     return arr
+
+
+def _set_scene(ctx, cfg):
+    if "scene" in cfg:
+        sc = cfg["scene"]
+        ctx.rt_set_scene(cgamd.random_scene(sc["random"], sc["seed"]), sc["random"], None, 0)
+    else:
+        tris, n, sph = cgamd.rt_scene()
+        ctx.rt_set_scene(tris, n, sph, 1)
 
 
 def _cam(cfg):
@@ -46,7 +57,11 @@ def test_rt_screenshot_golden(rt):
 @pytest.mark.parametrize("name", list(mg.rt_configs()))
 def test_rt_configs_match_golden(rt, golden, name):
     cfg = mg.rt_configs()[name]
-    argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+    _set_scene(rt, cfg)
+    try:
+        argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+    finally:
+        _set_scene(rt, {})
     h = mg.sha(argb)
     assert h == golden["rt"][name]["argb_sha256"], name
     ref = mg.REFERENCE_FINGERPRINTS.get(name)
@@ -109,6 +124,57 @@ def test_rt_full_1080p_vs_oracle(rt, golden):
     cfg = mg.rt_configs()["rt_1920x1080_f1080"]
     argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
     assert mg.sha(argb) == golden["rt"]["rt_1920x1080_f1080"]["argb_sha256"]
+
+
+def _sample_xy(W, H, n, seed):
+    """n pixels: the four corners, a stratified grid and uniform random ones."""
+    rng = np.random.default_rng(seed)
+    g = int(np.sqrt(n // 2))
+    gx, gy = np.meshgrid(np.linspace(0, W - 1, g).astype(int), np.linspace(0, H - 1, g).astype(int))
+    xy = [np.array([[0, 0], [W - 1, 0], [0, H - 1], [W - 1, H - 1]]),
+          np.stack([gx.ravel(), gy.ravel()], 1),
+          np.stack([rng.integers(0, W, n - 4 - g * g), rng.integers(0, H, n - 4 - g * g)], 1)]
+    return np.concatenate(xy).astype(np.int32)
+
+
+C4_FULL = dict(width=3840, height=2160, focal=2160.0, cam=[0, 0, -3.0, 1], R=None,
+               lights=[[[0.0, -0.5, -0.7, 1.0], [14.0, 14.0, 14.0]]], area=dict(side=0.1, n=8))
+
+
+def test_rt_c4_4k_soft_shadows_sampled(rt):
+    """C4 at full size (3840x2160, f=2160, 8x8 area light = 64 lights): the
+    whole GPU frame, 65,536 of its pixels checked bit-exactly against the
+    oracle (a full 4K oracle frame takes CPU-hours; the 480x270 C4 frame is
+    checked whole in test_rt_configs_match_golden)."""
+    cfg = C4_FULL
+    W, H = cfg["width"], cfg["height"]
+    argb, st = rt.rt_render(_cam(cfg), _lights(cfg))
+    xy = _sample_xy(W, H, 65536, 4)
+    ref = oracle.rt_draw_pixels(mg.rt_params_of(cfg), xy, threads=min(16, os.cpu_count() or 8))
+    got = argb.reshape(H, W)[xy[:, 1], xy[:, 0]]
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, f"{bad.size} differ, first at {xy[bad[:4]]}: gpu {got[bad[:4]]} ref {ref[bad[:4]]}"
+    assert (got >> 24 == 0x80).all()
+
+
+def test_rt_c4_sharded_matches_whole(rt):
+    """C4's multi-GPU form: 8 row-stripe shards + unstripe == the whole frame."""
+    torch = pytest.importorskip("torch")
+    cfg = dict(C4_FULL, width=960, height=540, focal=540.0)
+    W, H = cfg["width"], cfg["height"]
+    cam, lights = _cam(cfg), _lights(cfg)
+    full, _ = rt.rt_render(cam, lights)
+    st = torch.cuda.Stream()
+    n = 8
+    rows = cgdist.shard_rows(H, n)
+    g = torch.zeros(n * rows * W, dtype=torch.int32, device="cuda")
+    for r in range(n):
+        rt.rt_render_device(cam, g.data_ptr() + r * rows * W * 4, cgamd.RtShard(r, n, cgdist.DEFAULT_STRIPE),
+                            st.cuda_stream, lights=lights)
+    frame = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    rt.rt_unstripe_device(g.data_ptr(), W, H, n, cgdist.DEFAULT_STRIPE, frame.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    assert np.array_equal(frame.cpu().numpy().view(np.uint32), full)
 
 
 def test_rt_empty_scene_is_black(ctx):

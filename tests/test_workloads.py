@@ -1,0 +1,45 @@
+"""CPU: the build-defined workloads of SURVEY.md 8d (C4 area light, C5 random
+scene).  The library's host helpers (cg_rt_area_lights, cg_rt_random_scene,
+no device work) must produce the same bytes as the oracle's independent
+restatement of their definition (include/cg_render.h)."""
+import ctypes as C
+
+import numpy as np
+
+import cgamd
+import oracle
+
+
+def test_area_lights_match_oracle():
+    for side, n in ((0.1, 8), (0.25, 3), (0.0, 1)):
+        got = cgamd.area_lights(None, side, n)
+        want = oracle.rt_area_lights((0.0, -0.5, -0.7, 1.0), (14.0, 14.0, 14.0), side, n)
+        assert len(got) == len(want) == n * n
+        for g, (p, c) in zip(got, want):
+            assert (g.position.x, g.position.y, g.position.z, g.position.w) == p
+            assert (g.colour.x, g.colour.y, g.colour.z) == c
+    # 8x8: colour share 14/64 is exact, positions symmetric about the centre
+    L = cgamd.area_lights(None, 0.1, 8)
+    xs = sorted({l.position.x for l in L})
+    assert len(xs) == 8 and xs[0] == -xs[-1] and all(l.colour.x == 14.0 / 64 for l in L)
+
+
+def test_random_scene_matches_oracle():
+    n = 50000
+    got = cgamd.random_scene(n, 0x5EED)
+    want = oracle.rt_random_scene(0x5EED, n)
+    assert bytes(got) == bytes(want)
+    a = np.frombuffer(bytes(got), np.float32).reshape(n, 19)
+    v = a[:, :12].reshape(n, 3, 4)
+    assert np.all(v[:, :, 3] == 1.0) and np.all(np.abs(v[:, :, :3]) <= 1.02)
+    assert np.all((a[:, 16:19] >= 0.15) & (a[:, 16:19] <= 0.75))
+    assert np.all(a[:, 15] == 1.0)   # normal.w
+    assert bytes(cgamd.random_scene(16, 1)) != bytes(cgamd.random_scene(16, 2))
+
+
+def test_random_scene_rejects_bad_args():
+    lib = cgamd.load()
+    assert lib.cg_rt_random_scene(1, -1, None) < 0
+    assert lib.cg_rt_area_lights(None, 0.1, 8, None, 0) < 0
+    out = (cgamd.Light * 4)()
+    assert lib.cg_rt_area_lights(C.byref(cgamd.default_lights()[0]), 0.1, 8, out, 4) < 0
