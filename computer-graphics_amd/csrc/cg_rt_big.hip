@@ -1,0 +1,509 @@
+// cg_rt_big.hip -- raytracer hot path for large scenes (n_tris > 64, e.g. the
+// build-defined C5 workload: 1M random triangles), same Draw semantics as
+// cg_rt.hip (raytracer/Source/skeleton.cpp:104-169, ClosestIntersection
+// :263-363, DirectLight :366-415), bit-identical to brute force.
+//
+// The per-wave culling certificates of cg_rt_dev.h are exact for any ray
+// bundle, so they are applied hierarchically:
+//   K0 rt_bin_primary    per (bin of 128x32 pixels, triangle): camera-ray
+//                        certificate of the bin's bundle -> bin list;
+//   K1 rt_big_primary    per 8x8 wave: certificate of the wave's bundle over
+//                        its bin list (64 candidates per pass, one per lane),
+//                        then the closest-hit walk for the 9 sub-rays; hits
+//                        (index, t) to HBM, the wave's shadow-ray box too;
+//   K2 rt_bin_boxes      union of the wave boxes of each bin;
+//   K3 rt_bin_shadow     per (bin, triangle): shadow-ray certificate of the
+//                        light set against the bin's box -> shadow bin list;
+//   K4 rt_big_shade      per wave: certificate against its own box, the
+//                        survivors staged in LDS, DirectLight for every hit
+//                        and light in the reference's order, PutPixelSDL.
+// Bin lists are unordered (atomics): the closest hit is the minimum of
+// (distance, index) over the valid hits, which is exactly what the
+// reference's ascending loop with `distance >= best -> skip` returns, and a
+// shadow test is an any-hit search, so visiting order does not matter.
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "cg_rt_dev.h"
+
+namespace cg {
+
+constexpr int kBinW = 128, kBinH = 32;        // pixels; multiples of the 8x8 wave tile
+constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
+static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
+constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
+constexpr int kSurvCap = 2048;                // shadow survivors per wave staged in LDS
+
+struct BigBufs {
+    int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
+    int *sbin_list, *sbin_n;
+    int *hit_bi;                  // [9][rows_out * W]
+    float *hit_t;
+    ShadowBox *wave_box;          // [tiles_y][tiles_x]
+    ShadowBox *bin_box;           // [n_bins]
+    int cap, bins_x, bins_y, tiles_x, tiles_y;
+};
+
+// ---------------------------------------------------------------------------
+// Triangle tests with exact pre-rejections.  Both skip the IEEE divide only
+// when its outcome is certain:
+//  * t < 0: det and detT of opposite signs with |detT| >= 2^-60 |det|,
+//    |det| >= 2^-60 and len >= 2^-60, so t and distance = t*len are
+//    strictly negative (no underflow to -0): rejected at :311;
+//  * distance > bound: same signs and fl(|detT| len) >= fl(fl(|det| bound)
+//    (1 + 2^-18)) with the right side finite and >= 2^-100, which implies
+//    t*len >= bound (1 + 2^-20) and hence a rounded distance strictly above
+//    `bound` (:313 for the closest hit, :395 for a shadow ray).
+__device__ __forceinline__ bool surely_negative(float detT, float det, float len)
+{
+    const float adT = fabsf(detT), ad = fabsf(det);
+    return ((detT < 0.0f) != (det < 0.0f)) && detT != 0.0f && ad >= 0x1p-60f && len >= 0x1p-60f &&
+           adT >= ad * 0x1p-60f;
+}
+__device__ __forceinline__ bool surely_beyond(float detT, float det, float len, float bound)
+{
+    if (!((detT > 0.0f && det > 0.0f) || (detT < 0.0f && det < 0.0f))) return false;
+    const float rhs = (fabsf(det) * bound) * 1.000003814697265625f;   // 1 + 2^-18
+    return rhs <= FLT_MAX && rhs >= 0x1p-100f && fabsf(detT) * len >= rhs;
+}
+
+// One triangle, one camera sub-ray (camera-origin constants of RtTri):
+// lexicographic (distance, index) minimum.
+__device__ __forceinline__ void tri_closest(const RtTri &c, int k, vec3 nd, float len, float &best,
+                                            float &bt, int &bi)
+{
+    float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+    float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+    float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;      // det(-d, e1, e2) :289
+    if (surely_negative(c.detT, det, len)) return;
+    if (best < FLT_MAX && surely_beyond(c.detT, det, len, best)) return;
+    float t = c.detT / det;                                    // :306
+    float distance = t * len;                                  // :307
+    if (distance < 0.0f) return;                               // :311
+    if (distance > best || distance > FLT_MAX) return;         // :313
+    if (distance == best && k > bi) return;                    // ascending-index tie-break
+    float Q3 = nd.y * c.sz - c.sy * nd.z;
+    float detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;      // :317
+    float detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;      // :320
+    float u = detU / det;
+    float v = detV / det;
+    if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {             // :328-335
+        best = distance;
+        bt = t;
+        bi = k;
+    }
+}
+
+// One triangle, one shadow ray from `start` (generic start): accepted hit
+// with distance < rmag (skeleton.cpp:394-395).
+__device__ __forceinline__ bool tri_shadows(const RtTri &c, vec3 start, vec3 nd, float len, float rmag)
+{
+    float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
+    float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+    float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+    float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;
+    float K2 = sy * c.e2z - c.e2y * sz;
+    float K4 = sy * c.e1z - c.e1y * sz;
+    float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;
+    if (surely_negative(detT, det, len) || surely_beyond(detT, det, len, rmag)) return false;
+    float t = detT / det;
+    float distance = t * len;
+    if (distance < 0.0f) return false;
+    if (distance >= rmag || distance > FLT_MAX) return false;
+    float Q3 = nd.y * sz - sy * nd.z;
+    float K3 = c.e1y * sz - sy * c.e1z;
+    float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
+    float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
+    float u = detU / det;
+    float v = detV / det;
+    return (u >= 0) && (v >= 0) && ((u + v) <= 1);
+}
+
+// Exact float extremes of the camera sub-ray directions of a bin: dir =
+// R (u - W/2, v - H/2, f, 1) is monotone in u and in v (each float op is),
+// so the extremes are at the bin's corner pixels; +-0.5 as in the wave box.
+__device__ bool bin_bundle(const RtFrame &F, int bx, int by, float &x0, float &x1, float &y0, float &y1)
+{
+    const int u0 = bx * kBinW, u1 = min(F.W, u0 + kBinW) - 1;
+    const int L0 = by * kBinH, L1 = min(F.rows_out, L0 + kBinH) - 1;
+    const int v0 = shard_row(F, L0);
+    if (v0 >= F.H) return false;                      // padding rows only
+    const int v1 = min(shard_row(F, L1), F.H - 1);   // shard_row is increasing in L
+    x0 = y0 = FLT_MAX;
+    x1 = y1 = -FLT_MAX;
+    const int us[2] = {u0, u1}, vs[2] = {v0, v1};
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            vec4 d = mat4_mul(F.R, v4((float)(us[a] - F.W / 2), (float)(vs[b] - F.H / 2), F.focal, 1.0f));
+            x0 = fminf(x0, d.x); x1 = fmaxf(x1, d.x);
+            y0 = fminf(y0, d.y); y1 = fmaxf(y1, d.y);
+        }
+    x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    return true;
+}
+
+// Append the kept triangles of this workgroup to a bin list (one atomic per
+// workgroup); kept[r] is this thread's verdict on triangle base + r*256 + tid.
+__device__ __forceinline__ void bin_append(const bool kept[4], int base, int *list, int *count)
+{
+    __shared__ int s_w[4][4];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long m[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = __ballot(kept[r]);
+        if (lane == 0) s_w[r][w] = __popcll(m[r]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < 4; ++q) tot += s_w[r][q];
+        s_base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    int off = s_base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        int before = 0;
+        for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
+        if (kept[r]) list[off + before + __popcll(m[r] & lt)] = base + r * 256 + (int)threadIdx.x;
+        for (int q = 0; q < 4; ++q) off += s_w[r][q];
+    }
+}
+
+// K0: camera-ray certificate per (bin, triangle).
+__global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int bin = blockIdx.y;
+    float x0, x1, y0, y1;
+    if (!bin_bundle(F, bin % B.bins_x, bin / B.bins_x, x0, x1, y0, y1)) return;
+    const int base = blockIdx.x * kBinTris;
+    bool kept[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = base + r * 256 + (int)threadIdx.x;
+        kept[r] = i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal);
+    }
+    bin_append(kept, base, B.bin_list + (size_t)bin * B.cap, B.bin_n + bin);
+}
+
+// K1: closest hits of the 9 sub-rays of every pixel.
+__global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                                    const RtShade *__restrict__ shade,
+                                                                    const RtSphere *__restrict__ sph, BigBufs B)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
+    if (tx >= B.tiles_x) return;                                   // whole wave beyond W
+    const int u = tx * 8 + (lane & 7), L = ty * 8 + (lane >> 3);
+    const bool inside = u < F.W && L < F.rows_out;
+    const int v = inside ? shard_row(F, L) : 0;
+    const bool active = inside && v < F.H;
+    vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
+    dir = mat4_mul(F.R, dir);                                                         // :128
+    float x0 = wave_min(active ? dir.x : FLT_MAX), x1 = wave_max(active ? dir.x : -FLT_MAX);
+    float y0 = wave_min(active ? dir.y : FLT_MAX), y1 = wave_max(active ? dir.y : -FLT_MAX);
+    x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    const bool any = x0 <= x1;
+    const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
+    const int n = any ? B.bin_n[bin] : 0;
+    const int *list = B.bin_list + (size_t)bin * B.cap;
+    const float m = 0.5f;
+    float best[9], bt[9], len[9];
+    int bi[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+        const int i = s / 3 - 1, j = s % 3 - 1;
+        vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);       // :137
+        len[s] = length(nd);                                                          // :307
+        best[s] = FLT_MAX;
+        bt[s] = 0.0f;
+        bi[s] = INT_MIN;
+    }
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int cand = c0 + lane < n ? list[c0 + lane] : -1;
+        const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
+        unsigned long long mask = __ballot(keep);
+        while (mask) {
+            const int b = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+            const int k = __builtin_amdgcn_readlane(cand, b);
+            const RtTri T = tc[k];                                                    // scalar loads
+            if (active) {
+#pragma unroll
+                for (int s = 0; s < 9; ++s) {
+                    const int i = s / 3 - 1, j = s % 3 - 1;
+                    vec3 nd = -v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+                    tri_closest(T, k, nd, len[s], best[s], bt[s], bi[s]);
+                }
+            }
+        }
+    }
+    LaneShadowBox sb;
+    sb.init();
+    const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
+    if (active) {
+        const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+        const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
+#pragma unroll
+        for (int s = 0; s < 9; ++s) {
+            const int i = s / 3 - 1, j = s % 3 - 1;
+            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+            for (int q = 0; q < F.n_sph; ++q) {                                       // :341-355
+                float t;
+                if (sphere_intersect(sph[q], s3, nd, t) && t < best[s]) {
+                    best[s] = t;
+                    bt[s] = t;
+                    bi[s] = -1 - q;
+                }
+            }
+            const int hit = best[s] < FLT_MAX ? bi[s] : INT_MIN;                     // :357
+            B.hit_bi[s * npix + pix] = hit;
+            B.hit_t[s * npix + pix] = bt[s];
+            if (hit != INT_MIN && F.n_lights > 0) {
+                const float t = bt[s];
+                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+                shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, hit, pos));
+            }
+        }
+    }
+    ShadowBox W;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        W.lo[q] = wave_min(sb.lo[q]);
+        W.hi[q] = wave_max(sb.hi[q]);
+    }
+    W.pn = wave_max(sb.pn);
+    if (lane == 0) B.wave_box[(size_t)ty * B.tiles_x + tx] = W;
+}
+
+// K2: union of the wave boxes of each bin (one wave tile per lane).
+__global__ __launch_bounds__(64) void rt_bin_boxes_kernel(BigBufs B)
+{
+    const int bin = blockIdx.x, lane = threadIdx.x;
+    const int tx = (bin % B.bins_x) * kBinTilesX + (lane % kBinTilesX);
+    const int ty = (bin / B.bins_x) * kBinTilesY + (lane / kBinTilesX);
+    ShadowBox w;
+    w.lo[0] = w.lo[1] = w.lo[2] = FLT_MAX;
+    w.hi[0] = w.hi[1] = w.hi[2] = -FLT_MAX;
+    w.pn = 0.0f;
+    if (tx < B.tiles_x && ty < B.tiles_y) w = B.wave_box[(size_t)ty * B.tiles_x + tx];
+    ShadowBox r;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        r.lo[q] = wave_min(w.lo[q]);
+        r.hi[q] = wave_max(w.hi[q]);
+    }
+    r.pn = wave_max(w.pn);
+    if (lane == 0) B.bin_box[bin] = r;
+}
+
+// K3: shadow-ray certificate of the light set per (bin, triangle).
+__global__ __launch_bounds__(256) void rt_bin_shadow_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int bin = blockIdx.y;
+    const ShadowBox box = B.bin_box[bin];
+    if (!(box.lo[0] <= box.hi[0])) return;                         // no hits in this bin
+    const vec3 lc = v3(F.lc[0], F.lc[1], F.lc[2]);
+    const int base = blockIdx.x * kBinTris;
+    bool kept[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = base + r * 256 + (int)threadIdx.x;
+        kept[r] = i < F.n_tris && !cull_shadow(tc[i], lc, F.lrho, box);
+    }
+    bin_append(kept, base, B.sbin_list + (size_t)bin * B.cap, B.sbin_n + bin);
+}
+
+// DirectLight (skeleton.cpp:366-415) with the shadow ray tested against the
+// wave's survivors (or, after an LDS overflow, the whole shadow bin list).
+__device__ __forceinline__ vec3 big_direct_light(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                 const RtShade *__restrict__ shade,
+                                                 const RtSphere *__restrict__ sph, int bi, vec3 pos,
+                                                 vec3 normal, vec3 objColor, int l, const int *surv,
+                                                 int ns, bool from_lds)
+{
+    const RtLight Lt = F.lights[l];
+    vec3 lp = v3(Lt.x, Lt.y, Lt.z);
+    vec3 r = lp - pos;                                                   // :370
+    double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
+           r2 = (double)r.z * (double)r.z;
+    float rmag = (float)sqrt((r0 + r1) + r2);                            // :371
+    vec3 origin = pos + normal * 0.00001f;                              // :394
+    vec3 nd = -r;
+    float len = length(r);
+    bool shadow = false;
+    for (int i = 0; i < ns; ++i) {
+        const int k = __builtin_amdgcn_readfirstlane(surv[i]);
+        if (tri_shadows(tc[k], origin, nd, len, rmag)) {
+            shadow = true;
+            break;
+        }
+    }
+    (void)from_lds;
+    if (!shadow)
+        for (int q = 0; q < F.n_sph; ++q) {
+            float t;
+            if (sphere_intersect(sph[q], origin, r, t) && t < rmag) {
+                shadow = true;
+                break;
+            }
+        }
+    if (shadow) return v3(0.0f, 0.0f, 0.0f);                             // :394-398
+    vec3 ndn = normalize(r);                                             // :400
+    float a = dot(ndn, normal);                                          // :403
+    const float b = (float)(4 * M_PI);                                   // :404
+    float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
+    if (a <= 0) a = 0.f;                                                 // :409
+    vec3 lc = v3(Lt.r, Lt.g, Lt.b);
+    return ((objColor * lc) * a) / area;                                 // :412
+}
+
+// K4: shading in the reference's order (:143-166).
+__global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                                  const RtShade *__restrict__ shade,
+                                                                  const RtSphere *__restrict__ sph, BigBufs B,
+                                                                  uint32_t *__restrict__ out)
+{
+    __shared__ int s_surv[kRtThreads / 64][kSurvCap];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
+    if (tx >= B.tiles_x) return;
+    const int u = tx * 8 + (lane & 7), L = ty * 8 + (lane >> 3);
+    const bool inside = u < F.W && L < F.rows_out;
+    const int v = inside ? shard_row(F, L) : 0;
+    const bool active = inside && v < F.H;
+    const ShadowBox box = B.wave_box[(size_t)ty * B.tiles_x + tx];
+    const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
+    const int *slist = B.sbin_list + (size_t)bin * B.cap;
+    const int sn = box.lo[0] <= box.hi[0] && F.n_lights > 0 ? B.sbin_n[bin] : 0;
+    const vec3 lc = v3(F.lc[0], F.lc[1], F.lc[2]);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int ns = 0;
+    for (int c0 = 0; c0 < sn; c0 += 64) {
+        const int cand = c0 + lane < sn ? slist[c0 + lane] : -1;
+        const bool keep = cand >= 0 && !cull_shadow(tc[cand], lc, F.lrho, box);
+        const unsigned long long mk = __ballot(keep);
+        const int pos = ns + __popcll(mk & lt);
+        if (keep && pos < kSurvCap) s_surv[wave][pos] = cand;
+        ns += __popcll(mk);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const bool from_lds = ns <= kSurvCap;
+    const int *surv = from_lds ? s_surv[wave] : slist;
+    const int nsurv = from_lds ? ns : sn;
+    if (!inside) return;
+    uint32_t px = 0u;
+    if (active) {
+        const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
+        vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);    // :126
+        dir = mat4_mul(F.R, dir);                                                     // :128
+        const float m = 0.5f;
+        vec3 pc = v3(0.0f, 0.0f, 0.0f);
+        bool valid = false;
+        const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
+        for (int s = 0; s < 9; ++s) {
+            const int i = s / 3 - 1, j = s % 3 - 1;
+            const int bi = B.hit_bi[s * npix + pix];
+            if (bi == INT_MIN) continue;
+            const float t = B.hit_t[s * npix + pix];
+            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);   // :137
+            vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+            valid = true;
+            vec3 oc = object_colour(shade, sph, bi);
+            vec3 normal = hit_normal(shade, sph, bi, pos);
+            for (int l = 0; l < F.n_lights; ++l)                                      // :151-153
+                pc = pc + big_direct_light(F, tc, shade, sph, bi, pos, normal, oc, l, surv, nsurv, from_lds);
+            pc = pc + (oc * ind);                                                     // :156
+        }
+        px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));         // :160-166
+    }
+    out[(size_t)L * F.W + u] = px;
+}
+
+// ---------------------------------------------------------------------------
+BigBufs big_layout(const RtFrame &F, int cap)
+{
+    BigBufs B{};
+    B.cap = cap;
+    B.bins_x = (F.W + kBinW - 1) / kBinW;
+    B.bins_y = (F.rows_out + kBinH - 1) / kBinH;
+    B.tiles_x = (F.W + 7) / 8;
+    B.tiles_y = (F.rows_out + 7) / 8;
+    return B;
+}
+
+// Bytes of device scratch for big_layout(F, cap), and its carving.
+size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
+{
+    const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
+    const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
+    return 2 * bins * B.cap * 4 + 2 * bins * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) + 256;
+}
+void big_carve(BigBufs &B, const RtFrame &F, void *base)
+{
+    const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
+    const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
+    char *p = (char *)base;
+    B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears both
+    B.sbin_n = (int *)p; p += bins * 4;
+    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
+    B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
+    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    B.hit_bi = (int *)p;   p += 9 * npix * 4;
+    B.hit_t = (float *)p;  p += 9 * npix * 4;
+    B.bin_list = (int *)p; p += bins * B.cap * 4;
+    B.sbin_list = (int *)p;
+}
+
+hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
+                         void *scratch, uint32_t *d_out, hipStream_t st)
+{
+    BigBufs B = big_layout(F, F.n_tris);
+    big_carve(B, F, scratch);
+    const int bins = B.bins_x * B.bins_y;
+    hipError_t e = hipMemsetAsync(B.bin_n, 0, 2 * (size_t)bins * 4, st);
+    if (e != hipSuccess) return e;
+    const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
+    const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
+    hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+    hipLaunchKernelGGL(rt_big_primary_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+    hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
+    hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+    hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    return hipGetLastError();
+}
+
+// Diagnostics (CG_RT_BIG_DIAG=1): bin list sizes of the last frame.
+void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
+{
+    BigBufs B = big_layout(F, F.n_tris);
+    big_carve(B, F, scratch);
+    const int bins = B.bins_x * B.bins_y;
+    std::vector<int> n(2 * (size_t)bins);
+    if (hipMemcpyAsync(n.data(), B.bin_n, n.size() * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return;
+    long long s0 = 0, s1 = 0;
+    int m0 = 0, m1 = 0;
+    for (int b = 0; b < bins; ++b) {
+        s0 += n[b]; s1 += n[bins + b];
+        m0 = std::max(m0, n[b]); m1 = std::max(m1, n[bins + b]);
+    }
+    fprintf(stderr, "[cg_rt_big] bins %d: primary lists mean %lld max %d; shadow lists mean %lld max %d\n", bins,
+            s0 / bins, m0, s1 / bins, m1);
+}
+
+size_t rt_big_scratch_bytes(const RtFrame &F)
+{
+    BigBufs B = big_layout(F, F.n_tris);
+    return big_scratch_bytes(B, F);
+}
+
+}  // namespace cg

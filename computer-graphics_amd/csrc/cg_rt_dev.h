@@ -1,0 +1,436 @@
+// cg_rt_dev.h -- raytracer device functions shared by the Cornell-box kernel
+// (cg_rt.hip, <= 64 triangles, one certificate mask per wave) and the
+// large-scene binned kernels (cg_rt_big.hip).  Every float op follows
+// raytracer/Source/skeleton.cpp + GLM 0.9.7.2 association (see cg_math.h).
+#pragma once
+
+#include <float.h>
+
+#include "cg_internal.h"
+
+namespace cg {
+
+// ---------------------------------------------------------------------------
+// Sphere::intersect + solveQuadratic (raytracer/Source/TestModelH.h:24-66).
+__device__ __forceinline__ bool sphere_intersect(const RtSphere &S, vec3 start, vec3 dir, float &t)
+{
+    vec3 L = start - v3(S.cx, S.cy, S.cz);            // :48
+    float a = dot(dir, dir);                           // :49
+    float b = 2 * dot(dir, L);                         // :50
+    float c = dot(L, L) - S.r2;                        // :51
+    float x0, x1;
+    float disc = (b * b) - ((4 * a) * c);              // :27
+    if (disc < 0) return false;                        // :28
+    if (disc == 0) {                                   // :29, FP64 divide
+        x1 = (float)((-0.5 * (double)b) / (double)a);
+        x0 = x1;
+    } else {                                           // :31-35
+        float q;
+        if (b > 0) q = (float)(-0.5 * (double)(b + sqrtf(disc)));
+        else q = (float)(-0.5 * (double)(b - sqrtf(disc)));
+        x0 = q / a;
+        x1 = c / q;
+    }
+    if (x0 > x1) { float tmp = x0; x0 = x1; x1 = tmp; }   // :37 (and :54)
+    if (x0 < 0) {                                      // :57-61
+        x0 = x1;
+        if (x0 < 0) return false;
+    }
+    t = x0;
+    return true;
+}
+
+__device__ __forceinline__ vec3 object_colour(const RtShade *__restrict__ shade,
+                                              const RtSphere *__restrict__ sph, int bi)
+{
+    if (bi >= 0) {
+        RtShade s = shade[bi];
+        return v3(s.cr, s.cg, s.cb);
+    }
+    const RtSphere S = sph[-1 - bi];
+    return v3(S.cr, S.cg, S.cb);
+}
+
+__device__ __forceinline__ vec3 hit_normal(const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
+                                           int bi, vec3 pos)
+{
+    if (bi >= 0) {                                                       // :377-380
+        RtShade s = shade[bi];
+        return v3(s.nx, s.ny, s.nz);
+    }
+    const RtSphere S = sph[-1 - bi];                                     // :381-387
+    return normalize(pos - v3(S.cx, S.cy, S.cz));
+}
+
+// ---------------------------------------------------------------------------
+// Per-wave culling certificate for camera-origin rays.
+//
+// For a ray d from the camera, the reference's triangle test (skeleton.cpp:
+// 289-335) computes, in float, det = det3(-d, e1, e2), detU = det3(-d, s, e2),
+// detV = det3(-d, e1, s) with s = cam - v0 -- in exact arithmetic the linear
+// forms -d.(e1 x e2), -d.(s x e2), -d.(e1 x s).  A triangle is skipped for the
+// whole wave only if, for EVERY d of the wave's bundle (the box spanned by the
+// 9 sub-ray directions of its 64 pixels, exact float extremes), the float
+// evaluation is certain to reject it: det has a certain sign and t < 0, or
+// u < 0, or v < 0, or u + v > 1.  The linear forms are evaluated exactly
+// enough in FP64 and each float det3 evaluation is bounded by 16*eps times the
+// sum of its |triple products| (gamma_4 suffices), so a skipped triangle
+// could never have been accepted: results are bit-identical to testing all.
+__device__ __forceinline__ void lin_range(double cx, double cy, double hx, double hy, double f,
+                                          double X, double Y, double Z, double &lo, double &hi)
+{
+    // range of -d.(X,Y,Z) over d = (cx +- hx, cy +- hy, f)
+    double c = -(cx * X + cy * Y + f * Z);
+    double h = hx * fabs(X) + hy * fabs(Y);
+    lo = c - h;
+    hi = c + h;
+}
+
+__device__ __forceinline__ double det3_bound(double Dx, double Dy, double Dz, vec3 a, vec3 b)
+{
+    // sum of |triple products| of det3(-d, a, b) with |d| <= (Dx, Dy, Dz)
+    return Dx * (fabs((double)a.y * b.z) + fabs((double)b.y * a.z)) +
+           fabs((double)a.x) * (Dy * fabs((double)b.z) + fabs((double)b.y) * Dz) +
+           fabs((double)b.x) * (Dy * fabs((double)a.z) + fabs((double)a.y) * Dz);
+}
+
+__device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double g = 16.0 * eps;
+    vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z), s = v3(c.sx, c.sy, c.sz);
+    // N = e1 x e2, A = s x e2, B = e1 x s (float inputs: products exact in FP64)
+    double Nx = (double)e1.y * e2.z - (double)e2.y * e1.z, Ny = (double)e1.z * e2.x - (double)e2.z * e1.x,
+           Nz = (double)e1.x * e2.y - (double)e2.x * e1.y;
+    double Ax = (double)s.y * e2.z - (double)e2.y * s.z, Ay = (double)s.z * e2.x - (double)e2.z * s.x,
+           Az = (double)s.x * e2.y - (double)e2.x * s.y;
+    double Bx = (double)e1.y * s.z - (double)s.y * e1.z, By = (double)e1.z * s.x - (double)s.z * e1.x,
+           Bz = (double)e1.x * s.y - (double)s.x * e1.y;
+    double cx = 0.5 * ((double)x0 + x1), cy = 0.5 * ((double)y0 + y1);
+    double hx = 0.5 * ((double)x1 - x0), hy = 0.5 * ((double)y1 - y0), fz = f;
+    double Dx = fmax(fabs((double)x0), fabs((double)x1)), Dy = fmax(fabs((double)y0), fabs((double)y1)),
+           Dz = fabs(fz);
+    double dlo, dhi, ulo, uhi, vlo, vhi, blo, bhi;
+    lin_range(cx, cy, hx, hy, fz, Nx, Ny, Nz, dlo, dhi);
+    lin_range(cx, cy, hx, hy, fz, Ax, Ay, Az, ulo, uhi);
+    lin_range(cx, cy, hx, hy, fz, Bx, By, Bz, vlo, vhi);
+    lin_range(cx, cy, hx, hy, fz, Ax + Bx - Nx, Ay + By - Ny, Az + Bz - Nz, blo, bhi);
+    double Ed = g * det3_bound(Dx, Dy, Dz, e1, e2) + 1e-12 * (fabs(dlo) + fabs(dhi));
+    double Eu = g * det3_bound(Dx, Dy, Dz, s, e2) + 1e-12 * (fabs(ulo) + fabs(uhi));
+    double Ev = g * det3_bound(Dx, Dy, Dz, e1, s) + 1e-12 * (fabs(vlo) + fabs(vhi));
+    double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
+    if (!(isfinite(dlo) && isfinite(dhi) && isfinite(Ed + Eu + Ev + Eb) && isfinite(ulo + uhi + vlo + vhi + blo + bhi)))
+        return false;
+    int sg;
+    if (dlo - Ed > 0) sg = 1;
+    else if (dhi + Ed < 0) sg = -1;
+    else return false;                                   // det may vanish: keep
+    const double dmin = sg > 0 ? dlo - Ed : -(dhi + Ed);  // |det| >= dmin > 0
+    const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
+    // t = detT/det < 0 (and not underflowing to -0): distance < 0 rejects (:311)
+    double dT = c.detT;
+    if (dT != 0.0 && ((dT > 0) != (sg > 0)) && fabs(dT) > 1e-20 * dmax) return true;
+    // u < 0 or v < 0 (:328)
+    // (the quotient must not underflow to -0, which would pass u >= 0)
+    const double tiny = 1e-20 * dmax;
+    if (sg > 0 ? (uhi + Eu < -tiny) : (ulo - Eu > tiny)) return true;
+    if (sg > 0 ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) return true;
+    // u + v > 1 after float rounding of u, v and their sum: certain when
+    // (U + V - 1) > 4 eps (|U| + |V| + 1), U = detU/det, V = detV/det
+    double K = (fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev) / dmin + 1.0;
+    double margin = 4.0 * eps * K;
+    if (sg > 0 ? ((blo - Eb) / dmax > margin) : ((-(bhi + Eb)) / dmax > margin)) return true;
+    return false;
+}
+
+__device__ __forceinline__ float wave_min(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Per-wave culling certificate for DirectLight's shadow rays (skeleton.cpp:394).
+//
+// A shadow ray starts at S = P + n*1e-5 with direction d = L - P (the float
+// vectors the reference uses).  With a = L - v0 and p = S - L + d (a few 1e-5
+// at most, plus the rounding of s = S - v0), exact arithmetic gives
+//   det  = -d.(e1 x e2)                      (linear in d)
+//   detU = -d.(a x e2) - [d, p, e2]          (linear + |d||p||e2|)
+//   detV = -d.(e1 x a) - [d, e1, p]
+//   detT - det = a.(e1 x e2) + p.(e1 x e2)   (constant + |p||N|)
+// so over the wave's box of d the same certificate as for camera rays holds,
+// plus "the triangle lies beyond the light" (t > 1 + 1e-5, hence distance >=
+// rmag: no shadow).  `pn` bounds |p| (Euclidean) over the wave.
+struct ShadowBox {
+    float lo[3], hi[3];   // exact float extremes of d over the casting lanes
+    float pn;             // bound on |S - L + d| over the casting lanes
+};
+
+__device__ static bool cull_shadow(const RtTri &c, vec3 L, double rho, const ShadowBox &B)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double g = 16.0 * eps;
+    vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z);
+    double ax = (double)L.x - c.v0x, ay = (double)L.y - c.v0y, az = (double)L.z - c.v0z;
+    double Nx = (double)e1.y * e2.z - (double)e2.y * e1.z, Ny = (double)e1.z * e2.x - (double)e2.z * e1.x,
+           Nz = (double)e1.x * e2.y - (double)e2.x * e1.y;
+    double Ax = ay * e2.z - (double)e2.y * az, Ay = az * e2.x - (double)e2.z * ax, Az = ax * e2.y - (double)e2.x * ay;
+    double Bx = (double)e1.y * az - ay * e1.z, By = (double)e1.z * ax - az * e1.x, Bz = (double)e1.x * ay - ax * e1.y;
+    double cx = 0.5 * ((double)B.lo[0] + B.hi[0]), cy = 0.5 * ((double)B.lo[1] + B.hi[1]),
+           cz = 0.5 * ((double)B.lo[2] + B.hi[2]);
+    double hx = 0.5 * ((double)B.hi[0] - B.lo[0]), hy = 0.5 * ((double)B.hi[1] - B.lo[1]),
+           hz = 0.5 * ((double)B.hi[2] - B.lo[2]);
+    auto lin = [&](double X, double Y, double Z, double &lo, double &hi) {
+        double m = -(cx * X + cy * Y + cz * Z);
+        double h = hx * fabs(X) + hy * fabs(Y) + hz * fabs(Z);
+        lo = m - h;
+        hi = m + h;
+    };
+    double Dx = fmax(fabs((double)B.lo[0]), fabs((double)B.hi[0]));
+    double Dy = fmax(fabs((double)B.lo[1]), fabs((double)B.hi[1]));
+    double Dz = fmax(fabs((double)B.lo[2]), fabs((double)B.hi[2]));
+    double dn = sqrt(Dx * Dx + Dy * Dy + Dz * Dz);
+    // |s| <= |a| + |d| + |p| componentwise; p also absorbs s's own rounding
+    double Sx = fabs(ax) + rho + Dx + B.pn, Sy = fabs(ay) + rho + Dy + B.pn, Sz = fabs(az) + rho + Dz + B.pn;
+    double pn = (double)B.pn + eps * sqrt(Sx * Sx + Sy * Sy + Sz * Sz) + 1e-12;
+    double n1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    double n2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    double nN = sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+    double dlo, dhi, ulo, uhi, vlo, vhi, blo, bhi;
+    lin(Nx, Ny, Nz, dlo, dhi);
+    lin(Ax, Ay, Az, ulo, uhi);
+    lin(Bx, By, Bz, vlo, vhi);
+    lin(Ax + Bx - Nx, Ay + By - Ny, Az + Bz - Nz, blo, bhi);
+    // float-evaluation bounds (sum of |triple products|)
+    auto M3 = [](double x0, double y0, double z0, double x1, double y1, double z1, double x2, double y2,
+                 double z2) {   // |c0|,|c1|,|c2| components of det3(c0, c1, c2)
+        return x0 * (y1 * z2 + y2 * z1) + x1 * (y0 * z2 + y2 * z0) + x2 * (y0 * z1 + y1 * z0);
+    };
+    double ae1x = fabs((double)e1.x), ae1y = fabs((double)e1.y), ae1z = fabs((double)e1.z);
+    double ae2x = fabs((double)e2.x), ae2y = fabs((double)e2.y), ae2z = fabs((double)e2.z);
+    double Ed = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + 1e-12 * (fabs(dlo) + fabs(dhi));
+    double Eu = g * M3(Dx, Dy, Dz, Sx, Sy, Sz, ae2x, ae2y, ae2z) + dn * (pn + rho) * n2 + 1e-12 * (fabs(ulo) + fabs(uhi));
+    double Ev = g * M3(Dx, Dy, Dz, ae1x, ae1y, ae1z, Sx, Sy, Sz) + dn * (pn + rho) * n1 + 1e-12 * (fabs(vlo) + fabs(vhi));
+    double Et = g * M3(Sx, Sy, Sz, ae1x, ae1y, ae1z, ae2x, ae2y, ae2z) + (pn + rho) * nN;
+    double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
+    double aN = ax * Nx + ay * Ny + az * Nz;
+    double EaN = 1e-12 * (fabs(ax * Nx) + fabs(ay * Ny) + fabs(az * Nz));
+    if (!(isfinite(dlo + dhi + ulo + uhi + vlo + vhi + blo + bhi) && isfinite(Ed + Eu + Ev + Et + Eb + aN)))
+        return false;
+    int sg;
+    if (dlo - Ed > 0) sg = 1;
+    else if (dhi + Ed < 0) sg = -1;
+    else return false;
+    const double dmin = sg > 0 ? dlo - Ed : -(dhi + Ed);
+    const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
+    const double tiny = 1e-20 * dmax;
+    // detT = det + aN + (p.N): t = 1 + (detT - det)/det
+    double tlo = (aN - EaN - Et - Ed) / 1.0, thi = aN + EaN + Et + Ed;   // range of detT - det
+    // beyond the light: t - 1 > 1e-5 certain -> distance >= rmag (:395)
+    if (sg > 0 ? (tlo > 1e-5 * dmax) : (thi < -1e-5 * dmax)) return true;
+    // t < 0: detT = det + (detT - det) has the opposite sign of det, i.e.
+    // (detT - det)/det < -1 - margin
+    if (sg > 0 ? (thi + dmax < -tiny - 1e-6 * dmax) : (tlo - dmax > tiny + 1e-6 * dmax)) return true;
+    if (sg > 0 ? (uhi + Eu < -tiny) : (ulo - Eu > tiny)) return true;
+    if (sg > 0 ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) return true;
+    double K = (fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev) / dmin + 1.0;
+    double margin = 4.0 * eps * K;
+    if (sg > 0 ? ((blo - Eb) / dmax > margin) : ((-(bhi + Eb)) / dmax > margin)) return true;
+    return false;
+}
+
+// ClosestIntersection for camera-origin rays (skeleton.cpp:263-363).
+// Returns best index: >= 0 triangle, -1 - k sphere k, INT_MIN no hit; t out.
+// Triangles are visited in index order; with CULL only those whose bit is set
+// in `mask` (certified-rejected ones are skipped, see cull_primary).
+template <bool CULL>
+__device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__restrict__ tc,
+                                               const RtSphere *__restrict__ sph, vec3 d,
+                                               float &best_t, unsigned long long mask)
+{
+    const float bound = FLT_MAX;
+    float best = bound;
+    int bi = INT_MIN;
+    float bt = 0.f;
+    vec3 nd = -d;
+    float len = length(d);                                   // :307
+    for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
+        int k = it;
+        if (CULL) {
+            k = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+        }
+        const RtTri c = tc[k];
+        float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+        float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+        float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;  // det(-d, e1, e2) :289
+        float t = c.detT / det;                               // :306
+        float distance = t * len;                             // :307
+        if (distance < 0.0f) continue;                        // :311
+        if (distance >= best || distance > bound) continue;   // :313
+        float Q3 = nd.y * c.sz - c.sy * nd.z;
+        float detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;  // det(-d, s, e2) :317
+        float detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;  // det(-d, e1, s) :320
+        float u = detU / det;
+        float v = detV / det;
+        if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {        // :328-335
+            best = distance;
+            bt = t;
+            bi = k;
+        }
+    }
+    vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+#ifdef CG_ABLATE_SPHERE
+    if (0)
+#endif
+    for (int k = 0; k < F.n_sph; ++k) {                       // :341-355
+        float t;
+        if (sphere_intersect(sph[k], s3, d, t)) {
+            if (t < best) {
+                best = t;
+                bt = t;
+                bi = -1 - k;
+            }
+        }
+    }
+    best_t = bt;
+    return best < bound ? bi : INT_MIN;                       // :357
+}
+
+// Shadow test of DirectLight (skeleton.cpp:394-398): ClosestIntersection
+// from `start` towards the light, shadowed iff its distance < rmag.  The
+// closest distance is < rmag iff SOME accepted hit is, so this is an
+// any-hit search bounded by rmag with an early exit; triangles are tested
+// with the reference's float ops (their acceptance does not depend on the
+// running minimum, only on `distance < rmag` here).
+template <bool CULL>
+__device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restrict__ tc,
+                                         const RtSphere *__restrict__ sph, vec3 start, vec3 d,
+                                         float rmag, unsigned long long mask)
+{
+    const float bound = FLT_MAX;
+    vec3 nd = -d;
+    float len = length(d);
+    for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
+        int k = it;
+        if (CULL) {
+            k = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+        }
+        const RtTri c = tc[k];
+        float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
+        float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+        float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+        float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;
+        float K2 = sy * c.e2z - c.e2y * sz;
+        float K4 = sy * c.e1z - c.e1y * sz;
+        float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;                    // det(s, e1, e2)
+        float t = detT / det;
+        float distance = t * len;
+        if (distance < 0.0f) continue;
+        if (distance >= rmag || distance > bound) continue;
+        float Q3 = nd.y * sz - sy * nd.z;
+        float K3 = c.e1y * sz - sy * c.e1z;
+        float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
+        float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
+        float u = detU / det;
+        float v = detV / det;
+        if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) return true;
+    }
+#ifdef CG_ABLATE_SPHERE
+    if (0)
+#endif
+    for (int k = 0; k < F.n_sph; ++k) {
+        float t;
+        if (sphere_intersect(sph[k], start, d, t) && t < rmag) return true;
+    }
+    return false;
+}
+
+// DirectLight (skeleton.cpp:366-415) for a hit at `pos` on object `bi`.
+template <bool CULL>
+__device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__restrict__ tc,
+                                             const RtShade *__restrict__ shade,
+                                             const RtSphere *__restrict__ sph, int bi, vec3 pos,
+                                             vec3 objColor, int l, unsigned long long smask = ~0ull)
+{
+    const RtLight Lt = F.lights[l];                                      // uniform: scalar loads
+    vec3 lp = v3(Lt.x, Lt.y, Lt.z);
+    vec3 r = lp - pos;                                                   // :370
+    double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
+           r2 = (double)r.z * (double)r.z;
+    float rmag = (float)sqrt((r0 + r1) + r2);                            // :371
+    vec3 normal = hit_normal(shade, sph, bi, pos);
+    vec3 origin = pos + normal * 0.00001f;                              // :394
+#ifndef CG_ABLATE_SHADOW
+    if (shadowed<CULL>(F, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
+#endif
+    vec3 nd = normalize(r);                                              // :400
+    float a = dot(nd, normal);                                           // :403
+    const float b = (float)(4 * M_PI);                                   // :404
+    float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
+    if (a <= 0) a = 0.f;                                                 // :409
+    vec3 lc = v3(Lt.r, Lt.g, Lt.b);
+    return ((objColor * lc) * a) / area;                                 // :412
+}
+
+// Shadow-ray certificate for light l: per-lane box of d = L - pos and bound
+// on |S - L + d| over the hits given, reduced over the wave into one mask.
+struct LaneShadowBox {
+    float lo[3], hi[3], pn;
+    __device__ void init()
+    {
+        lo[0] = lo[1] = lo[2] = FLT_MAX;
+        hi[0] = hi[1] = hi[2] = -FLT_MAX;
+        pn = 0.0f;
+    }
+};
+
+__device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lmin, vec3 lmax, vec3 pos, vec3 normal)
+{
+    // d_k = fl(L_k - pos) (:370/:373) is monotone in L_k, so every light's
+    // direction lies in [fl(lmin - pos), fl(lmax - pos)] componentwise.
+    vec3 rlo = lmin - pos, rhi = lmax - pos;
+    vec3 S = pos + normal * 0.00001f;                                    // :394
+    // p_k = S - L_k + d_k = (S - pos) + rounding(d_k): |p_k| <= |S - pos|_1 + 2^-24 |d|_1
+    double sp = fabs((double)S.x - pos.x) + fabs((double)S.y - pos.y) + fabs((double)S.z - pos.z);
+    double dr = fmax(fabs((double)rlo.x), fabs((double)rhi.x)) + fmax(fabs((double)rlo.y), fabs((double)rhi.y)) +
+                fmax(fabs((double)rlo.z), fabs((double)rhi.z));
+    float pb = (float)((sp + 5.9604644775390625e-8 * dr) * (1.0 + 1e-6) + 1e-30);
+    b.lo[0] = fminf(b.lo[0], rlo.x); b.hi[0] = fmaxf(b.hi[0], rhi.x);
+    b.lo[1] = fminf(b.lo[1], rlo.y); b.hi[1] = fmaxf(b.hi[1], rhi.y);
+    b.lo[2] = fminf(b.lo[2], rlo.z); b.hi[2] = fmaxf(b.hi[2], rhi.z);
+    b.pn = fmaxf(b.pn, pb);
+}
+
+// Whole wave, converged control flow.
+__device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                             const LaneShadowBox &b, int lane)
+{
+    ShadowBox B;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        B.lo[c] = wave_min(b.lo[c]);
+        B.hi[c] = wave_max(b.hi[c]);
+    }
+    B.pn = wave_max(b.pn);
+    bool keep = true;
+    if (lane < F.n_tris && B.lo[0] <= B.hi[0])
+        keep = !cull_shadow(tc[lane], v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, B);
+    return __ballot(keep && lane < F.n_tris);
+}
+
+__device__ __forceinline__ int shard_row(const RtFrame &F, int L)
+{
+    int k = L / F.stripe_h;
+    return (k * F.nranks + F.rank) * F.stripe_h + (L - k * F.stripe_h);
+}
+
+}  // namespace cg

@@ -17,6 +17,10 @@ namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, int, const float *, RtTri *, RtShade *, hipStream_t);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             uint32_t *, hipStream_t);
+hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, void *, uint32_t *,
+                         hipStream_t);
+size_t rt_big_scratch_bytes(const RtFrame &);
+void rt_big_diag(const RtFrame &, void *, hipStream_t);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, uint32_t *, hipStream_t);
 hipError_t launch_rt_probe_closest(const RtFrame &, const cg_tri *, const RtSphere *,
                                    const cg_vec4 *, const cg_vec4 *, int, cg_isect *, int *,
@@ -64,7 +68,7 @@ struct cg_ctx {
     std::string err;
     // RT scene
     int n_tris = -1, n_sph = 0;
-    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights;
+    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big;
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
@@ -150,7 +154,7 @@ extern "C" void cg_destroy(cg_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->tris, &c->tc, &c->shade, &c->sph, &c->frame,
-                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights};
+                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights, &c->big};
     for (DevBuf *b : bufs) b->release();
     rast_release(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -283,6 +287,15 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t 
 {
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, F.cam, (RtTri *)c->tc.p,
                                 (RtShade *)c->shade.p, st), "rt_prepare launch");
+    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) {
+        // large scene: binned certificates (cg_rt_big.hip)
+        CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
+        CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
+                                c->big.p, d_out, st), "rt_big launch");
+        static const bool diag = getenv("CG_RT_BIG_DIAG") != nullptr;
+        if (diag) rt_big_diag(F, c->big.p, st);
+        return CG_OK;
+    }
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                (const RtSphere *)c->sph.p, d_out, st), "rt_pixel launch");
     return CG_OK;
