@@ -48,6 +48,15 @@ struct RtSphere {
     float cr, cg, cb, pad;  // color
 };
 
+// Uniform grid over a large scene's triangles (heuristic blocker search for
+// shadow rays; never a culling structure, see cg_rt_big.hip).
+struct RtGrid {
+    float lo[3], inv_h, h;      // cell (i, j, k) spans lo + h * [i, i + 1) x ...
+    int res[3];
+    const int *start;           // [cells + 1] prefix offsets into tris; null = no grid
+    const int *tris;
+};
+
 // Frame arguments, passed by value (kernarg -> SGPRs).
 struct RtFrame {
     int W, H;

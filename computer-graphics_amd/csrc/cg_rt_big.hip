@@ -22,6 +22,8 @@
 // reference's ascending loop with `distance >= best -> skip` returns, and a
 // shadow test is an any-hit search, so visiting order does not matter.
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -33,7 +35,6 @@ constexpr int kBinW = 128, kBinH = 32;        // pixels; multiples of the 8x8 wa
 constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
 static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
 constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
-constexpr int kSurvCap = 2048;                // shadow survivors per wave staged in LDS
 
 struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
@@ -42,7 +43,9 @@ struct BigBufs {
     float *hit_t;
     ShadowBox *wave_box;          // [tiles_y][tiles_x]
     ShadowBox *bin_box;           // [n_bins]
+    RtGrid grid;
     int cap, bins_x, bins_y, tiles_x, tiles_y;
+    unsigned long long *diag;     // CG_RT_BIG_DIAG: [waves, survivors, walk steps, lit rays, primary cands, primary kept]
 };
 
 // ---------------------------------------------------------------------------
@@ -228,6 +231,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
         const int cand = c0 + lane < n ? list[c0 + lane] : -1;
         const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
         unsigned long long mask = __ballot(keep);
+
         while (mask) {
             const int b = __builtin_ctzll(mask);
             mask &= mask - 1ull;
@@ -319,57 +323,140 @@ __global__ __launch_bounds__(256) void rt_bin_shadow_kernel(RtFrame F, const RtT
     bin_append(kept, base, B.sbin_list + (size_t)bin * B.cap, B.sbin_n + bin);
 }
 
-// DirectLight (skeleton.cpp:366-415) with the shadow ray tested against the
-// wave's survivors (or, after an LDS overflow, the whole shadow bin list).
-__device__ __forceinline__ vec3 big_direct_light(const RtFrame &F, const RtTri *__restrict__ tc,
-                                                 const RtShade *__restrict__ shade,
-                                                 const RtSphere *__restrict__ sph, int bi, vec3 pos,
-                                                 vec3 normal, vec3 objColor, int l, const int *surv,
-                                                 int ns, bool from_lds)
+// Shadow ray of DirectLight (skeleton.cpp:370-394) for hit `pos` and light l.
+struct ShadowRay {
+    vec3 origin, nd, r;
+    float len, rmag;
+};
+__device__ __forceinline__ ShadowRay shadow_ray(const RtLight &Lt, vec3 pos, vec3 normal)
 {
-    const RtLight Lt = F.lights[l];
-    vec3 lp = v3(Lt.x, Lt.y, Lt.z);
-    vec3 r = lp - pos;                                                   // :370
-    double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
-           r2 = (double)r.z * (double)r.z;
-    float rmag = (float)sqrt((r0 + r1) + r2);                            // :371
-    vec3 origin = pos + normal * 0.00001f;                              // :394
-    vec3 nd = -r;
-    float len = length(r);
-    bool shadow = false;
-    for (int i = 0; i < ns; ++i) {
-        const int k = __builtin_amdgcn_readfirstlane(surv[i]);
-        if (tri_shadows(tc[k], origin, nd, len, rmag)) {
-            shadow = true;
-            break;
-        }
+    ShadowRay q;
+    q.r = v3(Lt.x, Lt.y, Lt.z) - pos;                                    // :370
+    double r0 = (double)q.r.x * (double)q.r.x, r1 = (double)q.r.y * (double)q.r.y,
+           r2 = (double)q.r.z * (double)q.r.z;
+    q.rmag = (float)sqrt((r0 + r1) + r2);                                // :371
+    q.origin = pos + normal * 0.00001f;                                 // :394
+    q.nd = -q.r;
+    q.len = length(q.r);
+    return q;
+}
+
+// DirectLight's value once the shadow verdict on the triangles is known
+// (spheres are tested here, :341-355 then :395).
+__device__ __forceinline__ vec3 big_direct_light(const RtFrame &F, const RtSphere *__restrict__ sph,
+                                                 const RtLight &Lt, const ShadowRay &q, vec3 normal,
+                                                 vec3 objColor, bool tri_shadow)
+{
+    bool shadow = tri_shadow;
+    for (int k = 0; k < F.n_sph && !shadow; ++k) {
+        float t;
+        if (sphere_intersect(sph[k], q.origin, q.r, t) && t < q.rmag) shadow = true;
     }
-    (void)from_lds;
-    if (!shadow)
-        for (int q = 0; q < F.n_sph; ++q) {
-            float t;
-            if (sphere_intersect(sph[q], origin, r, t) && t < rmag) {
-                shadow = true;
-                break;
-            }
-        }
     if (shadow) return v3(0.0f, 0.0f, 0.0f);                             // :394-398
-    vec3 ndn = normalize(r);                                             // :400
+    vec3 ndn = normalize(q.r);                                           // :400
     float a = dot(ndn, normal);                                          // :403
     const float b = (float)(4 * M_PI);                                   // :404
-    float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
+    float area = (float)((double)b * ((double)q.rmag * (double)q.rmag)); // :406
     if (a <= 0) a = 0.f;                                                 // :409
     vec3 lc = v3(Lt.r, Lt.g, Lt.b);
     return ((objColor * lc) * a) / area;                                 // :412
 }
 
-// K4: shading in the reference's order (:143-166).
+// any-hit of one shadow ray over a uniform list of triangle indices: the
+// blocking triangle, or -1.
+__device__ __forceinline__ int any_hit(const RtTri *__restrict__ tc, const int *list, int n, const ShadowRay &q,
+                                       unsigned long long *diag = nullptr)
+{
+    int i = 0, hit = -1;
+    for (; i < n; ++i) {
+        const int k = __builtin_amdgcn_readfirstlane(list[i]);
+        if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) {
+            hit = k;
+            break;
+        }
+    }
+    if (diag) {
+        atomicAdd(&diag[2], (unsigned long long)(i + 1));
+        atomicAdd(&diag[6], 1ull);
+    }
+    return hit;
+}
+
+// Blocker search along the shadow segment S + t (L - P), t in [0, 1], through
+// the scene grid (3D DDA), testing each cell's triangles with the exact
+// reference test.  Heuristic only: a triangle it returns really blocks the
+// ray (the float test accepted it); when it finds none the caller runs the
+// exhaustive certified search.
+__device__ int grid_blocker(const RtGrid &G, const RtTri *__restrict__ tc, const ShadowRay &q, int *ntest = nullptr)
+{
+    if (!G.start) return -1;
+    const float o[3] = {q.origin.x, q.origin.y, q.origin.z}, d[3] = {q.r.x, q.r.y, q.r.z};
+    float t0 = 0.0f, t1 = 1.0f;
+    for (int a = 0; a < 3; ++a) {
+        const float lo = G.lo[a], hi = G.lo[a] + (float)G.res[a] * G.h;
+        if (fabsf(d[a]) < 1e-30f) {
+            if (o[a] < lo || o[a] > hi) return -1;
+            continue;
+        }
+        float ta = (lo - o[a]) / d[a], tb = (hi - o[a]) / d[a];
+        if (ta > tb) { float x = ta; ta = tb; tb = x; }
+        t0 = fmaxf(t0, ta);
+        t1 = fminf(t1, tb);
+    }
+    if (!(t0 <= t1)) return -1;
+    int c[3], step[3];
+    float tmax[3], tdel[3];
+    for (int a = 0; a < 3; ++a) {
+        const float p = o[a] + d[a] * t0;
+        c[a] = min(max((int)floorf((p - G.lo[a]) * G.inv_h), 0), G.res[a] - 1);
+        if (fabsf(d[a]) < 1e-30f) {
+            step[a] = 0;
+            tmax[a] = FLT_MAX;
+            tdel[a] = FLT_MAX;
+        } else {
+            step[a] = d[a] > 0.0f ? 1 : -1;
+            const float bound = G.lo[a] + (float)(c[a] + (step[a] > 0 ? 1 : 0)) * G.h;
+            tmax[a] = (bound - o[a]) / d[a];
+            tdel[a] = G.h / fabsf(d[a]);
+        }
+    }
+    const int max_steps = G.res[0] + G.res[1] + G.res[2] + 3;
+    for (int it = 0; it < max_steps; ++it) {
+        const int cell = (c[2] * G.res[1] + c[1]) * G.res[0] + c[0];
+        for (int i = G.start[cell], e = G.start[cell + 1]; i < e; ++i) {
+            const int k = G.tris[i];
+            if (ntest) ++*ntest;
+            if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) return k;
+        }
+        const int a = tmax[0] < tmax[1] ? (tmax[0] < tmax[2] ? 0 : 2) : (tmax[1] < tmax[2] ? 1 : 2);
+        if (tmax[a] > t1) break;
+        c[a] += step[a];
+        if (c[a] < 0 || c[a] >= G.res[a]) break;
+        tmax[a] += tdel[a];
+    }
+    return -1;
+}
+
+// K4: shadow verdicts, then shading in the reference's order (:143-166).
+//  1. Each shadow ray (sub-ray s, light l) tries likely blockers: the
+//     triangle it starts on (the 1e-5 normal offset puts the origin behind it
+//     when the normal faces away from the light), the lane's previous
+//     blocker, then the scene grid.  Any triangle the exact test accepts
+//     blocks it -- an any-hit verdict does not depend on the order.
+//  2. Rays still unresolved (unblocked, or the heuristics missed) get the
+//     exhaustive search: the wave certifies its bin's shadow list against
+//     the box of just those rays (one candidate per lane, LDS segments of
+//     kSegCap survivors) and walks the survivors.
+// One verdict bit per (s, l) needs 9 * n_lights <= 64; with more lights the
+// shading loop resolves each pair itself (grid, then the whole bin list).
+constexpr int kSegCap = 2048;
+
 __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph, BigBufs B,
                                                                   uint32_t *__restrict__ out)
 {
-    __shared__ int s_surv[kRtThreads / 64][kSurvCap];
+    __shared__ int s_seg[kRtThreads / 64][kSegCap];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
@@ -377,33 +464,105 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
     const bool inside = u < F.W && L < F.rows_out;
     const int v = inside ? shard_row(F, L) : 0;
     const bool active = inside && v < F.H;
-    const ShadowBox box = B.wave_box[(size_t)ty * B.tiles_x + tx];
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
     const int *slist = B.sbin_list + (size_t)bin * B.cap;
-    const int sn = box.lo[0] <= box.hi[0] && F.n_lights > 0 ? B.sbin_n[bin] : 0;
-    const vec3 lc = v3(F.lc[0], F.lc[1], F.lc[2]);
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    int ns = 0;
-    for (int c0 = 0; c0 < sn; c0 += 64) {
-        const int cand = c0 + lane < sn ? slist[c0 + lane] : -1;
-        const bool keep = cand >= 0 && !cull_shadow(tc[cand], lc, F.lrho, box);
-        const unsigned long long mk = __ballot(keep);
-        const int pos = ns + __popcll(mk & lt);
-        if (keep && pos < kSurvCap) s_surv[wave][pos] = cand;
-        ns += __popcll(mk);
+    const int sn = F.n_lights > 0 ? B.sbin_n[bin] : 0;
+    const size_t npix = (size_t)F.rows_out * F.W, pix = active ? (size_t)L * F.W + u : 0;
+    vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
+    dir = mat4_mul(F.R, dir);                                                         // :128
+    const float m = 0.5f;
+    const bool flags_fit = 9 * F.n_lights <= 64;
+    unsigned long long shadowed = 0ull, pending = 0ull;   // bit s * n_lights + l
+    LaneShadowBox pb;
+    pb.init();
+    int gtests = 0;
+    const long long tk0 = B.diag ? clock64() : 0;
+    if (flags_fit && active && F.n_lights > 0) {
+        int last = -1;
+        for (int s = 0; s < 9; ++s) {
+            const int bi = B.hit_bi[s * npix + pix];
+            if (bi == INT_MIN) continue;
+            const int i = s / 3 - 1, j = s % 3 - 1;
+            const float t = B.hit_t[s * npix + pix];
+            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);   // :137
+            vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+            vec3 normal = hit_normal(shade, sph, bi, pos);
+            for (int l = 0; l < F.n_lights; ++l) {
+                const RtLight Lt = F.lights[l];
+                const ShadowRay q = shadow_ray(Lt, pos, normal);
+                int k = -1;
+                if (bi >= 0 && tri_shadows(tc[bi], q.origin, q.nd, q.len, q.rmag)) k = bi;
+                else if (last >= 0 && tri_shadows(tc[last], q.origin, q.nd, q.len, q.rmag)) k = last;
+                else k = grid_blocker(B.grid, tc, q, &gtests);
+                const unsigned long long bit = 1ull << (s * F.n_lights + l);
+                if (k >= 0) {
+                    shadowed |= bit;
+                    last = k;
+                } else {
+                    pending |= bit;
+                    const vec3 lp = v3(Lt.x, Lt.y, Lt.z);
+                    shadow_box_add(pb, lp, lp, pos, normal);
+                }
+            }
+        }
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    const bool from_lds = ns <= kSurvCap;
-    const int *surv = from_lds ? s_surv[wave] : slist;
-    const int nsurv = from_lds ? ns : sn;
+    long long tk1 = 0;
+    if (B.diag) {
+        atomicAdd(&B.diag[3], (unsigned long long)__popcll(pending));
+        atomicAdd(&B.diag[7], (unsigned long long)gtests);
+        tk1 = clock64();
+        if (lane == 0) {
+            atomicAdd(&B.diag[0], 1ull);
+            atomicAdd(&B.diag[4], (unsigned long long)(tk1 - tk0));
+        }
+    }
+    if (__ballot(pending != 0ull) != 0ull) {
+        // exhaustive search for the unresolved rays only
+        ShadowBox box;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            box.lo[q] = wave_min(pb.lo[q]);
+            box.hi[q] = wave_max(pb.hi[q]);
+        }
+        box.pn = wave_max(pb.pn);
+        const vec3 lcen = v3(F.lc[0], F.lc[1], F.lc[2]);
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        for (int c0 = 0; c0 < sn;) {
+            int ns = 0;
+            for (; c0 < sn && ns + 64 <= kSegCap; c0 += 64) {
+                const int cand = c0 + lane < sn ? slist[c0 + lane] : -1;
+                const bool keep = cand >= 0 && !cull_shadow(tc[cand], lcen, F.lrho, box);
+                const unsigned long long mk = __ballot(keep);
+                if (keep) s_seg[wave][ns + __popcll(mk & lt)] = cand;
+                ns += __popcll(mk);
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (B.diag && lane == 0) atomicAdd(&B.diag[1], (unsigned long long)ns);
+            for (unsigned long long p = pending; p != 0ull; p &= p - 1ull) {
+                const int bit = __builtin_ctzll(p), s = bit / F.n_lights, l = bit - s * F.n_lights;
+                const int bi = B.hit_bi[s * npix + pix];
+                const int i = s / 3 - 1, j = s % 3 - 1;
+                const float t = B.hit_t[s * npix + pix];
+                vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+                const ShadowRay q = shadow_ray(F.lights[l], pos, hit_normal(shade, sph, bi, pos));
+                if (any_hit(tc, s_seg[wave], ns, q, B.diag) >= 0) {
+                    shadowed |= 1ull << bit;
+                    pending &= ~(1ull << bit);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();     // segment reused
+            if (__ballot(pending != 0ull) == 0ull) break;
+        }
+        if (B.diag && lane == 0) {
+            atomicAdd(&B.diag[5], (unsigned long long)(clock64() - tk1));
+            atomicAdd(&B.diag[1], 1ull << 32);
+        }
+    }
     if (!inside) return;
     uint32_t px = 0u;
     if (active) {
-        const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
-        vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);    // :126
-        dir = mat4_mul(F.R, dir);                                                     // :128
-        const float m = 0.5f;
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
@@ -417,8 +576,14 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
             valid = true;
             vec3 oc = object_colour(shade, sph, bi);
             vec3 normal = hit_normal(shade, sph, bi, pos);
-            for (int l = 0; l < F.n_lights; ++l)                                      // :151-153
-                pc = pc + big_direct_light(F, tc, shade, sph, bi, pos, normal, oc, l, surv, nsurv, from_lds);
+            for (int l = 0; l < F.n_lights; ++l) {                                    // :151-153
+                const RtLight Lt = F.lights[l];
+                const ShadowRay q = shadow_ray(Lt, pos, normal);
+                bool ts;
+                if (flags_fit) ts = ((shadowed >> (s * F.n_lights + l)) & 1ull) != 0;
+                else ts = grid_blocker(B.grid, tc, q) >= 0 || any_hit(tc, slist, sn, q) >= 0;
+                pc = pc + big_direct_light(F, sph, Lt, q, normal, oc, ts);
+            }
             pc = pc + (oc * ind);                                                     // :156
         }
         px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));         // :160-166
@@ -463,10 +628,17 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
 }
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
-                         void *scratch, uint32_t *d_out, hipStream_t st)
+                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st)
 {
     BigBufs B = big_layout(F, F.n_tris);
     big_carve(B, F, scratch);
+    B.grid = grid;
+    static const bool diag = getenv("CG_RT_BIG_DIAG") != nullptr;
+    if (diag) {
+        B.diag = (unsigned long long *)((char *)scratch + big_scratch_bytes(B, F) - 64);
+        hipError_t e = hipMemsetAsync(B.diag, 0, 64, st);
+        if (e != hipSuccess) return e;
+    }
     const int bins = B.bins_x * B.bins_y;
     hipError_t e = hipMemsetAsync(B.bin_n, 0, 2 * (size_t)bins * 4, st);
     if (e != hipSuccess) return e;
@@ -498,6 +670,83 @@ void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
     }
     fprintf(stderr, "[cg_rt_big] bins %d: primary lists mean %lld max %d; shadow lists mean %lld max %d\n", bins,
             s0 / bins, m0, s1 / bins, m1);
+    unsigned long long d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpy(d, (char *)scratch + big_scratch_bytes(B, F) - 64, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess)
+        fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays in %llu waves, "
+                "exhaustive survivors %llu, walks %llu (%.1f steps each); wave clocks: heuristics %.3g, exhaustive %.3g\n",
+                d[0], d[7], d[3], d[1] >> 32, d[1] & 0xffffffffull, d[6], d[6] ? (double)d[2] / d[6] : 0.0,
+                (double)d[4], (double)d[5]);
+}
+
+// Host build of the scene grid: cubic cells sized for ~2 triangle centroids
+// per cell, each triangle listed in every cell its bounding box touches.
+// Returns false (no grid) when the lists would exceed max_entries.
+bool rt_grid_build(const cg_tri *t, int n, RtGrid &g, std::vector<int> &start, std::vector<int> &tris,
+                   size_t max_entries)
+{
+    if (n <= 0) return false;
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    auto bb = [&](const cg_tri &q, float mn[3], float mx[3]) {
+        const cg_vec4 *v[3] = {&q.v0, &q.v1, &q.v2};
+        for (int a = 0; a < 3; ++a) { mn[a] = FLT_MAX; mx[a] = -FLT_MAX; }
+        for (const cg_vec4 *p : v) {
+            const float c[3] = {p->x, p->y, p->z};
+            for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], c[a]); mx[a] = std::max(mx[a], c[a]); }
+        }
+    };
+    for (int i = 0; i < n; ++i) {
+        float mn[3], mx[3];
+        bb(t[i], mn, mx);
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], mn[a]); hi[a] = std::max(hi[a], mx[a]); }
+    }
+    double ext[3], vol = 1.0;
+    for (int a = 0; a < 3; ++a) {
+        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
+        lo[a] -= 1e-4f;
+        hi[a] += 1e-4f;
+        ext[a] = (double)hi[a] - lo[a];
+        vol *= ext[a];
+    }
+    double h = std::cbrt(vol / std::max(1.0, n / 2.0));
+    for (int a = 0; a < 3; ++a) h = std::max(h, ext[a] / 512.0);
+    for (int a = 0; a < 3; ++a) {
+        g.lo[a] = lo[a];
+        g.res[a] = std::max(1, std::min(512, (int)std::ceil(ext[a] / h)));
+    }
+    g.h = (float)h;
+    g.inv_h = (float)(1.0 / h);
+    const size_t cells = (size_t)g.res[0] * g.res[1] * g.res[2];
+    auto range = [&](const cg_tri &q, int c0[3], int c1[3]) {
+        float mn[3], mx[3];
+        bb(q, mn, mx);
+        for (int a = 0; a < 3; ++a) {
+            c0[a] = std::min(std::max((int)std::floor((mn[a] - g.lo[a]) * g.inv_h), 0), g.res[a] - 1);
+            c1[a] = std::min(std::max((int)std::floor((mx[a] - g.lo[a]) * g.inv_h), 0), g.res[a] - 1);
+        }
+    };
+    std::vector<int> count(cells + 1, 0);
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        int c0[3], c1[3];
+        range(t[i], c0, c1);
+        total += (size_t)(c1[0] - c0[0] + 1) * (c1[1] - c0[1] + 1) * (c1[2] - c0[2] + 1);
+        if (total > max_entries) return false;
+        for (int z = c0[2]; z <= c1[2]; ++z)
+            for (int y = c0[1]; y <= c1[1]; ++y)
+                for (int x = c0[0]; x <= c1[0]; ++x) ++count[((size_t)z * g.res[1] + y) * g.res[0] + x];
+    }
+    start.assign(cells + 1, 0);
+    for (size_t c = 0; c < cells; ++c) start[c + 1] = start[c] + count[c];
+    tris.assign(total, 0);
+    std::vector<int> fill(start.begin(), start.end() - 1);
+    for (int i = 0; i < n; ++i) {
+        int c0[3], c1[3];
+        range(t[i], c0, c1);
+        for (int z = c0[2]; z <= c1[2]; ++z)
+            for (int y = c0[1]; y <= c1[1]; ++y)
+                for (int x = c0[0]; x <= c1[0]; ++x) tris[fill[((size_t)z * g.res[1] + y) * g.res[0] + x]++] = i;
+    }
+    return true;
 }
 
 size_t rt_big_scratch_bytes(const RtFrame &F)

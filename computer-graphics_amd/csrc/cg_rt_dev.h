@@ -94,6 +94,29 @@ __device__ __forceinline__ double det3_bound(double Dx, double Dy, double Dz, ve
            fabs((double)b.x) * (Dy * fabs((double)a.z) + fabs((double)a.y) * Dz);
 }
 
+// The float det's sign is uncertain over the bundle.  A float hit still needs
+// u, v >= 0 and u + v <= 1, i.e. detU, detV and W = det - detU - detV (exact
+// linear forms over the bundle) all of the float det's sign, up to their
+// error bounds.  Away from the triangle's plane detU, detV and W have mixed
+// signs (they sum to det ~ 0), so the triangle is rejected when, for each
+// sign the float det can take, one of them certainly has the other sign.
+// b = detU + detV - det = -W (range [blo, bhi], evaluation error in Eb).
+// Float u + v <= 1 with det_f > 0 implies U + V - D <= Ew (first-order
+// rounding of the two quotients and their sum, 4 eps to spare).
+__device__ __forceinline__ bool sign_free_reject(double dlo, double dhi, double Ed, double ulo, double uhi,
+                                                 double Eu, double vlo, double vhi, double Ev, double blo,
+                                                 double bhi, double Eb)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double dmx = fmax(fabs(dlo - Ed), fabs(dhi + Ed));   // max |det_f|
+    const double tiny = 1e-20 * dmx;                           // quotients stay clear of -0
+    const double umx = fmax(fabs(ulo), fabs(uhi)) + Eu, vmx = fmax(fabs(vlo), fabs(vhi)) + Ev;
+    const double Ew = Eb * (1.0 + 4.0 * eps) + 4.0 * eps * (umx + vmx + dmx) + tiny;
+    if (dhi + Ed > 0.0 && !((uhi + Eu < -tiny) || (vhi + Ev < -tiny) || (blo > Ew))) return false;
+    if (dlo - Ed < 0.0 && !((ulo - Eu > tiny) || (vlo - Ev > tiny) || (bhi < -Ew))) return false;
+    return true;
+}
+
 __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f)
 {
     const double eps = 5.9604644775390625e-8;   // 2^-24
@@ -124,7 +147,7 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
     int sg;
     if (dlo - Ed > 0) sg = 1;
     else if (dhi + Ed < 0) sg = -1;
-    else return false;                                   // det may vanish: keep
+    else return sign_free_reject(dlo, dhi, Ed, ulo, uhi, Eu, vlo, vhi, Ev, blo, bhi, Eb);   // det may vanish
     const double dmin = sg > 0 ? dlo - Ed : -(dhi + Ed);  // |det| >= dmin > 0
     const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
     // t = detT/det < 0 (and not underflowing to -0): distance < 0 rejects (:311)
@@ -227,7 +250,7 @@ __device__ static bool cull_shadow(const RtTri &c, vec3 L, double rho, const Sha
     int sg;
     if (dlo - Ed > 0) sg = 1;
     else if (dhi + Ed < 0) sg = -1;
-    else return false;
+    else return sign_free_reject(dlo, dhi, Ed, ulo, uhi, Eu, vlo, vhi, Ev, blo, bhi, Eb);   // det may vanish
     const double dmin = sg > 0 ? dlo - Ed : -(dhi + Ed);
     const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
     const double tiny = 1e-20 * dmax;

@@ -17,8 +17,9 @@ namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, int, const float *, RtTri *, RtShade *, hipStream_t);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             uint32_t *, hipStream_t);
-hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, void *, uint32_t *,
-                         hipStream_t);
+hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
+                         uint32_t *, hipStream_t);
+bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &);
 void rt_big_diag(const RtFrame &, void *, hipStream_t);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, uint32_t *, hipStream_t);
@@ -68,7 +69,8 @@ struct cg_ctx {
     std::string err;
     // RT scene
     int n_tris = -1, n_sph = 0;
-    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big;
+    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
+    RtGrid grid{};                      // large scenes only (n_tris > 64)
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
@@ -154,7 +156,8 @@ extern "C" void cg_destroy(cg_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->tris, &c->tc, &c->shade, &c->sph, &c->frame,
-                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights, &c->big};
+                      &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights, &c->big,
+                      &c->gstart, &c->gtris};
     for (DevBuf *b : bufs) b->release();
     rast_release(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -191,6 +194,21 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     if (n_spheres)
         CG_TRY(c, hipMemcpyAsync(c->sph.p, S.data(), S.size() * sizeof(RtSphere),
                                  hipMemcpyHostToDevice, c->stream), "upload spheres");
+    c->grid = RtGrid{};
+    if (n_tris > 64) {   // large scene: grid for the shadow-ray blocker search
+        std::vector<int> gs, gt;
+        RtGrid g{};
+        if (rt_grid_build(tris, n_tris, g, gs, gt, (size_t)64 << 20)) {
+            CG_TRY(c, c->gstart.ensure(gs.size() * 4), "alloc grid");
+            CG_TRY(c, c->gtris.ensure(std::max<size_t>(gt.size(), 1) * 4), "alloc grid");
+            CG_TRY(c, hipMemcpy(c->gstart.p, gs.data(), gs.size() * 4, hipMemcpyHostToDevice), "upload grid");
+            if (!gt.empty())
+                CG_TRY(c, hipMemcpy(c->gtris.p, gt.data(), gt.size() * 4, hipMemcpyHostToDevice), "upload grid");
+            g.start = (const int *)c->gstart.p;
+            g.tris = (const int *)c->gtris.p;
+            c->grid = g;
+        }
+    }
     CG_TRY(c, hipStreamSynchronize(c->stream), "scene upload");
     c->n_tris = n_tris;
     c->n_sph = n_spheres;
@@ -291,7 +309,7 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t 
         // large scene: binned certificates (cg_rt_big.hip)
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
         CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
-                                c->big.p, d_out, st), "rt_big launch");
+                                c->grid, c->big.p, d_out, st), "rt_big launch");
         static const bool diag = getenv("CG_RT_BIG_DIAG") != nullptr;
         if (diag) rt_big_diag(F, c->big.p, st);
         return CG_OK;
