@@ -35,6 +35,9 @@ constexpr int kBinW = 128, kBinH = 32;        // pixels; multiples of the 8x8 wa
 constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
 static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
 constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
+constexpr int kPendCap = 4096;                // certified candidates kept per pending ray
+constexpr int kMaxPend = 32768;               // pending rays with their own certified list
+constexpr int kPendGridY = 128;               // workgroup rows of the pending-certify kernel
 
 struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
@@ -44,6 +47,14 @@ struct BigBufs {
     ShadowBox *wave_box;          // [tiles_y][tiles_x]
     ShadowBox *bin_box;           // [n_bins]
     RtGrid grid;
+    // shadow verdicts (9 * n_lights <= 64): per pixel, bit s * n_lights + l
+    unsigned long long *sh_bits, *pend_bits;
+    int *pend_n;                  // pixels with unresolved rays (counter, after bin_n/sbin_n)
+    int *pend_pix;                // [kMaxPend] pending ray: local pixel index L * W + u
+    int *pend_bit;                // [kMaxPend] and its verdict bit s * n_lights + l
+    ShadowBox *pend_box;          // [kMaxPend] box of their unresolved rays
+    int *pend_cnt;                // [kMaxPend] certified candidates found per pending pixel
+    int *pend_list;               // [kMaxPend][kPendCap]
     int cap, bins_x, bins_y, tiles_x, tiles_y;
     unsigned long long *diag;     // CG_RT_BIG_DIAG: [waves, survivors, walk steps, lit rays, primary cands, primary kept]
 };
@@ -174,6 +185,39 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
         int before = 0;
         for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
         if (kept[r]) list[off + before + __popcll(m[r] & lt)] = base + r * 256 + (int)threadIdx.x;
+        for (int q = 0; q < 4; ++q) off += s_w[r][q];
+    }
+}
+
+// bin_append with a capacity: the count keeps growing past `cap` (the reader
+// detects the overflow), entries past it are dropped.
+__device__ __forceinline__ void bin_append_capped(const bool kept[4], int base, int *list, int *count, int cap)
+{
+    __shared__ int s_w[4][4];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long m[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = __ballot(kept[r]);
+        if (lane == 0) s_w[r][w] = __popcll(m[r]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < 4; ++q) tot += s_w[r][q];
+        s_base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    int off = s_base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        int before = 0;
+        for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
+        const int pos = off + before + __popcll(m[r] & lt);
+        if (kept[r] && pos < cap) list[pos] = base + r * 256 + (int)threadIdx.x;
         for (int q = 0; q < 4; ++q) off += s_w[r][q];
     }
 }
@@ -437,26 +481,44 @@ __device__ int grid_blocker(const RtGrid &G, const RtTri *__restrict__ tc, const
     return -1;
 }
 
-// K4: shadow verdicts, then shading in the reference's order (:143-166).
-//  1. Each shadow ray (sub-ray s, light l) tries likely blockers: the
-//     triangle it starts on (the 1e-5 normal offset puts the origin behind it
-//     when the normal faces away from the light), the lane's previous
-//     blocker, then the scene grid.  Any triangle the exact test accepts
-//     blocks it -- an any-hit verdict does not depend on the order.
-//  2. Rays still unresolved (unblocked, or the heuristics missed) get the
-//     exhaustive search: the wave certifies its bin's shadow list against
-//     the box of just those rays (one candidate per lane, LDS segments of
-//     kSegCap survivors) and walks the survivors.
-// One verdict bit per (s, l) needs 9 * n_lights <= 64; with more lights the
-// shading loop resolves each pair itself (grid, then the whole bin list).
-constexpr int kSegCap = 2048;
-
-__global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
-                                                                  const RtShade *__restrict__ shade,
-                                                                  const RtSphere *__restrict__ sph, BigBufs B,
-                                                                  uint32_t *__restrict__ out)
+// Shadow verdicts for 9 * n_lights <= 64, in three parallel steps:
+//  K4 rt_shadow_hints   each shadow ray (sub-ray s, light l) tries likely
+//                       blockers: the triangle it starts on (the 1e-5 normal
+//                       offset puts the origin behind it when the normal faces
+//                       away from the light), the lane's previous blocker, then
+//                       the scene grid.  Any triangle the exact test accepts
+//                       blocks the ray (an any-hit verdict does not depend on
+//                       the order).  Unresolved rays are marked pending; a
+//                       wave with pending rays registers the box of just those
+//                       rays.
+//  K5 rt_pending_cert   every triangle against every registered box (shadow
+//                       certificate), survivors appended per pending wave;
+//  K6 rt_pending_walk   the pending rays walk their wave's survivors (or, past
+//                       kPendCap survivors, every triangle): the exhaustive
+//                       search that makes the verdict exact.
+__device__ __forceinline__ void hit_geometry(const RtFrame &F, const BigBufs &B, const RtShade *__restrict__ shade,
+                                             const RtSphere *__restrict__ sph, vec4 dir, int s, size_t pix,
+                                             size_t npix, int &bi, vec3 &pos, vec3 &normal)
 {
-    __shared__ int s_seg[kRtThreads / 64][kSegCap];
+    const float m = 0.5f;
+    bi = B.hit_bi[s * npix + pix];
+    if (bi == INT_MIN) return;
+    const int i = s / 3 - 1, j = s % 3 - 1;
+    const float t = B.hit_t[s * npix + pix];
+    vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);           // :137
+    pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);         // :326/:345
+    normal = hit_normal(shade, sph, bi, pos);
+}
+
+__device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
+{
+    return mat4_mul(F.R, v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f));   // :126-128
+}
+
+__global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                                     const RtShade *__restrict__ shade,
+                                                                     const RtSphere *__restrict__ sph, BigBufs B)
+{
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
@@ -464,29 +526,17 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
     const bool inside = u < F.W && L < F.rows_out;
     const int v = inside ? shard_row(F, L) : 0;
     const bool active = inside && v < F.H;
-    const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
-    const int *slist = B.sbin_list + (size_t)bin * B.cap;
-    const int sn = F.n_lights > 0 ? B.sbin_n[bin] : 0;
-    const size_t npix = (size_t)F.rows_out * F.W, pix = active ? (size_t)L * F.W + u : 0;
-    vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
-    dir = mat4_mul(F.R, dir);                                                         // :128
-    const float m = 0.5f;
-    const bool flags_fit = 9 * F.n_lights <= 64;
-    unsigned long long shadowed = 0ull, pending = 0ull;   // bit s * n_lights + l
-    LaneShadowBox pb;
-    pb.init();
+    const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
+    const vec4 dir = pixel_dir(F, u, v);
+    unsigned long long shadowed = 0ull, pending = 0ull;
     int gtests = 0;
-    const long long tk0 = B.diag ? clock64() : 0;
-    if (flags_fit && active && F.n_lights > 0) {
+    if (active) {
         int last = -1;
         for (int s = 0; s < 9; ++s) {
-            const int bi = B.hit_bi[s * npix + pix];
+            int bi;
+            vec3 pos, normal;
+            hit_geometry(F, B, shade, sph, dir, s, pix, npix, bi, pos, normal);
             if (bi == INT_MIN) continue;
-            const int i = s / 3 - 1, j = s % 3 - 1;
-            const float t = B.hit_t[s * npix + pix];
-            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);   // :137
-            vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
-            vec3 normal = hit_normal(shade, sph, bi, pos);
             for (int l = 0; l < F.n_lights; ++l) {
                 const RtLight Lt = F.lights[l];
                 const ShadowRay q = shadow_ray(Lt, pos, normal);
@@ -500,88 +550,138 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
                     last = k;
                 } else {
                     pending |= bit;
+                    LaneShadowBox pb;
+                    pb.init();
                     const vec3 lp = v3(Lt.x, Lt.y, Lt.z);
                     shadow_box_add(pb, lp, lp, pos, normal);
+                    const int p = atomicAdd(B.pend_n, 1);
+                    if (p < kMaxPend) {
+                        ShadowBox box;
+                        for (int c = 0; c < 3; ++c) {
+                            box.lo[c] = pb.lo[c];
+                            box.hi[c] = pb.hi[c];
+                        }
+                        box.pn = pb.pn;
+                        B.pend_pix[p] = (int)pix;
+                        B.pend_bit[p] = s * F.n_lights + l;
+                        B.pend_box[p] = box;
+                        B.pend_cnt[p] = 0;
+                    }
                 }
             }
         }
+        B.sh_bits[pix] = shadowed;
+        B.pend_bits[pix] = pending;
     }
-    long long tk1 = 0;
     if (B.diag) {
         atomicAdd(&B.diag[3], (unsigned long long)__popcll(pending));
         atomicAdd(&B.diag[7], (unsigned long long)gtests);
-        tk1 = clock64();
-        if (lane == 0) {
-            atomicAdd(&B.diag[0], 1ull);
-            atomicAdd(&B.diag[4], (unsigned long long)(tk1 - tk0));
-        }
+        if (lane == 0) atomicAdd(&B.diag[0], 1ull);
     }
-    if (__ballot(pending != 0ull) != 0ull) {
-        // exhaustive search for the unresolved rays only
-        ShadowBox box;
+}
+
+// K5: shadow certificate of the light set, every triangle against every
+// pending wave's box.
+__global__ __launch_bounds__(256) void rt_pending_cert_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int np = min(*B.pend_n, kMaxPend);
+    const vec3 lc = v3(F.lc[0], F.lc[1], F.lc[2]);
+    const int base = blockIdx.x * kBinTris;
+    for (int p = blockIdx.y; p < np; p += gridDim.y) {
+        const ShadowBox box = B.pend_box[p];
+        bool kept[4];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            box.lo[q] = wave_min(pb.lo[q]);
-            box.hi[q] = wave_max(pb.hi[q]);
+        for (int r = 0; r < 4; ++r) {
+            const int i = base + r * 256 + (int)threadIdx.x;
+            kept[r] = i < F.n_tris && !cull_shadow(tc[i], lc, F.lrho, box);
         }
-        box.pn = wave_max(pb.pn);
-        const vec3 lcen = v3(F.lc[0], F.lc[1], F.lc[2]);
-        const unsigned long long lt = (1ull << lane) - 1ull;
-        for (int c0 = 0; c0 < sn;) {
-            int ns = 0;
-            for (; c0 < sn && ns + 64 <= kSegCap; c0 += 64) {
-                const int cand = c0 + lane < sn ? slist[c0 + lane] : -1;
-                const bool keep = cand >= 0 && !cull_shadow(tc[cand], lcen, F.lrho, box);
-                const unsigned long long mk = __ballot(keep);
-                if (keep) s_seg[wave][ns + __popcll(mk & lt)] = cand;
-                ns += __popcll(mk);
-            }
-            __builtin_amdgcn_s_waitcnt(0);
-            __builtin_amdgcn_wave_barrier();
-            if (B.diag && lane == 0) atomicAdd(&B.diag[1], (unsigned long long)ns);
-            for (unsigned long long p = pending; p != 0ull; p &= p - 1ull) {
-                const int bit = __builtin_ctzll(p), s = bit / F.n_lights, l = bit - s * F.n_lights;
-                const int bi = B.hit_bi[s * npix + pix];
-                const int i = s / 3 - 1, j = s % 3 - 1;
-                const float t = B.hit_t[s * npix + pix];
-                vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
-                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
-                const ShadowRay q = shadow_ray(F.lights[l], pos, hit_normal(shade, sph, bi, pos));
-                if (any_hit(tc, s_seg[wave], ns, q, B.diag) >= 0) {
-                    shadowed |= 1ull << bit;
-                    pending &= ~(1ull << bit);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();     // segment reused
-            if (__ballot(pending != 0ull) == 0ull) break;
-        }
-        if (B.diag && lane == 0) {
-            atomicAdd(&B.diag[5], (unsigned long long)(clock64() - tk1));
-            atomicAdd(&B.diag[1], 1ull << 32);
-        }
+        bin_append_capped(kept, base, B.pend_list + (size_t)p * kPendCap, B.pend_cnt + p, kPendCap);
+        __syncthreads();
     }
+}
+
+// K6: the exhaustive search of the pending rays, one thread per ray over its
+// certified list (every triangle past kPendCap survivors).  Rays past
+// kMaxPend keep their pending bit for rt_big_shade_kernel.
+__global__ __launch_bounds__(256) void rt_pending_walk_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                              const RtShade *__restrict__ shade,
+                                                              const RtSphere *__restrict__ sph, BigBufs B)
+{
+    const int np = min(*B.pend_n, kMaxPend);
+    const size_t npix = (size_t)F.rows_out * F.W;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
+        const size_t pix = (size_t)B.pend_pix[p];
+        const int bit = B.pend_bit[p], cnt = B.pend_cnt[p];
+        const bool all = cnt > kPendCap;
+        const int n = all ? F.n_tris : cnt;
+        const int *list = B.pend_list + (size_t)p * kPendCap;
+        const int L = (int)(pix / F.W), u = (int)(pix - (size_t)L * F.W);
+        const vec4 dir = pixel_dir(F, u, shard_row(F, L));
+        const int s = bit / F.n_lights, l = bit - s * F.n_lights;
+        int bi;
+        vec3 pos, normal;
+        hit_geometry(F, B, shade, sph, dir, s, pix, npix, bi, pos, normal);
+        const ShadowRay q = shadow_ray(F.lights[l], pos, normal);
+        if (B.diag) {
+            atomicAdd(&B.diag[1], (unsigned long long)n);
+            atomicAdd(&B.diag[6], 1ull);
+        }
+        bool hit = false;
+        for (int i = 0; i < n && !hit; ++i) hit = tri_shadows(tc[all ? i : list[i]], q.origin, q.nd, q.len, q.rmag);
+        if (hit) atomicOr(&B.sh_bits[pix], 1ull << bit);
+        atomicAnd(&B.pend_bits[pix], ~(1ull << bit));
+    }
+}
+
+// K7: shading in the reference's order (:143-166) from the shadow verdicts;
+// with more than 7 lights each (s, l) is resolved here (grid, then the
+// bin's certified shadow list).
+__global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                                  const RtShade *__restrict__ shade,
+                                                                  const RtSphere *__restrict__ sph, BigBufs B,
+                                                                  uint32_t *__restrict__ out)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
+    if (tx >= B.tiles_x) return;
+    const int u = tx * 8 + (lane & 7), L = ty * 8 + (lane >> 3);
+    const bool inside = u < F.W && L < F.rows_out;
     if (!inside) return;
+    const int v = shard_row(F, L);
+    const bool active = v < F.H;
     uint32_t px = 0u;
     if (active) {
+        const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
+        const vec4 dir = pixel_dir(F, u, v);
+        const bool flags_fit = 9 * F.n_lights <= 64;
+        const unsigned long long shadowed = flags_fit && F.n_lights > 0 ? B.sh_bits[pix] : 0ull;
+        // pixels past kMaxPend still carry pending bits: exhaustive search here
+        const unsigned long long left = flags_fit && F.n_lights > 0 ? B.pend_bits[pix] : 0ull;
+        const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
+        const int *slist = B.sbin_list + (size_t)bin * B.cap;
+        const int sn = flags_fit ? 0 : B.sbin_n[bin];
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
         for (int s = 0; s < 9; ++s) {
-            const int i = s / 3 - 1, j = s % 3 - 1;
-            const int bi = B.hit_bi[s * npix + pix];
+            int bi;
+            vec3 pos, normal;
+            hit_geometry(F, B, shade, sph, dir, s, pix, npix, bi, pos, normal);
             if (bi == INT_MIN) continue;
-            const float t = B.hit_t[s * npix + pix];
-            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);   // :137
-            vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
             valid = true;
             vec3 oc = object_colour(shade, sph, bi);
-            vec3 normal = hit_normal(shade, sph, bi, pos);
             for (int l = 0; l < F.n_lights; ++l) {                                    // :151-153
                 const RtLight Lt = F.lights[l];
                 const ShadowRay q = shadow_ray(Lt, pos, normal);
                 bool ts;
-                if (flags_fit) ts = ((shadowed >> (s * F.n_lights + l)) & 1ull) != 0;
-                else ts = grid_blocker(B.grid, tc, q) >= 0 || any_hit(tc, slist, sn, q) >= 0;
+                const int bit = s * F.n_lights + l;
+                if (flags_fit) {
+                    ts = ((shadowed >> bit) & 1ull) != 0;
+                    if (!ts && ((left >> bit) & 1ull))
+                        for (int k = 0; k < F.n_tris && !ts; ++k) ts = tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag);
+                } else {
+                    ts = grid_blocker(B.grid, tc, q) >= 0 || any_hit(tc, slist, sn, q) >= 0;
+                }
                 pc = pc + big_direct_light(F, sph, Lt, q, normal, oc, ts);
             }
             pc = pc + (oc * ind);                                                     // :156
@@ -608,21 +708,32 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return 2 * bins * B.cap * 4 + 2 * bins * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) + 256;
+    return 2 * bins * B.cap * 4 + 2 * bins * 4 + 16 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
+           2 * npix * 8 + (size_t)kMaxPend * (4 + 4 + 4 + sizeof(ShadowBox)) + (size_t)kMaxPend * kPendCap * 4 + 512;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
     char *p = (char *)base;
-    B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears both
+    B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears them
     B.sbin_n = (int *)p; p += bins * 4;
+    B.pend_n = (int *)p; p += 16;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.hit_bi = (int *)p;   p += 9 * npix * 4;
     B.hit_t = (float *)p;  p += 9 * npix * 4;
+    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    B.sh_bits = (unsigned long long *)p;   p += npix * 8;
+    B.pend_bits = (unsigned long long *)p; p += npix * 8;
+    B.pend_box = (ShadowBox *)p;           p += (size_t)kMaxPend * sizeof(ShadowBox);
+    B.pend_pix = (int *)p;                 p += (size_t)kMaxPend * 4;
+    B.pend_bit = (int *)p;                 p += (size_t)kMaxPend * 4;
+    B.pend_cnt = (int *)p;                 p += (size_t)kMaxPend * 4;
+    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    B.pend_list = (int *)p;                p += (size_t)kMaxPend * kPendCap * 4;
     B.bin_list = (int *)p; p += bins * B.cap * 4;
     B.sbin_list = (int *)p;
 }
@@ -640,14 +751,21 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         if (e != hipSuccess) return e;
     }
     const int bins = B.bins_x * B.bins_y;
-    hipError_t e = hipMemsetAsync(B.bin_n, 0, 2 * (size_t)bins * 4, st);
+    hipError_t e = hipMemsetAsync(B.bin_n, 0, 2 * (size_t)bins * 4 + 16, st);
     if (e != hipSuccess) return e;
+    const bool flags_fit = 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
     hipLaunchKernelGGL(rt_big_primary_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-    hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
-    hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+    if (!flags_fit) {
+        hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
+        hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+    } else if (F.n_lights > 0) {
+        hipLaunchKernelGGL(rt_shadow_hints_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        hipLaunchKernelGGL(rt_pending_cert_kernel, dim3(bgrid.x, kPendGridY), dim3(256), 0, st, F, d_tc, B);
+        hipLaunchKernelGGL(rt_pending_walk_kernel, dim3(kMaxPend / 256), dim3(256), 0, st, F, d_tc, d_shade, d_sph, B);
+    }
     hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     return hipGetLastError();
 }
@@ -670,12 +788,27 @@ void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
     }
     fprintf(stderr, "[cg_rt_big] bins %d: primary lists mean %lld max %d; shadow lists mean %lld max %d\n", bins,
             s0 / bins, m0, s1 / bins, m1);
+    int np = 0;
+    if (hipMemcpy(&np, B.pend_n, 4, hipMemcpyDeviceToHost) == hipSuccess && np > 0) {
+        np = std::min(np, kMaxPend);
+        std::vector<int> cnt(np);
+        std::vector<ShadowBox> bx(np);
+        (void)hipMemcpy(cnt.data(), B.pend_cnt, np * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(bx.data(), B.pend_box, np * sizeof(ShadowBox), hipMemcpyDeviceToHost);
+        std::vector<int> sorted(cnt);
+        std::sort(sorted.begin(), sorted.end());
+        int over = 0;
+        for (int c : cnt) over += c > kPendCap;
+        fprintf(stderr, "[cg_rt_big] pending waves %d: candidates min %d median %d p90 %d max %d, over cap %d\n", np,
+                sorted[0], sorted[np / 2], sorted[(np * 9) / 10], sorted[np - 1], over);
+        for (int i = 0; i < np && i < 6; ++i)
+            fprintf(stderr, "  pending %d: cnt %d box lo (%g %g %g) hi (%g %g %g) pn %g\n", i, cnt[i], bx[i].lo[0],
+                    bx[i].lo[1], bx[i].lo[2], bx[i].hi[0], bx[i].hi[1], bx[i].hi[2], bx[i].pn);
+    }
     unsigned long long d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpy(d, (char *)scratch + big_scratch_bytes(B, F) - 64, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess)
-        fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays in %llu waves, "
-                "exhaustive survivors %llu, walks %llu (%.1f steps each); wave clocks: heuristics %.3g, exhaustive %.3g\n",
-                d[0], d[7], d[3], d[1] >> 32, d[1] & 0xffffffffull, d[6], d[6] ? (double)d[2] / d[6] : 0.0,
-                (double)d[4], (double)d[5]);
+        fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays; "
+                "pending waves %llu with %llu certified candidates in total\n", d[0], d[7], d[3], d[6], d[1]);
 }
 
 // Host build of the scene grid: cubic cells sized for ~2 triangle centroids
