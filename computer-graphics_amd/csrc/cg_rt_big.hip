@@ -35,9 +35,14 @@ constexpr int kBinW = 128, kBinH = 32;        // pixels; multiples of the 8x8 wa
 constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
 static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
 constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
-constexpr int kPendCap = 4096;                // certified candidates kept per pending ray
-constexpr int kMaxPend = 32768;               // pending rays with their own certified list
-constexpr int kPendGridY = 128;               // workgroup rows of the pending-certify kernel
+constexpr int kMaxPend = 65536;               // pending shadow rays searched exhaustively in K5
+
+// A shadow ray K4 could not resolve (skeleton.cpp:394 arguments, reference
+// float values) and where its verdict goes.
+struct PendRay {
+    float ox, oy, oz, nx, ny, nz, len, rmag;
+    int pix, bit;
+};
 
 struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
@@ -49,12 +54,8 @@ struct BigBufs {
     RtGrid grid;
     // shadow verdicts (9 * n_lights <= 64): per pixel, bit s * n_lights + l
     unsigned long long *sh_bits, *pend_bits;
-    int *pend_n;                  // pixels with unresolved rays (counter, after bin_n/sbin_n)
-    int *pend_pix;                // [kMaxPend] pending ray: local pixel index L * W + u
-    int *pend_bit;                // [kMaxPend] and its verdict bit s * n_lights + l
-    ShadowBox *pend_box;          // [kMaxPend] box of their unresolved rays
-    int *pend_cnt;                // [kMaxPend] certified candidates found per pending pixel
-    int *pend_list;               // [kMaxPend][kPendCap]
+    int *pend_n;                  // shadow rays left unresolved by K4 (counter, after bin_n/sbin_n)
+    struct PendRay *pend_ray;     // [kMaxPend]
     int cap, bins_x, bins_y, tiles_x, tiles_y;
     unsigned long long *diag;     // CG_RT_BIG_DIAG: [waves, survivors, walk steps, lit rays, primary cands, primary kept]
 };
@@ -185,39 +186,6 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
         int before = 0;
         for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
         if (kept[r]) list[off + before + __popcll(m[r] & lt)] = base + r * 256 + (int)threadIdx.x;
-        for (int q = 0; q < 4; ++q) off += s_w[r][q];
-    }
-}
-
-// bin_append with a capacity: the count keeps growing past `cap` (the reader
-// detects the overflow), entries past it are dropped.
-__device__ __forceinline__ void bin_append_capped(const bool kept[4], int base, int *list, int *count, int cap)
-{
-    __shared__ int s_w[4][4];
-    __shared__ int s_base;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    unsigned long long m[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        m[r] = __ballot(kept[r]);
-        if (lane == 0) s_w[r][w] = __popcll(m[r]);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int r = 0; r < 4; ++r)
-            for (int q = 0; q < 4; ++q) tot += s_w[r][q];
-        s_base = tot ? atomicAdd(count, tot) : 0;
-    }
-    __syncthreads();
-    int off = s_base;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        int before = 0;
-        for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
-        const int pos = off + before + __popcll(m[r] & lt);
-        if (kept[r] && pos < cap) list[pos] = base + r * 256 + (int)threadIdx.x;
         for (int q = 0; q < 4; ++q) off += s_w[r][q];
     }
 }
@@ -481,21 +449,17 @@ __device__ int grid_blocker(const RtGrid &G, const RtTri *__restrict__ tc, const
     return -1;
 }
 
-// Shadow verdicts for 9 * n_lights <= 64, in three parallel steps:
-//  K4 rt_shadow_hints   each shadow ray (sub-ray s, light l) tries likely
-//                       blockers: the triangle it starts on (the 1e-5 normal
-//                       offset puts the origin behind it when the normal faces
-//                       away from the light), the lane's previous blocker, then
-//                       the scene grid.  Any triangle the exact test accepts
-//                       blocks the ray (an any-hit verdict does not depend on
-//                       the order).  Unresolved rays are marked pending; a
-//                       wave with pending rays registers the box of just those
-//                       rays.
-//  K5 rt_pending_cert   every triangle against every registered box (shadow
-//                       certificate), survivors appended per pending wave;
-//  K6 rt_pending_walk   the pending rays walk their wave's survivors (or, past
-//                       kPendCap survivors, every triangle): the exhaustive
-//                       search that makes the verdict exact.
+// Shadow verdicts for 9 * n_lights <= 64 (one bit per (sub-ray s, light l)
+// and pixel), in two parallel steps:
+//  K4 rt_shadow_hints   each shadow ray tries likely blockers: the triangle it
+//                       starts on (the 1e-5 normal offset puts the origin
+//                       behind it when the normal faces away from the light),
+//                       the lane's previous blocker, then the scene grid.  Any
+//                       triangle the exact test accepts blocks the ray -- an
+//                       any-hit verdict does not depend on the order.  Rays
+//                       still unresolved are queued;
+//  K5 rt_pending_test   the exhaustive search for the queued rays: every
+//                       triangle, the reference's own test.
 __device__ __forceinline__ void hit_geometry(const RtFrame &F, const BigBufs &B, const RtShade *__restrict__ shade,
                                              const RtSphere *__restrict__ sph, vec4 dir, int s, size_t pix,
                                              size_t npix, int &bi, vec3 &pos, vec3 &normal)
@@ -549,24 +513,12 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
                     shadowed |= bit;
                     last = k;
                 } else {
-                    pending |= bit;
-                    LaneShadowBox pb;
-                    pb.init();
-                    const vec3 lp = v3(Lt.x, Lt.y, Lt.z);
-                    shadow_box_add(pb, lp, lp, pos, normal);
                     const int p = atomicAdd(B.pend_n, 1);
-                    if (p < kMaxPend) {
-                        ShadowBox box;
-                        for (int c = 0; c < 3; ++c) {
-                            box.lo[c] = pb.lo[c];
-                            box.hi[c] = pb.hi[c];
-                        }
-                        box.pn = pb.pn;
-                        B.pend_pix[p] = (int)pix;
-                        B.pend_bit[p] = s * F.n_lights + l;
-                        B.pend_box[p] = box;
-                        B.pend_cnt[p] = 0;
-                    }
+                    if (p < kMaxPend)
+                        B.pend_ray[p] = PendRay{q.origin.x, q.origin.y, q.origin.z, q.nd.x, q.nd.y, q.nd.z,
+                                                q.len, q.rmag, (int)pix, s * F.n_lights + l};
+                    else
+                        pending |= bit;       // past kMaxPend: rt_big_shade_kernel searches it
                 }
             }
         }
@@ -580,56 +532,30 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
     }
 }
 
-// K5: shadow certificate of the light set, every triangle against every
-// pending wave's box.
-__global__ __launch_bounds__(256) void rt_pending_cert_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+// K5: exhaustive any-hit of the unresolved shadow rays with the reference's
+// own test (cheaper than certifying): each workgroup keeps 1024 triangles in
+// registers and runs every pending ray against them; a hit sets the ray's
+// verdict bit.
+__global__ __launch_bounds__(256) void rt_pending_test_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
     const int np = min(*B.pend_n, kMaxPend);
-    const vec3 lc = v3(F.lc[0], F.lc[1], F.lc[2]);
-    const int base = blockIdx.x * kBinTris;
-    for (int p = blockIdx.y; p < np; p += gridDim.y) {
-        const ShadowBox box = B.pend_box[p];
-        bool kept[4];
+    if (np == 0) return;
+    RtTri T[4];
+    bool ok[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = base + r * 256 + (int)threadIdx.x;
-            kept[r] = i < F.n_tris && !cull_shadow(tc[i], lc, F.lrho, box);
-        }
-        bin_append_capped(kept, base, B.pend_list + (size_t)p * kPendCap, B.pend_cnt + p, kPendCap);
-        __syncthreads();
+    for (int r = 0; r < 4; ++r) {
+        const int i = blockIdx.x * kBinTris + r * 256 + (int)threadIdx.x;
+        ok[r] = i < F.n_tris;
+        T[r] = tc[ok[r] ? i : 0];
     }
-}
-
-// K6: the exhaustive search of the pending rays, one thread per ray over its
-// certified list (every triangle past kPendCap survivors).  Rays past
-// kMaxPend keep their pending bit for rt_big_shade_kernel.
-__global__ __launch_bounds__(256) void rt_pending_walk_kernel(RtFrame F, const RtTri *__restrict__ tc,
-                                                              const RtShade *__restrict__ shade,
-                                                              const RtSphere *__restrict__ sph, BigBufs B)
-{
-    const int np = min(*B.pend_n, kMaxPend);
-    const size_t npix = (size_t)F.rows_out * F.W;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
-        const size_t pix = (size_t)B.pend_pix[p];
-        const int bit = B.pend_bit[p], cnt = B.pend_cnt[p];
-        const bool all = cnt > kPendCap;
-        const int n = all ? F.n_tris : cnt;
-        const int *list = B.pend_list + (size_t)p * kPendCap;
-        const int L = (int)(pix / F.W), u = (int)(pix - (size_t)L * F.W);
-        const vec4 dir = pixel_dir(F, u, shard_row(F, L));
-        const int s = bit / F.n_lights, l = bit - s * F.n_lights;
-        int bi;
-        vec3 pos, normal;
-        hit_geometry(F, B, shade, sph, dir, s, pix, npix, bi, pos, normal);
-        const ShadowRay q = shadow_ray(F.lights[l], pos, normal);
-        if (B.diag) {
-            atomicAdd(&B.diag[1], (unsigned long long)n);
-            atomicAdd(&B.diag[6], 1ull);
-        }
+    for (int p = 0; p < np; ++p) {
+        const PendRay R = B.pend_ray[p];                       // uniform: scalar loads
+        const vec3 o = v3(R.ox, R.oy, R.oz), nd = v3(R.nx, R.ny, R.nz);
         bool hit = false;
-        for (int i = 0; i < n && !hit; ++i) hit = tri_shadows(tc[all ? i : list[i]], q.origin, q.nd, q.len, q.rmag);
-        if (hit) atomicOr(&B.sh_bits[pix], 1ull << bit);
-        atomicAnd(&B.pend_bits[pix], ~(1ull << bit));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hit |= ok[r] && tri_shadows(T[r], o, nd, R.len, R.rmag);
+        if (__ballot(hit) != 0ull && (threadIdx.x & 63) == __builtin_ctzll(__ballot(hit)))
+            atomicOr(&B.sh_bits[R.pix], 1ull << R.bit);
     }
 }
 
@@ -709,7 +635,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
     return 2 * bins * B.cap * 4 + 2 * bins * 4 + 16 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
-           2 * npix * 8 + (size_t)kMaxPend * (4 + 4 + 4 + sizeof(ShadowBox)) + (size_t)kMaxPend * kPendCap * 4 + 512;
+           2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 512;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
 {
@@ -728,12 +654,7 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.sh_bits = (unsigned long long *)p;   p += npix * 8;
     B.pend_bits = (unsigned long long *)p; p += npix * 8;
-    B.pend_box = (ShadowBox *)p;           p += (size_t)kMaxPend * sizeof(ShadowBox);
-    B.pend_pix = (int *)p;                 p += (size_t)kMaxPend * 4;
-    B.pend_bit = (int *)p;                 p += (size_t)kMaxPend * 4;
-    B.pend_cnt = (int *)p;                 p += (size_t)kMaxPend * 4;
-    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    B.pend_list = (int *)p;                p += (size_t)kMaxPend * kPendCap * 4;
+    B.pend_ray = (PendRay *)p;             p += (size_t)kMaxPend * sizeof(PendRay);
     B.bin_list = (int *)p; p += bins * B.cap * 4;
     B.sbin_list = (int *)p;
 }
@@ -763,8 +684,7 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
     } else if (F.n_lights > 0) {
         hipLaunchKernelGGL(rt_shadow_hints_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-        hipLaunchKernelGGL(rt_pending_cert_kernel, dim3(bgrid.x, kPendGridY), dim3(256), 0, st, F, d_tc, B);
-        hipLaunchKernelGGL(rt_pending_walk_kernel, dim3(kMaxPend / 256), dim3(256), 0, st, F, d_tc, d_shade, d_sph, B);
+        hipLaunchKernelGGL(rt_pending_test_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
     }
     hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     return hipGetLastError();
@@ -789,22 +709,8 @@ void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
     fprintf(stderr, "[cg_rt_big] bins %d: primary lists mean %lld max %d; shadow lists mean %lld max %d\n", bins,
             s0 / bins, m0, s1 / bins, m1);
     int np = 0;
-    if (hipMemcpy(&np, B.pend_n, 4, hipMemcpyDeviceToHost) == hipSuccess && np > 0) {
-        np = std::min(np, kMaxPend);
-        std::vector<int> cnt(np);
-        std::vector<ShadowBox> bx(np);
-        (void)hipMemcpy(cnt.data(), B.pend_cnt, np * 4, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(bx.data(), B.pend_box, np * sizeof(ShadowBox), hipMemcpyDeviceToHost);
-        std::vector<int> sorted(cnt);
-        std::sort(sorted.begin(), sorted.end());
-        int over = 0;
-        for (int c : cnt) over += c > kPendCap;
-        fprintf(stderr, "[cg_rt_big] pending waves %d: candidates min %d median %d p90 %d max %d, over cap %d\n", np,
-                sorted[0], sorted[np / 2], sorted[(np * 9) / 10], sorted[np - 1], over);
-        for (int i = 0; i < np && i < 6; ++i)
-            fprintf(stderr, "  pending %d: cnt %d box lo (%g %g %g) hi (%g %g %g) pn %g\n", i, cnt[i], bx[i].lo[0],
-                    bx[i].lo[1], bx[i].lo[2], bx[i].hi[0], bx[i].hi[1], bx[i].hi[2], bx[i].pn);
-    }
+    if (hipMemcpy(&np, B.pend_n, 4, hipMemcpyDeviceToHost) == hipSuccess)
+        fprintf(stderr, "[cg_rt_big] pending shadow rays %d (searched exhaustively: %d)\n", np, std::min(np, kMaxPend));
     unsigned long long d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpy(d, (char *)scratch + big_scratch_bytes(B, F) - 64, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess)
         fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays; "

@@ -28,6 +28,8 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench_rt 600 python bench.py --steps 200 --warmup 20
   step bench_rast 300 python bench.py --workload rast --steps 200 --warmup 20
+  step bench_c4 300 python bench.py --workload c4 --steps 30 --warmup 3
+  step bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 2
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
@@ -35,6 +37,10 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
       python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline
   step rocprof_rast 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rast" -o rast -- \
       python3 "$ROOT/bench.py" --workload rast --steps 50 --warmup 5 --no-cpu-baseline
+  step rocprof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o c4 -- \
+      python3 "$ROOT/bench.py" --workload c4 --steps 10 --warmup 2 --no-cpu-baseline
+  step rocprof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o c5 -- \
+      python3 "$ROOT/bench.py" --workload c5 --steps 10 --warmup 2 --no-cpu-baseline
   cd "$ROOT"
 fi
 echo done
