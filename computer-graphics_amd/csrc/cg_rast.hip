@@ -1,7 +1,8 @@
 // cg_rast.hip -- rasteriser fill + post-pass for gfx950 (MI355X).
 //
 // Reference: rasteriser/Source/skeleton.cpp, texture mode 0 / colour mode 0.
-// Four launches per frame, all order-exact (no atomics touch colour/depth):
+// Launches per frame (after rast_geometry_kernel, cg_geometry.hip, when the
+// geometry runs on the device), all order-exact (no atomics touch colour/depth):
 //   1. rast_setup_kernel   (one workgroup per clipped triangle)
 //        VertexShader (:510-522) x3, then ComputePolygonRows (:433-498):
 //        every edge sample of Interpolate (:524-551) is reduced into its row
@@ -9,14 +10,14 @@
 //        reproduces the reference's `<=` / `>=` "later sample wins ties"
 //        updates exactly; each visible row becomes a RastSpan holding what
 //        DrawPolygonRows' Interpolate needs.
-//   2. rast_rowlist_kernel (one wave per screen row)
-//        ordered list of the triangles whose spans cover the row (ballot +
-//        popcount compaction, triangle order preserved).
-//   3. rast_fill_kernel    (one wave per 64-pixel row segment)
-//        walks its row's list in triangle order -- the reference's ordered
+//   2. rast_rows_kernel    (one wave per screen row)
+//        64-byte RowRec per triangle covering the row, in triangle order
+//        (ballot + popcount compaction).
+//   3. rast_fill_kernel    (one wave per 256-pixel row segment)
+//        walks its row's records in triangle order -- the reference's ordered
 //        z-buffer (`>=` for colour, `>` for shadow marks, :574/:668) with
 //        depth/shadow/shade state held in registers; PixelShader +
-//        calculateIllumination (:559-586, :664-688).
+//        calculateIllumination (:559-586, :664-688), deferred to the winner.
 //   4. rast_post_kernel    (one thread per pixel)
 //        the in-place raster-order post-pass (:283-307): a pixel's up/left
 //        neighbours are seen darkened and down/right ones not, which is
