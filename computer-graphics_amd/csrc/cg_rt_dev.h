@@ -269,6 +269,28 @@ __device__ static bool cull_shadow(const RtTri &c, vec3 L, double rho, const Sha
     return false;
 }
 
+// Triangle tests with exact pre-rejections.  Both skip the IEEE divide only
+// when its outcome is certain:
+//  * t < 0: det and detT of opposite signs with |detT| >= 2^-60 |det|,
+//    |det| >= 2^-60 and len >= 2^-60, so t and distance = t*len are
+//    strictly negative (no underflow to -0): rejected at :311;
+//  * distance > bound: same signs and fl(|detT| len) >= fl(fl(|det| bound)
+//    (1 + 2^-18)) with the right side finite and >= 2^-100, which implies
+//    t*len >= bound (1 + 2^-20) and hence a rounded distance strictly above
+//    `bound` (:313 for the closest hit, :395 for a shadow ray).
+__device__ __forceinline__ bool surely_negative(float detT, float det, float len)
+{
+    const float adT = fabsf(detT), ad = fabsf(det);
+    return ((detT < 0.0f) != (det < 0.0f)) && detT != 0.0f && ad >= 0x1p-60f && len >= 0x1p-60f &&
+           adT >= ad * 0x1p-60f;
+}
+__device__ __forceinline__ bool surely_beyond(float detT, float det, float len, float bound)
+{
+    if (!((detT > 0.0f && det > 0.0f) || (detT < 0.0f && det < 0.0f))) return false;
+    const float rhs = (fabsf(det) * bound) * 1.000003814697265625f;   // 1 + 2^-18
+    return rhs <= FLT_MAX && rhs >= 0x1p-100f && fabsf(detT) * len >= rhs;
+}
+
 // ClosestIntersection for camera-origin rays (skeleton.cpp:263-363).
 // Returns best index: >= 0 triangle, -1 - k sphere k, INT_MIN no hit; t out.
 // Triangles are visited in index order; with CULL only those whose bit is set
