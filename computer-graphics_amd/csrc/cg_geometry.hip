@@ -25,35 +25,90 @@ GeomParams geom_params(const cg_rast_params &p)
 
 constexpr int kGeomThreads = 512;
 constexpr int kGeomWaves = kGeomThreads / 64;
+constexpr int kGeomLds = 512;      // list entries held in LDS per list (more spill to global)
+
+// A list of triangles between clip planes: only the vertices change while
+// clipping -- a split's extra triangle copies normal, colour, texture and index
+// from its parent (skeleton.cpp:838-841) -- so an entry is three vertices plus
+// the input triangle it descends from.  Entries [0, kGeomLds) live in LDS, the
+// rest in a global spill buffer (vertices + `index` = parent).
+struct GeomList {
+    float4 v0[kGeomLds], v1[kGeomLds], v2[kGeomLds];
+    int par[kGeomLds];
+};
+
+__device__ __forceinline__ void glist_put(GeomList &L, cg_rtri *spill, int i, const cg_rtri &t, int parent)
+{
+    if (i < kGeomLds) {
+        L.v0[i] = make_float4(t.v0.x, t.v0.y, t.v0.z, t.v0.w);
+        L.v1[i] = make_float4(t.v1.x, t.v1.y, t.v1.z, t.v1.w);
+        L.v2[i] = make_float4(t.v2.x, t.v2.y, t.v2.z, t.v2.w);
+        L.par[i] = parent;
+    } else {
+        cg_rtri &d = spill[i - kGeomLds];
+        d.v0 = t.v0;
+        d.v1 = t.v1;
+        d.v2 = t.v2;
+        d.index = parent;
+    }
+}
+
+__device__ __forceinline__ cg_rtri glist_get(const GeomList &L, const cg_rtri *spill, int i, int &parent)
+{
+    cg_rtri t{};
+    if (i < kGeomLds) {
+        const float4 a = L.v0[i], b = L.v1[i], c = L.v2[i];
+        t.v0 = cg_vec4{a.x, a.y, a.z, a.w};
+        t.v1 = cg_vec4{b.x, b.y, b.z, b.w};
+        t.v2 = cg_vec4{c.x, c.y, c.z, c.w};
+        parent = L.par[i];
+    } else {
+        const cg_rtri &d = spill[i - kGeomLds];
+        t.v0 = d.v0;
+        t.v1 = d.v1;
+        t.v2 = d.v2;
+        parent = d.index;
+    }
+    return t;
+}
 
 // One workgroup, breadth-first -- the reference's own order (clip() walks the
 // whole list plane by plane, a split inserting [modified, extra] in place):
 // per plane, thread i clips list entry i into 0..2 children, a wave ballot
-// scan plus a 16-entry LDS scan gives each child its slot, and the children
+// scan plus an 8-entry LDS scan gives each child its slot, and the children
 // land, in order, in the next list.  Plane 1 reads the input triangles built
-// on the fly (room, then each box triangle and its 6 shadow triangles); the
-// lists ping-pong between scr0/scr1 (cap entries each) and plane 6 writes out.
+// on the fly (room, then each box triangle and its 6 shadow triangles; kept in
+// `inb` for their attributes); the lists ping-pong between the two LDS lists
+// (spilling to scr0/scr1) and plane 6 writes whole triangles to `out`.
 // out_n[0] = final count, out_light = rotated camera-space light (:223).
 __global__ __launch_bounds__(kGeomThreads) void rast_geometry_kernel(
     GeomParams p, const cg_rtri *__restrict__ room, int n_room, const cg_rtri *__restrict__ boxes,
-    int n_boxes, cg_rtri *__restrict__ out, cg_rtri *scr0, cg_rtri *scr1, int cap, int *__restrict__ out_n,
-    cg_vec4 *__restrict__ out_light)
+    int n_boxes, cg_rtri *__restrict__ out, cg_rtri *scr0, cg_rtri *scr1, cg_rtri *inb, int cap,
+    int *__restrict__ out_n, cg_vec4 *__restrict__ out_light)
 {
+    __shared__ GeomList s_list[2];
     __shared__ int wsum[kGeomWaves];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
     if (threadIdx.x == 0) *out_light = C4(mat4_mul(p.R, geom_light_camera(p)));
     int len = n_room + 7 * n_boxes;
-    const cg_rtri *src = nullptr;
     for (int pl = 1; pl <= 6; ++pl) {
-        cg_rtri *dst = pl == 6 ? out : (pl & 1) ? scr0 : scr1;
+        const int si = pl & 1, di = si ^ 1;                 // plane 1 writes list 0
+        const cg_rtri *sspill = si ? scr1 : scr0;
+        cg_rtri *dspill = di ? scr1 : scr0;
         int carry = 0;
         for (int base = 0; base < len; base += kGeomThreads) {
             const int i = base + (int)threadIdx.x;
             cg_rtri ch[2];
-            int k = 0;
+            int k = 0, parent = i;
             if (i < len) {
-                const cg_rtri t = pl == 1 ? geom_input(p, room, n_room, boxes, i) : src[i];
+                cg_rtri t;
+                if (pl == 1) {
+                    t = geom_input(p, room, n_room, boxes, i);
+                    inb[i] = t;
+                } else {
+                    t = glist_get(s_list[si], sspill, i, parent);
+                }
                 k = clip_plane(t, pl, p, ch);
             }
             const unsigned long long b0 = __ballot(k & 1), b1 = __ballot(k >> 1);
@@ -67,24 +122,37 @@ __global__ __launch_bounds__(kGeomThreads) void rast_geometry_kernel(
                 tot += v;
             }
             off += pre;
-            if (k > 0 && off < cap) dst[off] = ch[0];
-            if (k > 1 && off + 1 < cap) dst[off + 1] = ch[1];
+            if (pl < 6) {
+                if (k > 0 && off < cap) glist_put(s_list[di], dspill, off, ch[0], parent);
+                if (k > 1 && off + 1 < cap) glist_put(s_list[di], dspill, off + 1, ch[1], parent);
+            } else if (k > 0) {
+                cg_rtri o = inb[parent];                      // normal, colour, texture, index
+                if (off < cap) {
+                    o.v0 = ch[0].v0; o.v1 = ch[0].v1; o.v2 = ch[0].v2;
+                    out[off] = o;
+                }
+                if (k > 1 && off + 1 < cap) {
+                    o.v0 = ch[1].v0; o.v1 = ch[1].v1; o.v2 = ch[1].v2;
+                    out[off + 1] = o;
+                }
+            }
             carry += tot;
             __syncthreads();                 // wsum reuse
         }
         len = min(carry, cap);
-        src = dst;
-        __syncthreads();                     // dst visible to the whole workgroup
+        __threadfence_block();
+        __syncthreads();                     // the new list (LDS and spill) visible to the workgroup
     }
     if (threadIdx.x == 0) *out_n = len;
 }
 
 hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
                                 const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_scr0,
-                                cg_rtri *d_scr1, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st)
+                                cg_rtri *d_scr1, cg_rtri *d_inb, int cap, int *d_n, cg_vec4 *d_light,
+                                hipStream_t st)
 {
     hipLaunchKernelGGL(rast_geometry_kernel, dim3(1), dim3(kGeomThreads), 0, st, geom_params(prm), d_room,
-                       n_room, d_boxes, n_boxes, d_out, d_scr0, d_scr1, cap, d_n, d_light);
+                       n_room, d_boxes, n_boxes, d_out, d_scr0, d_scr1, d_inb, cap, d_n, d_light);
     return hipGetLastError();
 }
 

@@ -26,6 +26,22 @@ CG_HD vec3 operator*(vec3 a, vec3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z
 CG_HD vec3 operator*(vec3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 CG_HD vec3 operator/(vec3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
 CG_HD vec3 operator-(vec3 a) { return v3(-a.x, -a.y, -a.z); }   // type_vec3.inl:557-563
+
+// x / b for the constant divisors b = 3, 5, 9 (r = fl(1/b)) without the IEEE
+// divide sequence: q0 = x r corrected by one FMA residual step.  Bit-identical
+// to fl(x / b) for every float x -- all 2^32 inputs checked per divisor by
+// scripts/divchk.c (a zero residual keeps q0, which also preserves -0 and
+// the non-finite cases).
+CG_HD float div_const(float x, float b, float r)
+{
+    const float q0 = x * r;
+    const float e = fmaf(-q0, b, x);
+    return (e == 0.0f || !isfinite(x)) ? q0 : fmaf(e, r, q0);
+}
+CG_HD vec3 div_const(vec3 a, float b, float r)
+{
+    return v3(div_const(a.x, b, r), div_const(a.y, b, r), div_const(a.z, b, r));
+}
 CG_HD vec4 operator+(vec4 a, vec4 b) { return v4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 CG_HD vec4 operator-(vec4 a, vec4 b) { return v4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
 CG_HD vec4 operator*(vec4 a, float s) { return v4(a.x * s, a.y * s, a.z * s, a.w * s); }

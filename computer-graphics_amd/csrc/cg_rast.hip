@@ -132,9 +132,9 @@ __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
     const cg_rtri *__restrict__ tris, RastArgs A, const int *__restrict__ n_dev, RastSpan *__restrict__ spans,
     RastHdr *__restrict__ hdr, int *__restrict__ first_tri)
 {
-    __shared__ unsigned long long lkey[kRastMaxRows];
-    __shared__ unsigned long long rkey[kRastMaxRows];
+    extern __shared__ unsigned long long s_keys[];          // [2 * H]: left | right keys per row
     __shared__ unsigned long long fkey;
+    unsigned long long *lkey = s_keys, *rkey = s_keys + A.H;
     const int n = n_dev ? min(*n_dev, A.n) : A.n;
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
         rast_setup_one(tris, A, spans, hdr, first_tri, t, lkey, rkey, fkey);
@@ -176,9 +176,11 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
     }
     if (threadIdx.x == 0) fkey = ~0ull;
     __syncthreads();
+    // the three edges' Interpolate set-up (:524-538), shared by both passes
+    const Edge E0 = make_edge(vp[0], vp[1]), E1 = make_edge(vp[1], vp[2]), E2 = make_edge(vp[2], vp[0]);
     // Edge samples -> rows (:466-497).  Rows outside the screen never shade.
     for (int ei = 0; ei < 3; ++ei) {
-        Edge e = make_edge(vp[ei], vp[ei == 2 ? 0 : ei + 1]);
+        const Edge &e = ei == 0 ? E0 : ei == 1 ? E1 : E2;
         // Only a sample that can still win its row issues an LDS atomic: the
         // left winner is the minimum x with the latest sequence among equals,
         // so a sample whose previous same-row neighbour has a smaller x, or
@@ -215,8 +217,8 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
             unsigned ls = ~(unsigned)(lk & 0xffffffffu), rs = (unsigned)(rk & 0xffffffffu);
             int le = (int)(ls >> 30), lj = (int)(ls & 0x3fffffffu);
             int re = (int)(rs >> 30), rj = (int)(rs & 0x3fffffffu);
-            Edge el = make_edge(vp[le], vp[le == 2 ? 0 : le + 1]);
-            Edge er = make_edge(vp[re], vp[re == 2 ? 0 : re + 1]);
+            const Edge el = le == 0 ? E0 : le == 1 ? E1 : E2;
+            const Edge er = re == 0 ? E0 : re == 1 ? E1 : E2;
             int lx = edge_x(el, lj), rx = edge_x(er, rj);
             float lz, lX, lY, rz, rX, rY;
             edge_attr(el, lj, lz, lX, lY);
@@ -348,7 +350,7 @@ __device__ __forceinline__ vec3 illum_D(const RastArgs &A, float zinv, float X, 
 // One wave per kFillPx-pixel row segment, kFillPx/64 pixels per lane, state in
 // registers; records walked in triangle order (the reference's ordered
 // z-buffer), one uniform overlap test per record.
-constexpr int kFillPx = 256;
+constexpr int kFillPx = 64;
 constexpr int kFillPerLane = kFillPx / 64;
 
 __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRec *__restrict__ recs,
@@ -445,33 +447,32 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
     }
 }
 
-// shade buffers of one pixel, as they stand after the fill.
-__device__ __forceinline__ void shade3(const cg_rtri *__restrict__ tris, const RastArgs &A, float4 st,
-                                       vec3 &sc, vec3 &lo, vec3 &hi)
+// shade buffers of one pixel as they stand after the fill (:580-585), from its
+// state and its triangle's colour
+__device__ __forceinline__ void shade3c(const RastArgs &A, float4 st, cg_vec3 col, vec3 &sc, vec3 &lo, vec3 &hi)
 {
-    int tb = __float_as_int(st.x);
+    const int tb = __float_as_int(st.x);
     if (tb < 0) {
         sc = lo = hi = v3(0.f, 0.f, 0.f);
         return;
     }
-    int t = tb & ~(1 << 30);
-    float ind = (tb & (1 << 30)) ? A.ind_first : 0.2f * 1;
-    cg_rtri T = tris[t];
-    vec3 c = v3(T.color.x, T.color.y, T.color.z);
-    vec3 D = v3(st.y, st.z, st.w);
+    const float ind = (tb & (1 << 30)) ? A.ind_first : 0.2f * 1;
+    const vec3 c = v3(col.x, col.y, col.z);
+    const vec3 D = v3(st.y, st.z, st.w);
     sc = c * (D + v3(ind, ind, ind));                      // :580
     lo = c * (D + v3(0.0f * 1, 0.0f * 1, 0.0f * 1));       // :582
     hi = c * (D + v3(0.4f * 1, 0.4f * 1, 0.4f * 1));       // :584
 }
 
-// soft-shadow darkening amount for interior pixel o, 0 if not shadowed (:286-303, :1725-1733)
-__device__ __forceinline__ float darken(const int32_t *__restrict__ sh, int W, size_t o)
+// soft-shadow darkening amount of a pixel whose 3x3 shadow neighbourhood is
+// sh[cy-1..cy+1][cx-1..cx+1] (row stride ld), 0 if not shadowed
+// (:286-303, :1725-1733; [y+1][x-1] counted twice, [y+1][x+1] omitted)
+__device__ __forceinline__ float darken_at(const int *sh, int ld, int cy, int cx)
 {
-    if (sh[o] != 1) return 0.0f;
-    int k = sh[o] + sh[o - W] + sh[o - W - 1] + sh[o - W + 1] + sh[o + W - 1] + sh[o + W] +
-            sh[o + W - 1] + sh[o - 1] + sh[o + 1];
-    float val = (float)k;
-    val /= 9.0f;
+    const int *c = sh + cy * ld + cx;
+    if (c[0] != 1) return 0.0f;
+    int k = c[0] + c[-ld] + c[-ld - 1] + c[-ld + 1] + c[ld - 1] + c[ld] + c[ld - 1] + c[-1] + c[1];
+    float val = div_const((float)k, 9.0f, 1.0f / 9.0f);                 // val /= 9.0f
     if ((double)val < 0.6) return 0.05f;
     if ((double)val < 0.7) return 0.08f;
     if ((double)val < 0.8) return 0.1f;
@@ -479,43 +480,113 @@ __device__ __forceinline__ float darken(const int32_t *__restrict__ sh, int W, s
     return 0.3f;
 }
 
+// Post-pass (:283-307) on a 64x8 tile: the shadow plane (halo 2) goes to LDS,
+// then every pixel of the tile and its 1-pixel halo gets its three shade
+// buffers and its darkening computed once, then each interior pixel runs
+// antiAliasing (:1736-1753) on its 5 taps from LDS.  Raster order: the pixel
+// itself and its up/left neighbours are seen darkened, down/right not (a
+// darkening of 0 subtracts exactly nothing).
+constexpr int kPostTW = 64, kPostTH = 8;
+constexpr int kPostHW = kPostTW + 2, kPostHH = kPostTH + 2;      // shade halo 1
+constexpr int kPostSW = kPostTW + 4, kPostSH = kPostTH + 4;      // shadow halo 2
+
 __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
                                                        const float4 *__restrict__ state,
                                                        const int32_t *__restrict__ sh,
                                                        uint32_t *__restrict__ argb)
 {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= A.W || y >= A.H) return;
-    const int W = A.W;
-    const size_t o = (size_t)y * W + x;
-    if (x < 1 || y < 1 || x >= W - 1 || y >= A.H - 1) {   // :283-284 border never written
-        argb[o] = 0u;
-        return;
-    }
-    vec3 s[5], l[5], h[5];
-    const size_t taps[5] = {o, o - W, o + W, o - 1, o + 1};   // centre, up, down, left, right
+    __shared__ int s_sh[kPostSH][kPostSW];
+    __shared__ float s_c[9][kPostHH][kPostHW];      // sc.xyz, lo.xyz, hi.xyz
+    __shared__ float s_d[kPostHH][kPostHW];
+    const int W = A.W, H = A.H;
+    const int gx0 = blockIdx.x * kPostTW, gy0 = blockIdx.y * kPostTH;
+    // all global loads first (shadow tile, shade state, then the colour
+    // gathers they index), so each thread has them in flight together
+    constexpr int kShR = (kPostSH * kPostSW + 255) / 256, kStR = (kPostHH * kPostHW + 255) / 256;
+    int shv[kShR];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) shade3(tris, A, state[taps[k]], s[k], l[k], h[k]);
-    // darkened before the AA of this pixel: itself, the pixel above and the one
-    // to the left (both interior-only, raster order)
-    float d0 = darken(sh, W, o);
-    float dU = (y - 1 >= 1) ? darken(sh, W, o - W) : 0.0f;
-    float dL = (x - 1 >= 1) ? darken(sh, W, o - 1) : 0.0f;
-    if (sh[o] == 1) s[0] = s[0] - v3(d0, d0, d0);
-    if (y - 1 >= 1 && sh[o - W] == 1) s[1] = s[1] - v3(dU, dU, dU);
-    if (x - 1 >= 1 && sh[o - 1] == 1) s[3] = s[3] - v3(dL, dL, dL);
-    // antiAliasing (:1741-1750)
-    vec3 val = ((((s[0] + s[1]) + s[2]) + s[3]) + s[4]) / 5.0f;
-    vec3 val1 = ((((l[0] + l[1]) + l[2]) + l[3]) + l[4]) / 5.0f;
-    vec3 val2 = ((((h[0] + h[1]) + h[2]) + h[3]) + h[4]) / 5.0f;
-    val = ((val + val1) + val2) / 3.0f;
-    argb[o] = put_pixel(val);
+    for (int r = 0; r < kShR; ++r) {
+        const int i = threadIdx.x + 256 * r;
+        const int cy = i / kPostSW, cx = i - cy * kPostSW;
+        const int gx = gx0 - 2 + cx, gy = gy0 - 2 + cy;
+        shv[r] = (i < kPostSH * kPostSW && gx >= 0 && gy >= 0 && gx < W && gy < H) ? sh[(size_t)gy * W + gx] : 0;
+    }
+    float4 stv[kStR];
+    bool inb[kStR];
+#pragma unroll
+    for (int r = 0; r < kStR; ++r) {
+        const int i = threadIdx.x + 256 * r;
+        const int cy = i / kPostHW, cx = i - cy * kPostHW;
+        const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
+        inb[r] = i < kPostHH * kPostHW && gx >= 0 && gy >= 0 && gx < W && gy < H;
+        stv[r] = inb[r] ? state[(size_t)gy * W + gx] : make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
+    }
+    cg_vec3 col[kStR];
+#pragma unroll
+    for (int r = 0; r < kStR; ++r) {
+        const int tb = __float_as_int(stv[r].x);
+        col[r] = tb >= 0 ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int r = 0; r < kShR; ++r) {
+        const int i = threadIdx.x + 256 * r;
+        if (i < kPostSH * kPostSW) (&s_sh[0][0])[i] = shv[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kStR; ++r) {
+        const int i = threadIdx.x + 256 * r;
+        if (i >= kPostHH * kPostHW) break;
+        const int cy = i / kPostHW, cx = i - cy * kPostHW;
+        const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
+        vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
+        float d = 0.0f;
+        if (inb[r]) {
+            shade3c(A, stv[r], col[r], sc, lo, hi);
+            if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
+        }
+        s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
+        s_c[3][cy][cx] = lo.x; s_c[4][cy][cx] = lo.y; s_c[5][cy][cx] = lo.z;
+        s_c[6][cy][cx] = hi.x; s_c[7][cy][cx] = hi.y; s_c[8][cy][cx] = hi.z;
+        s_d[cy][cx] = d;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kPostTH * kPostTW; i += 256) {
+        const int ty = i / kPostTW, tx = i - ty * kPostTW;
+        const int x = gx0 + tx, y = gy0 + ty;
+        if (x >= W || y >= H) continue;
+        const size_t o = (size_t)y * W + x;
+        if (x < 1 || y < 1 || x >= W - 1 || y >= H - 1) {   // :283-284 border never written
+            argb[o] = 0u;
+            continue;
+        }
+        const int cy = ty + 1, cx = tx + 1;
+        auto tap = [&](int b, int yy, int xx) { return v3(s_c[b][yy][xx], s_c[b + 1][yy][xx], s_c[b + 2][yy][xx]); };
+        auto dk = [&](int yy, int xx) { const float d = s_d[yy][xx]; return v3(d, d, d); };
+        const int ty5[5] = {cy, cy - 1, cy + 1, cy, cy}, tx5[5] = {cx, cx, cx, cx - 1, cx + 1};  // c, up, down, left, right
+        vec3 sv[5], lv[5], hv[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            sv[k] = tap(0, ty5[k], tx5[k]);
+            lv[k] = tap(3, ty5[k], tx5[k]);
+            hv[k] = tap(6, ty5[k], tx5[k]);
+        }
+        sv[0] = sv[0] - dk(cy, cx);                        // darkened: itself, up, left
+        sv[1] = sv[1] - dk(cy - 1, cx);
+        sv[3] = sv[3] - dk(cy, cx - 1);
+        // :1741-1750 (x / 5.0f and / 3.0f via div_const, bit-identical)
+        vec3 val = div_const((((sv[0] + sv[1]) + sv[2]) + sv[3]) + sv[4], 5.0f, 1.0f / 5.0f);
+        vec3 val1 = div_const((((lv[0] + lv[1]) + lv[2]) + lv[3]) + lv[4], 5.0f, 1.0f / 5.0f);
+        vec3 val2 = div_const((((hv[0] + hv[1]) + hv[2]) + hv[3]) + hv[4], 5.0f, 1.0f / 5.0f);
+        val = div_const((val + val1) + val2, 3.0f, 1.0f / 3.0f);
+        argb[o] = put_pixel(val);
+    }
 }
 
 hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
                                 const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_scr0,
-                                cg_rtri *d_scr1, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st);
+                                cg_rtri *d_scr1, cg_rtri *d_inb, int cap, int *d_n, cg_vec4 *d_light,
+                                hipStream_t st);
 
 // The fill + post pipeline.  Either the triangle count is known on the host
 // (n_dev == nullptr, n = count) or it lives on the device (n_dev, n = capacity,
@@ -542,14 +613,16 @@ int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri
     // planes 1-4 and 6 can each split a triangle in two; plane 5 never does
     const int cap = n_in > 0 ? 32 * n_in : 1;
     hipError_t e;
-    cg_rtri *tris = (cg_rtri *)ctx_buf(c, 0, 3 * (size_t)cap * sizeof(cg_rtri), &e);   // out + 2 scratch lists
+    // out + 2 spill lists + the input triangles
+    cg_rtri *tris = (cg_rtri *)ctx_buf(c, 0, (3 * (size_t)cap + n_in + 1) * sizeof(cg_rtri), &e);
     if (!tris) return ctx_fail(c, e, "alloc clipped triangles");
     int *geo = (int *)ctx_buf(c, 9, 64, &e);               // [0] count, [4..7] light
     if (!geo) return ctx_fail(c, e, "alloc geometry header");
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
     if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
-    if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, tris + 2 * (size_t)cap, cap, geo, (cg_vec4 *)(geo + 4), st)) !=
+    if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, tris + 2 * (size_t)cap,
+                                  tris + 3 * (size_t)cap, cap, geo, (cg_vec4 *)(geo + 4), st)) !=
         hipSuccess)
         return ctx_fail(c, e, "rast_geometry launch");
     if (n_out) *n_out = geo;
@@ -598,9 +671,9 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     if (A.want_first && (e = hipMemsetAsync(first_tri, 0x7f, sizeof(int), st)) != hipSuccess)
         return ctx_fail(c, e, "memset");
     if (n > 0) {
-        const int grid = n < 512 ? n : 512;                  // 2 workgroups/CU (64 KB LDS each)
-        hipLaunchKernelGGL(rast_setup_kernel, dim3(grid), dim3(kSetupThreads), 0, st, d_tris, A, n_dev, spans, hdr,
-                           first_tri);
+        const int grid = n < 1024 ? n : 1024;                // LDS 16 B per row: several workgroups per CU
+        hipLaunchKernelGGL(rast_setup_kernel, dim3(grid), dim3(kSetupThreads), 2 * (size_t)H * 8, st, d_tris, A, n_dev,
+                           spans, hdr, first_tri);
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
     }
     hipLaunchKernelGGL(rast_rows_kernel, dim3((H + 3) / 4), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,
@@ -610,9 +683,8 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     hipLaunchKernelGGL(rast_fill_kernel, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
                        state, d_depth, shadow);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
-    const int segs = (W + 63) / 64;
-    hipLaunchKernelGGL(rast_post_kernel, dim3(segs, (H + 3) / 4), dim3(256), 0, st, d_tris, A, state,
-                       shadow, d_argb);
+    hipLaunchKernelGGL(rast_post_kernel, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH), dim3(256), 0,
+                       st, d_tris, A, state, shadow, d_argb);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");
     if (stats && (e = hipEventRecord(e1, st)) != hipSuccess) return ctx_fail(c, e, "event");
     if (stats) {

@@ -590,7 +590,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
             }
             pc = pc + (oc * ind);                                                     // :156
         }
-        px = valid ? put_pixel(pc / 9.0f) : put_pixel(v3(0.0f, 0.0f, 0.0f));         // :160-166
+        px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));         // :160-166
     }
     out[(size_t)L * F.W + u] = px;
 }
