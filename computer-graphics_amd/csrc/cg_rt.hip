@@ -121,6 +121,9 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));             // :160-166
     }
+#ifdef CG_RT_DIAG_MASKS
+    px = ((uint32_t)__popcll(mask) << 8) | (uint32_t)__popcll(smask);   // diagnostics build only
+#endif
     out[(size_t)L * F.W + u] = px;
 }
 

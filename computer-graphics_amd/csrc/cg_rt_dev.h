@@ -12,12 +12,18 @@ namespace cg {
 
 // ---------------------------------------------------------------------------
 // Sphere::intersect + solveQuadratic (raytracer/Source/TestModelH.h:24-66).
+__device__ __forceinline__ bool sphere_intersect_pre(vec3 L, float c, vec3 dir, float &t);
 __device__ __forceinline__ bool sphere_intersect(const RtSphere &S, vec3 start, vec3 dir, float &t)
 {
     vec3 L = start - v3(S.cx, S.cy, S.cz);            // :48
+    return sphere_intersect_pre(L, dot(L, L) - S.r2, dir, t);   // :51
+}
+// the same test with start-dependent terms computed by the caller:
+// L = start - centre (:48), c = dot(L, L) - r^2 (:51)
+__device__ __forceinline__ bool sphere_intersect_pre(vec3 L, float c, vec3 dir, float &t)
+{
     float a = dot(dir, dir);                           // :49
     float b = 2 * dot(dir, L);                         // :50
-    float c = dot(L, L) - S.r2;                        // :51
     float x0, x1;
     float disc = (b * b) - ((4 * a) * c);              // :27
     if (disc < 0) return false;                        // :28
@@ -331,13 +337,15 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
             bi = k;
         }
     }
-    vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+    const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
 #ifdef CG_ABLATE_SPHERE
     if (0)
 #endif
     for (int k = 0; k < F.n_sph; ++k) {                       // :341-355
         float t;
-        if (sphere_intersect(sph[k], s3, d, t)) {
+        const RtSphere S = sph[k];
+        const vec3 L = s3 - v3(S.cx, S.cy, S.cz);             // camera-constant (:48, :51)
+        if (sphere_intersect_pre(L, dot(L, L) - S.r2, d, t)) {
             if (t < best) {
                 best = t;
                 bt = t;
@@ -444,11 +452,12 @@ __device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lmin, vec3
     // direction lies in [fl(lmin - pos), fl(lmax - pos)] componentwise.
     vec3 rlo = lmin - pos, rhi = lmax - pos;
     vec3 S = pos + normal * 0.00001f;                                    // :394
-    // p_k = S - L_k + d_k = (S - pos) + rounding(d_k): |p_k| <= |S - pos|_1 + 2^-24 |d|_1
-    double sp = fabs((double)S.x - pos.x) + fabs((double)S.y - pos.y) + fabs((double)S.z - pos.z);
-    double dr = fmax(fabs((double)rlo.x), fabs((double)rhi.x)) + fmax(fabs((double)rlo.y), fabs((double)rhi.y)) +
-                fmax(fabs((double)rlo.z), fabs((double)rhi.z));
-    float pb = (float)((sp + 5.9604644775390625e-8 * dr) * (1.0 + 1e-6) + 1e-30);
+    // p_k = S - L_k + d_k = (S - pos) + rounding(d_k): |p_k| <= |S - pos|_1 + 2^-24 |d|_1.
+    // Evaluated in float: at most 8 rounded ops of relative error 2^-24 each,
+    // covered by the (1 + 2^-18) factor, so pb stays an upper bound.
+    float sp = (fabsf(S.x - pos.x) + fabsf(S.y - pos.y)) + fabsf(S.z - pos.z);
+    float dr = (fmaxf(fabsf(rlo.x), fabsf(rhi.x)) + fmaxf(fabsf(rlo.y), fabsf(rhi.y))) + fmaxf(fabsf(rlo.z), fabsf(rhi.z));
+    float pb = ((sp + 5.9604644775390625e-8f * dr) * 1.000003814697265625f) + 1e-30f;
     b.lo[0] = fminf(b.lo[0], rlo.x); b.hi[0] = fmaxf(b.hi[0], rhi.x);
     b.lo[1] = fminf(b.lo[1], rlo.y); b.hi[1] = fmaxf(b.hi[1], rhi.y);
     b.lo[2] = fminf(b.lo[2], rlo.z); b.hi[2] = fmaxf(b.hi[2], rhi.z);

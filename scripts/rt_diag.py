@@ -1,7 +1,8 @@
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["CGAMD_LIB"] = os.path.join(ROOT, "computer-graphics_amd/_var/diag/libcgamd.so")
+os.environ["CGAMD_LIB"] = os.path.join(ROOT, "computer-graphics_amd/_build_diag/libcgamd.so")
 sys.path[:0] = [os.path.join(ROOT, "computer-graphics_amd")]
+import torch  # noqa: F401
 import numpy as np, cgamd
 ctx = cgamd.Context(0); t, n, s = cgamd.rt_scene(); ctx.rt_set_scene(t, n, s, 1)
 a, _ = ctx.rt_render(cgamd.rt_camera(1920, 1080, 1080.0))
