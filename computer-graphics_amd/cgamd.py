@@ -61,12 +61,13 @@ class RTri(C.Structure):       # rasteriser Triangle, 84 B
 class RastParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", Vec4),
                 ("R", C.c_float * 16), ("light_scene", Vec4), ("light_power", Vec3),
-                ("indirect_first", C.c_float)]
+                ("indirect_first", C.c_float), ("colour_mode", C.c_int), ("pad_", C.c_int),
+                ("rand_offset", C.c_uint64)]
 
 
 class Stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("total_ms", C.c_double), ("n_tris", C.c_int),
-                ("n_spans", C.c_int)]
+                ("n_spans", C.c_int), ("n_shaded", C.c_longlong)]
 
 
 assert C.sizeof(Tri) == 76 and C.sizeof(Sphere) == 44 and C.sizeof(Light) == 28
@@ -79,6 +80,7 @@ _SIGS = {
     "cg_last_error": (C.c_char_p, [P]),
     "cg_device_count": (C.c_int, []),
     "cg_rt_load_test_model": (C.c_int, [C.POINTER(Tri), C.c_int, C.POINTER(Sphere)]),
+    "cg_glibc_rand": (C.c_int, [C.c_uint64, C.c_int, P]),
     "cg_rt_area_lights": (C.c_int, [C.POINTER(Light), C.c_float, C.c_int, C.POINTER(Light), C.c_int]),
     "cg_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(Tri)]),
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
@@ -168,6 +170,16 @@ def area_lights(centre=None, side=0.1, n=8):
     return out
 
 
+def glibc_rand(offset, n):
+    """cg_glibc_rand: n values of glibc rand() from call `offset` (seed 1)."""
+    lib = load()
+    out = np.zeros(max(n, 1), np.int32)
+    rc = lib.cg_glibc_rand(offset, n, out.ctypes.data_as(C.c_void_p))
+    if rc:
+        raise RuntimeError(f"cg_glibc_rand failed: {rc}")
+    return out[:n]
+
+
 def random_scene(n, seed=0x5EED):
     """C5 random triangles (cg_rt_random_scene): ctypes Tri array of n."""
     lib = load()
@@ -179,7 +191,7 @@ def random_scene(n, seed=0x5EED):
 
 
 def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
-                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2):
+                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2, colour_mode=0, rand_offset=0):
     p = RastParams()
     p.width, p.height, p.focal = width, height, focal
     p.camera = Vec4(*cam)
@@ -188,6 +200,8 @@ def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
     f = float(np.float32(20.0) * np.float32(1.0))
     p.light_power = Vec3(f, f, f)
     p.indirect_first = indirect_first
+    p.colour_mode = colour_mode
+    p.rand_offset = rand_offset
     return p
 
 

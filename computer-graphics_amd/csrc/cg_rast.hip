@@ -26,7 +26,7 @@
 #include <float.h>
 #include <limits.h>
 
-#include "cg_internal.h"
+#include "cg_rast_dev.h"
 
 namespace cg {
 
@@ -36,21 +36,6 @@ void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b);
 
 constexpr int kSetupThreads = 256;
 constexpr int kRastMaxRows = 4096;   // LDS rows per triangle in span setup (H <= 4096)
-
-struct RastArgs {
-    int W, H, n;
-    float focal;
-    float light[3];
-    float lp[3];            // lightPower
-    float ind_first;        // indirectLightPowerPerArea at frame start
-    int want_first;         // ind_first differs from the steady-state 0.2
-    const cg_vec4 *d_light; // if set, the light comes from the device geometry
-};
-
-struct RastHdr {
-    int ylo, yhi;           // visible rows [ylo, yhi] (ylo > yhi: none)
-    int fy, fx;             // first shadeable fragment (if want_first), fy = INT_MAX none
-};
 
 struct Pix {                // rasteriser Pixel (:88-94) minus w
     int x, y;
@@ -269,18 +254,6 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
     if (threadIdx.x == 0) hdr[t] = h;
 }
 
-// Ordered per-row records (one wave per screen row): for every triangle in
-// order whose span on this row has a fragment on screen, a 64-byte record
-// with everything the fill needs -- one scalar load per record, no
-// dependent loads in the fill loop.
-struct alignas(16) RowRec {
-    int lx, rx;
-    float lz, sz, lX, sX, lY, sY;
-    int t, first_x;          // triangle index; x of the frame's first shaded fragment on this row, else -1
-    int shadow;              // colour.x < 0 (shadow-volume triangle)
-    float nx, ny, nz, pad0, pad1;
-};
-static_assert(sizeof(RowRec) == 64, "RowRec");
 
 __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
                                                        const int *__restrict__ n_dev,
@@ -325,24 +298,6 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
         c += __popcll(m);
     }
     if (lane == 0) count[y] = c;
-}
-
-// calculateIllumination's direct term D (:674-683); the post-pass rebuilds
-// screen/low/high = colour * (D + indirect) from it with the same ops.
-__device__ __forceinline__ vec3 illum_D(const RastArgs &A, float zinv, float X, float Y, vec3 N)
-{
-    // Interpolate pos3d (:546-548)
-    float pz = 1 / zinv;
-    float px = X / zinv;
-    float py = Y / zinv;
-    vec3 r = v3(A.light[0] - px, A.light[1] - py, A.light[2] - pz);               // :675
-    double a = (double)r.x * (double)r.x, b = (double)r.y * (double)r.y,
-           c = (double)r.z * (double)r.z;
-    float r2 = (float)((a + b) + c);                                              // :677
-    float vp = dot(r, N);                                                         // :681
-    float m = gmax(vp, 0.0f);
-    float area = (float)((double)4.0f * M_PI * (double)r2);                       // :682
-    return v3((A.lp[0] * m) / area, (A.lp[1] * m) / area, (A.lp[2] * m) / area);
 }
 
 // Per-pixel shade state between fill and post: .x = triangle index (as bits;
@@ -456,6 +411,11 @@ __device__ __forceinline__ void shade3c(const RastArgs &A, float4 st, cg_vec3 co
         sc = lo = hi = v3(0.f, 0.f, 0.f);
         return;
     }
+    if (tb & kStateDirect) {                               // colour modes 1-2 (:652, :660)
+        sc = v3(st.y, st.z, st.w);
+        lo = hi = v3(0.f, 0.f, 0.f);                       // cleared buffers (:250-257)
+        return;
+    }
     const float ind = (tb & (1 << 30)) ? A.ind_first : 0.2f * 1;
     const vec3 c = v3(col.x, col.y, col.z);
     const vec3 D = v3(st.y, st.z, st.w);
@@ -525,7 +485,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
 #pragma unroll
     for (int r = 0; r < kStR; ++r) {
         const int tb = __float_as_int(stv[r].x);
-        col[r] = tb >= 0 ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f};
+        col[r] = (tb >= 0 && !(tb & kStateDirect)) ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
@@ -582,6 +542,10 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         argb[o] = put_pixel(val);
     }
 }
+
+int rast_colour_fill(cg_ctx *c, const RastArgs &A, const cg_rast_params *p, const RowRec *recs, const int *count,
+                     const RastHdr *hdr, const int *n_dev, int max_recs, float4 *state, float *d_depth,
+                     int32_t *shadow, hipStream_t st, long long *n_shaded);
 
 hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
                                 const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_scr0,
@@ -663,7 +627,7 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     A.light[0] = light.x; A.light[1] = light.y; A.light[2] = light.z;
     A.lp[0] = p->light_power.x; A.lp[1] = p->light_power.y; A.lp[2] = p->light_power.z;
     A.ind_first = p->indirect_first;
-    A.want_first = p->indirect_first != 0.2f * 1;
+    A.want_first = p->colour_mode == 0 && p->indirect_first != 0.2f * 1;   // the :585 rewrite is mode 0 only
     A.d_light = d_light;
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
@@ -679,10 +643,18 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     hipLaunchKernelGGL(rast_rows_kernel, dim3((H + 3) / 4), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,
                        first_tri, recs, count);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rows launch");
-    const int fsegs = (W + kFillPx - 1) / kFillPx;
-    hipLaunchKernelGGL(rast_fill_kernel, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
-                       state, d_depth, shadow);
-    if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
+    if (p->colour_mode != 0) {
+        long long ns = 0;
+        const int rc = rast_colour_fill(c, A, p, recs, count, hdr, n_dev, nn, state, d_depth, shadow, st, &ns);
+        if (rc) return rc;
+        if (stats) stats->n_shaded = ns;
+    } else {
+        const int fsegs = (W + kFillPx - 1) / kFillPx;
+        hipLaunchKernelGGL(rast_fill_kernel, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
+                           state, d_depth, shadow);
+        if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
+        if (stats) stats->n_shaded = -1;
+    }
     hipLaunchKernelGGL(rast_post_kernel, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH), dim3(256), 0,
                        st, d_tris, A, state, shadow, d_argb);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");

@@ -74,6 +74,7 @@ struct cg_ctx {
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
+    DevBuf rpc, rtl, rrnd, rjt;          // colour modes 1-2 (cg_rast_colour.hip)
     int n_room = -1, n_boxes = 0;
 };
 
@@ -93,6 +94,10 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
     case 7: b = &c->rcount; break;
     case 8: b = &c->rrecs; break;
     case 9: b = &c->rgeo; break;
+    case 10: b = &c->rpc; break;
+    case 11: b = &c->rtl; break;
+    case 12: b = &c->rrnd; break;
+    case 13: b = &c->rjt; break;
     default: *e = hipErrorInvalidValue; return nullptr;
     }
     *e = b->ensure(bytes);
@@ -114,6 +119,7 @@ void rast_release(cg_ctx *c)
     c->rtris.release(); c->rhdr.release(); c->rspan.release(); c->rpix.release();
     c->rargb.release(); c->rdepth.release(); c->rshadow.release(); c->rcount.release();
     c->rrecs.release(); c->rgeo.release(); c->rroom.release(); c->rboxes.release();
+    c->rpc.release(); c->rtl.release(); c->rrnd.release(); c->rjt.release();
 }
 }  // namespace cg
 

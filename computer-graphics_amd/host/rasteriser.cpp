@@ -9,7 +9,7 @@
 // + cg_rast_render keep the host-geometry split available.)  Scripted keys as
 // in Update() (:311-417): w s a d q e =
 // light, 1 2 = indirect, U D L R z x = camera, n m = yaw, f g = focal,
-// ESC = 'X'.
+// ' ' (SPACE) = colour mode, ESC = 'X'.
 //
 //   rasteriser [--width W] [--height H] [--focal F] [--keys KEYS] [--out FILE]
 #include <cmath>
@@ -34,6 +34,8 @@ mat4 R(1.0f);                                                 // :35
 vec4 sceneCoordinatesLightPos(0, -0.5, 0, 1);                 // :52
 vec3 lightPower = 20.0f * vec3(1, 1, 1);                      // :53
 vec3 indirectLightPowerPerArea = 0.15f * vec3(1, 1, 1);       // :54
+int randColourSelect = 0;                                     // :81
+uint64_t randCalls = 0;                                       // glibc rand() calls so far (never seeded)
 vector<rast::Triangle> originalroom;                          // :84
 vector<rast::Triangle> originalbox;                           // :85
 
@@ -60,12 +62,19 @@ void Draw(screen *screen)
                             sceneCoordinatesLightPos.z, sceneCoordinatesLightPos.w};
     p.light_power = cg_vec3{lightPower.x, lightPower.y, lightPower.z};
     p.indirect_first = indirectLightPowerPerArea.x;
+    p.colour_mode = randColourSelect;
+    p.pad_ = 0;
+    p.rand_offset = randCalls;
     // geometry (shadow volumes + clip), fill and post-pass all on the GPU
     cg_stats st;
     int rc = cg_rast_draw(g_ctx, &p, screen->buffer, nullptr, nullptr, &st);
     if (rc) die(rc, "cg_rast_draw");
-    // PixelShader leaves the global at 0.2 after the first shaded fragment (:585)
-    if (st.n_tris > 0) indirectLightPowerPerArea = 0.2f * vec3(1, 1, 1);
+    if (randColourSelect == 0) {
+        // PixelShader leaves the global at 0.2 after the first shaded fragment (:585)
+        if (st.n_tris > 0) indirectLightPowerPerArea = 0.2f * vec3(1, 1, 1);
+    } else {
+        randCalls += 3 * (uint64_t)st.n_shaded;              // :649-651 / :657-659 per fragment
+    }
 }
 
 // skeleton.cpp:311-417 with scripted keys
@@ -96,6 +105,7 @@ bool Update()
         R[1][0] = 0;        R[1][1] = 1; R[1][2] = 0;
         R[2][0] = sin(yaw); R[2][1] = 0; R[2][2] = cos(yaw);
         break;
+    case ' ': randColourSelect = (randColourSelect + 1) % 3; break;   // SPACE (:406-409)
     case 'f': focalLength += 5; break;
     case 'g': focalLength -= 5; break;
     case 'X': return false;

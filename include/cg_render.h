@@ -74,7 +74,14 @@ typedef struct {
     cg_vec4 light_scene;      /* sceneCoordinatesLightPos (:52) */
     cg_vec3 light_power;      /* lightPower (:53) */
     float indirect_first;     /* indirectLightPowerPerArea at frame start (:54, :581-585):
-                                 0.15 on the very first frame, 0.2 afterwards */
+                                 0.15 on the very first frame, 0.2 after the first
+                                 colour-mode-0 fragment was shaded */
+    int colour_mode;          /* randColourSelect (:81, SPACE key :408): 0 lit triangle colour,
+                                 1 random colour, 2 night vision (:647-662) */
+    int pad_;
+    uint64_t rand_offset;     /* modes 1-2: glibc rand() calls made before this frame (the
+                                 reference never seeds: srand(1)); each shaded fragment
+                                 consumes 3 (cg_stats.n_shaded) */
 } cg_rast_params;
 
 typedef struct {
@@ -82,6 +89,7 @@ typedef struct {
     double total_ms;         /* host wall time of the call */
     int n_tris;              /* triangles rendered (RAST: after clipping) */
     int n_spans;             /* RAST: row spans produced by span setup */
+    long long n_shaded;      /* RAST colour modes 1-2: fragments shaded (rand() calls / 3); -1 otherwise */
 } cg_stats;
 
 /* ---- context ---------------------------------------------------------- */
@@ -136,6 +144,11 @@ int cg_rt_probe_direct_light(cg_ctx *ctx, const cg_isect *isects, const cg_light
                              cg_vec3 *out);
 
 /* ---- rasteriser ------------------------------------------------------- */
+/* glibc rand() as colour modes 1-2 consume it (seed 1, never reseeded by the
+ * reference): n values starting at call index `offset`.  Host-only probe of
+ * the generator the device path uses (jump-ahead restatement of glibc's
+ * TYPE_3 random_r). */
+int cg_glibc_rand(uint64_t offset, int n, int32_t *out);
 /* LoadTestModel (rasteriser/Source/TestModelH.h:48-312) with texture
  * selectors 0: room (10) and boxes (20). Returns n_room + n_boxes. */
 int cg_rast_load_test_model(cg_rtri *room, int room_cap, int *n_room, cg_rtri *boxes,

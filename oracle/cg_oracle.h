@@ -102,12 +102,19 @@ typedef struct {
     cgo_v4 light_scene;       /* sceneCoordinatesLightPos, skeleton.cpp:52 */
     cgo_v3 light_power;       /* skeleton.cpp:53 */
     float indirect_first;     /* value of indirectLightPowerPerArea at frame start (0.15 first frame, 0.2 after) */
+    int colour_mode;          /* randColourSelect (skeleton.cpp:81, :408): 0 lit colour, 1 random, 2 night vision */
+    int pad_;
+    uint64_t rand_offset;     /* glibc rand() calls made before this frame (srand never called: seed 1) */
 } cgo_rast_params;
 
 typedef struct {
     uint64_t n_tris, n_spans, n_frags, n_shaded, n_shadow;
 } cgo_rast_counters;
 
+/* n values of the process's libc rand() stream starting at call `offset`
+ * (srand(1) first): the reference's own RNG, used to pin the product's
+ * restatement of glibc's TYPE_3 generator. */
+void cgo_glibc_rand(uint64_t offset, int n, int32_t *out);
 int  cgo_rast_load_scene(cgo_rast_tri *room, int *n_room, cgo_rast_tri *boxes, int *n_boxes);
 void cgo_rast_default_params(cgo_rast_params *p, int width, int height);
 /* Host geometry of Draw (skeleton.cpp:205-241): returns number of clipped

@@ -474,7 +474,21 @@ static cgo_v3 illum(const rast_state *s, const cgo_pixel *px, cgo_v4 N, float in
     return v3_add(D, v3(ind, ind, ind));
 }
 
-/* skeleton.cpp:559-586, 664-671 (texture 0, colour mode 0) */
+void cgo_glibc_rand(uint64_t offset, int n, int32_t *out)
+{
+    srand(1);
+    for (uint64_t k = 0; k < offset; ++k) (void)rand();
+    for (int i = 0; i < n; ++i) out[i] = rand();
+}
+
+/* skeleton.cpp:563-565, 649-651: LO + rand() / (RAND_MAX/HI - LO), all float */
+static inline float rand_unit(void)
+{
+    const float LO = 0.2f, HI = 0.5f;
+    return LO + (float)rand() / ((float)(RAND_MAX / HI - LO));
+}
+
+/* skeleton.cpp:559-586, 647-671 (texture 0; colour modes 0, 1, 2) */
 static void pixel_shader(rast_state *s, const cgo_pixel *px, const cgo_rast_tri *t)
 {
     const int W = s->p->width, H = s->p->height;
@@ -482,7 +496,15 @@ static void pixel_shader(rast_state *s, const cgo_pixel *px, const cgo_rast_tri 
     if (!(x >= 0 && x < W && y >= 0 && y < H)) return;
     size_t o = (size_t)y * W + x;
     if (s->cnt) s->cnt->n_frags++;
-    if (px->zinv >= s->depth[o] && t->color.x >= 0) {
+    if (px->zinv >= s->depth[o] && t->color.x >= 0 && s->p->colour_mode != 0) {
+        float r0 = rand_unit(), r1 = rand_unit(), r2 = rand_unit();   /* :649-651, :657-659 */
+        cgo_v3 c = s->p->colour_mode == 1 ? v3(r0, r1, r2) : v3(r0 - 0.2f, 1.0f, r2 - 0.2f);
+        (void)r1;
+        cgo_v3 sc = v3_mul(c, illum(s, px, t->normal, s->indirect));  /* :652, :660 */
+        s->screen[3 * o + 0] = sc.x; s->screen[3 * o + 1] = sc.y; s->screen[3 * o + 2] = sc.z;
+        s->depth[o] = px->zinv;                                       /* :665 */
+        if (s->cnt) s->cnt->n_shaded++;
+    } else if (px->zinv >= s->depth[o] && t->color.x >= 0) {
         cgo_v3 c = t->color;
         cgo_v3 sc = v3_mul(c, illum(s, px, t->normal, s->indirect));
         cgo_v3 lo = v3_mul(c, illum(s, px, t->normal, 0.0f * 1));
@@ -528,6 +550,10 @@ void cgo_rast_draw(const cgo_rast_params *p, uint32_t *argb, float *depth, int32
     memset(s.high, 0, sizeof(float) * 3 * npx);
     memset(s.shadow, 0, sizeof(int32_t) * npx);
     s.indirect = p->indirect_first;
+    if (p->colour_mode != 0) {                                /* the frame's place in the rand() stream */
+        srand(1);
+        for (uint64_t k = 0; k < p->rand_offset; ++k) (void)rand();
+    }
     if (cnt) cnt->n_tris += (uint64_t)n;
     cgo_pixel *left = (cgo_pixel *)malloc(sizeof(cgo_pixel) * (size_t)(H + 2) * 64);
     cgo_pixel *right = (cgo_pixel *)malloc(sizeof(cgo_pixel) * (size_t)(H + 2) * 64);

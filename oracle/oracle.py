@@ -64,7 +64,8 @@ class Pixel(C.Structure):
 class RastParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", V4),
                 ("R", C.c_float * 16), ("light_scene", V4), ("light_power", V3),
-                ("indirect_first", C.c_float)]
+                ("indirect_first", C.c_float), ("colour_mode", C.c_int), ("pad_", C.c_int),
+                ("rand_offset", C.c_uint64)]
 
 
 class RastCounters(C.Structure):
@@ -119,6 +120,7 @@ def load():
         "cgo_rast_interpolate": (None, [Pixel, Pixel, C.POINTER(Pixel), C.c_int]),
         "cgo_rast_draw": (None, [C.POINTER(RastParams), P, P, P, P, P, P,
                                  C.POINTER(RastCounters)]),
+        "cgo_glibc_rand": (None, [C.c_uint64, C.c_int, P]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -206,8 +208,16 @@ def rt_draw_pixels(p, xy, scene=None, threads=1):
     return out
 
 
+def glibc_rand(offset, n):
+    """n values of libc rand() after `offset` calls from srand(1) (the reference's RNG)."""
+    lib = load()
+    out = np.zeros(n, np.int32)
+    lib.cgo_glibc_rand(offset, n, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
 def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
-                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2):
+                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2, colour_mode=0, rand_offset=0):
     lib = load()
     p = RastParams()
     lib.cgo_rast_default_params(C.byref(p), width, height)
@@ -217,6 +227,8 @@ def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
         p.R = (C.c_float * 16)(*list(R))
     p.light_scene = V4(*light)
     p.indirect_first = indirect_first
+    p.colour_mode = colour_mode
+    p.rand_offset = rand_offset
     return p
 
 

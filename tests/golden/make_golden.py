@@ -100,6 +100,16 @@ def rast_configs():
                                  light=[f32(0.1), -0.5, f32(-0.2), 1], indirect_first=f32(0.2)),
         "rast_320x240_close": dict(width=320, height=240, focal=180.0, cam=[0, 0, f32(-1.2), 1], R=None,
                                    light=[0, -0.5, 0, 1], indirect_first=f32(0.2)),
+        # colour modes 1-2 (randColourSelect, skeleton.cpp:647-662): libc rand() from the oracle
+        "rast_640x480_colour1": dict(width=640, height=480, focal=360.0, cam=[0, 0, f32(-3.001), 1], R=None,
+                                     light=[0, -0.5, 0, 1], indirect_first=f32(0.2), colour_mode=1,
+                                     rand_offset=0),
+        "rast_900x720_colour2_offset": dict(width=900, height=720, focal=512.0, cam=[0, 0, f32(-3.001), 1],
+                                            R=None, light=[0, -0.5, 0, 1], indirect_first=f32(0.2),
+                                            colour_mode=2, rand_offset=3_000_001),
+        "rast_320x240_colour1_first": dict(width=320, height=240, focal=180.0, cam=[0, 0, f32(-3.001), 1],
+                                           R=None, light=[0, -0.5, 0, 1], indirect_first=f32(0.15),
+                                           colour_mode=1, rand_offset=0),
     }
 
 
@@ -127,7 +137,8 @@ def rt_oracle_scene(cfg):
 
 def rast_params_of(cfg):
     return oracle.rast_params(cfg["width"], cfg["height"], cfg["focal"], tuple(cfg["cam"]), cfg["R"],
-                              tuple(cfg["light"]), cfg["indirect_first"])
+                              tuple(cfg["light"]), cfg["indirect_first"], cfg.get("colour_mode", 0),
+                              cfg.get("rand_offset", 0))
 
 
 def screenshot_argb(path=os.path.join(HERE, "rt_screenshot_320x256.bmp")) -> np.ndarray:
@@ -182,6 +193,8 @@ def main():
             for plane in ("argb", "depth", "shadow"):
                 assert e[plane + "_sha256"].startswith(ref[plane]), (name, plane)
             e["pinned_by"] = "SURVEY.md 8c reference fingerprint"
+        elif cfg.get("colour_mode", 0):
+            e["pinned_by"] = "restatement + the C library's own rand() (no reference fingerprint for colour modes)"
         else:
             e["pinned_by"] = "restatement only (parity unpinned beyond the oracle)"
         out["rast"][name] = e

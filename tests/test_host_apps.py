@@ -54,3 +54,19 @@ def test_rasteriser_app_keys(tmp_path):
     ref = oracle.rast_draw(oracle.rast_params(320, 240, 180.0, (0.0, 0.0, cam_z, 1.0),
                                               light=(light_x, -0.5, 0.0, 1.0), indirect_first=f32(0.2)))[0]
     assert np.array_equal(mg.screenshot_argb(out), ref)
+
+
+def test_rasteriser_app_colour_modes(tmp_path):
+    """SPACE, UP, SPACE: frames in colour mode 1, 1 (camera moved) and 2.  The
+    rand() stream runs on across frames (3 calls per shaded fragment) and the
+    first-frame indirect 0.15 is never rewritten outside mode 0."""
+    out = _run("rasteriser", ["--width", "320", "--height", "240", "--focal", "180", "--keys", " U "], tmp_path)
+    f32 = lambda x: float(np.float32(x))
+    ind, off = f32(0.15), 0
+    cams = [-3.001, f32(np.float32(-3.001) + np.float32(0.1)), f32(np.float32(-3.001) + np.float32(0.1))]
+    for mode, z in zip((1, 1, 2), cams):
+        p = oracle.rast_params(320, 240, 180.0, (0.0, 0.0, f32(z), 1.0), indirect_first=ind, colour_mode=mode,
+                               rand_offset=off)
+        ref, _, _, cnt = oracle.rast_draw(p, counters=True)
+        off += 3 * cnt.n_shaded
+    assert np.array_equal(mg.screenshot_argb(out), ref)

@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 def _params(cfg):
     R = (C.c_float * 16)(*cfg["R"]) if cfg["R"] else None
     return cgamd.rast_params(cfg["width"], cfg["height"], cfg["focal"], tuple(cfg["cam"]), R,
-                             tuple(cfg["light"]), cfg["indirect_first"])
+                             tuple(cfg["light"]), cfg["indirect_first"], cfg.get("colour_mode", 0),
+                             cfg.get("rand_offset", 0))
 
 
 def _render(ctx, cfg):
@@ -63,6 +64,8 @@ def test_rast_device_geometry_draw_matches_golden(ctx, golden, name):
     argb, depth, shadow, st = ctx.rast_draw(_params(cfg))
     e = golden["rast"][name]
     assert st.n_tris == e["counters"]["n_tris"]
+    if cfg.get("colour_mode", 0):   # rand() calls consumed: 3 per shaded fragment
+        assert st.n_shaded == e["counters"]["n_shaded"]
     assert mg.sha(shadow) == e["shadow_sha256"], "shadow plane"
     assert mg.sha(depth) == e["depth_sha256"], "depth plane"
     assert mg.sha(argb) == e["argb_sha256"], "colour plane"

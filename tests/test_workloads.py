@@ -43,3 +43,10 @@ def test_random_scene_rejects_bad_args():
     assert lib.cg_rt_area_lights(None, 0.1, 8, None, 0) < 0
     out = (cgamd.Light * 4)()
     assert lib.cg_rt_area_lights(C.byref(cgamd.default_lights()[0]), 0.1, 8, out, 4) < 0
+
+
+def test_glibc_rand_restatement_matches_libc():
+    """cg_glibc_rand (jump-ahead restatement used by colour modes 1-2) against
+    the C library's own rand(), the reference's RNG, at several offsets."""
+    for off in (0, 1, 30, 31, 344, 10_007, 1_234_567):
+        assert np.array_equal(cgamd.glibc_rand(off, 200), oracle.glibc_rand(off, 200)), off
