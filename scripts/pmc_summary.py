@@ -20,14 +20,20 @@ def per_kernel(wl, ctr):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 20",
-       "units": "bytes per launch", "round": sys.argv[1] if len(sys.argv) > 1 else "r01"}
+path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+try:
+    out = json.load(open(path))          # keep other sections (e.g. the SQ figures)
+except (OSError, ValueError):
+    out = {}
+out.update({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 20",
+            "units": "bytes per launch", "round": sys.argv[1] if len(sys.argv) > 1 else "r01"})
 for wl, kernels in DOMINANT.items():
     f, w = per_kernel(wl, "FETCH_SIZE"), per_kernel(wl, "WRITE_SIZE")
     det = {k: {"fetch_kib_raw": f.get(k), "write_kib": w.get(k),
                "hbm_bytes_corrected": (2 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024} for k in kernels}
-    out[wl] = {"kernels": det, "hbm_bytes_per_launch": sum(d["hbm_bytes_corrected"] for d in det.values())}
+    out.setdefault(wl, {}).update({"kernels": det,
+                                   "hbm_bytes_per_launch": sum(d["hbm_bytes_corrected"] for d in det.values())})
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as fh:
+with open(path, "w") as fh:
     json.dump(out, fh, indent=1)
 print(json.dumps(out, indent=1))

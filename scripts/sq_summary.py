@@ -9,10 +9,12 @@ import collections, csv, glob, json, os, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = sys.argv[1] if len(sys.argv) > 1 else "rt_pixel_kernel"
+SRC = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "sq_*", "sq_counter_collection.csv")
+SECTION = sys.argv[3] if len(sys.argv) > 3 else "rt"
 SIMDS = 256 * 4
 
 agg = collections.defaultdict(list)
-for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "sq_*", "sq_counter_collection.csv"))):
+for f in sorted(glob.glob(SRC)):
     for r in csv.DictReader(open(f)):
         if KERNEL in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -27,6 +29,9 @@ sq = {"kernel": KERNEL, "counters_per_launch": c,
       "note": "valu_issue_frac = SQ_INSTS_VALU x 2 cyc / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
 path = os.path.join(ROOT, "profiles", "pmc_summary.json")
 out = json.load(open(path))
-out.setdefault("rt", {})["sq"] = sq
+sqs = out.setdefault(SECTION, {}).setdefault("sq_kernels", {})
+sqs[KERNEL] = sq
+if SECTION == "rt":
+    out["rt"]["sq"] = sq
 json.dump(out, open(path, "w"), indent=1)
 print(json.dumps(sq, indent=1))
