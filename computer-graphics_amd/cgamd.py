@@ -81,6 +81,9 @@ _SIGS = {
     "cg_device_count": (C.c_int, []),
     "cg_rt_load_test_model": (C.c_int, [C.POINTER(Tri), C.c_int, C.POINTER(Sphere)]),
     "cg_glibc_rand": (C.c_int, [C.c_uint64, C.c_int, P]),
+    "cg_starfield_init": (C.c_int, [P, C.c_int]),
+    "cg_starfield_update": (C.c_int, [P, C.c_int, C.c_float]),
+    "cg_starfield_draw": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P]),
     "cg_rt_area_lights": (C.c_int, [C.POINTER(Light), C.c_float, C.c_int, C.POINTER(Light), C.c_int]),
     "cg_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(Tri)]),
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
@@ -178,6 +181,21 @@ def glibc_rand(offset, n):
     if rc:
         raise RuntimeError(f"cg_glibc_rand failed: {rc}")
     return out[:n]
+
+
+def starfield_init(n=1000):
+    """cg_starfield_init: (n, 3) float32 stars (starfield/Source/skeleton.cpp:41-46)."""
+    st = np.zeros((n, 3), np.float32)
+    rc = load().cg_starfield_init(st.ctypes.data_as(C.c_void_p), n)
+    if rc:
+        raise RuntimeError(f"cg_starfield_init failed: {rc}")
+    return st
+
+
+def starfield_update(stars, dt):
+    rc = load().cg_starfield_update(stars.ctypes.data_as(C.c_void_p), len(stars), dt)
+    if rc:
+        raise RuntimeError(f"cg_starfield_update failed: {rc}")
 
 
 def random_scene(n, seed=0x5EED):
@@ -315,6 +333,12 @@ class Context:
         return out
 
     # -- RAST --
+    def starfield_draw(self, stars, width=320, height=256):
+        out = np.zeros(width * height, np.uint32)
+        self._check(self.lib.cg_starfield_draw(self.h, stars.ctypes.data_as(P), len(stars), width, height,
+                                               out.ctypes.data_as(P)), "cg_starfield_draw")
+        return out
+
     def rast_render(self, tris, n, params, light, want_depth=True, want_shadow=True):
         npx = params.width * params.height
         argb = np.zeros(npx, np.uint32)

@@ -75,6 +75,7 @@ struct cg_ctx {
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
     DevBuf rpc, rtl, rrnd, rjt;          // colour modes 1-2 (cg_rast_colour.hip)
+    DevBuf sstars, sframe;               // starfield (cg_starfield.hip)
     int n_room = -1, n_boxes = 0;
 };
 
@@ -98,6 +99,8 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
     case 11: b = &c->rtl; break;
     case 12: b = &c->rrnd; break;
     case 13: b = &c->rjt; break;
+    case 14: b = &c->sstars; break;
+    case 15: b = &c->sframe; break;
     default: *e = hipErrorInvalidValue; return nullptr;
     }
     *e = b->ensure(bytes);
@@ -120,6 +123,7 @@ void rast_release(cg_ctx *c)
     c->rargb.release(); c->rdepth.release(); c->rshadow.release(); c->rcount.release();
     c->rrecs.release(); c->rgeo.release(); c->rroom.release(); c->rboxes.release();
     c->rpc.release(); c->rtl.release(); c->rrnd.release(); c->rjt.release();
+    c->sstars.release(); c->sframe.release();
 }
 }  // namespace cg
 

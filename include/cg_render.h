@@ -187,6 +187,15 @@ int cg_rast_draw(cg_ctx *ctx, const cg_rast_params *p, uint32_t *argb, float *de
 int cg_rast_draw_device(cg_ctx *ctx, const cg_rast_params *p, uint32_t *d_argb, float *d_depth,
                         int32_t *d_shadow, void *stream);
 
+/* ---- starfield (starfield/Source/skeleton.cpp) -------------------------- */
+/* n stars as (x, y, z) float triples from glibc rand() (:41-46, seed 1). */
+int cg_starfield_init(float *stars, int n);
+/* Update() (:82-104) for a frame time dt in ms (the reference's float(t2 - t)). */
+int cg_starfield_update(float *stars, int n, float dt);
+/* Draw() (:66-79): clear, project each star, PutPixelSDL white; W*H ARGB
+ * into the caller-owned host buffer. */
+int cg_starfield_draw(cg_ctx *ctx, const float *stars, int n, int width, int height, uint32_t *argb);
+
 #ifdef __cplusplus
 }
 #endif

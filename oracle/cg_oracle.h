@@ -132,6 +132,11 @@ int  cgo_rast_polygon_rows(const cgo_pixel *vp, cgo_pixel *left, cgo_pixel *righ
 void cgo_rast_draw(const cgo_rast_params *p, uint32_t *argb, float *depth, int32_t *shadow,
                    float *screen_buf, float *low_buf, float *high_buf, cgo_rast_counters *cnt);
 
+/* ---------------------------- starfield -------------------------------- */
+void cgo_starfield_init(float *stars, int n);
+void cgo_starfield_update(float *stars, int n, float dt);
+void cgo_starfield_draw(const float *stars, int n, int W, int H, uint32_t *argb);
+
 #ifdef __cplusplus
 }
 #endif

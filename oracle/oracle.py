@@ -121,6 +121,9 @@ def load():
         "cgo_rast_draw": (None, [C.POINTER(RastParams), P, P, P, P, P, P,
                                  C.POINTER(RastCounters)]),
         "cgo_glibc_rand": (None, [C.c_uint64, C.c_int, P]),
+        "cgo_starfield_init": (None, [P, C.c_int]),
+        "cgo_starfield_update": (None, [P, C.c_int, C.c_float]),
+        "cgo_starfield_draw": (None, [P, C.c_int, C.c_int, C.c_int, P]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -213,6 +216,23 @@ def glibc_rand(offset, n):
     lib = load()
     out = np.zeros(n, np.int32)
     lib.cgo_glibc_rand(offset, n, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def starfield_init(n=1000):
+    lib = load()
+    st = np.zeros((n, 3), np.float32)
+    lib.cgo_starfield_init(st.ctypes.data_as(C.c_void_p), n)
+    return st
+
+
+def starfield_update(stars, dt):
+    load().cgo_starfield_update(stars.ctypes.data_as(C.c_void_p), len(stars), dt)
+
+
+def starfield_draw(stars, W=320, H=256):
+    out = np.zeros(W * H, np.uint32)
+    load().cgo_starfield_draw(stars.ctypes.data_as(C.c_void_p), len(stars), W, H, out.ctypes.data_as(C.c_void_p))
     return out
 
 

@@ -50,3 +50,14 @@ def test_glibc_rand_restatement_matches_libc():
     the C library's own rand(), the reference's RNG, at several offsets."""
     for off in (0, 1, 30, 31, 344, 10_007, 1_234_567):
         assert np.array_equal(cgamd.glibc_rand(off, 200), oracle.glibc_rand(off, 200)), off
+
+
+def test_starfield_init_and_update_match_oracle():
+    """starfield/Source/skeleton.cpp:41-46 (glibc rand, double intermediates) and
+    Update :93-100 (z drift in double), library vs oracle, bytes."""
+    a, b = cgamd.starfield_init(1000), oracle.starfield_init(1000)
+    assert a.tobytes() == b.tobytes()
+    for dt in (0.0, 16.0, 33.0, 1000.0, 2500.0):
+        cgamd.starfield_update(a, dt)
+        oracle.starfield_update(b, dt)
+        assert a.tobytes() == b.tobytes(), dt
