@@ -46,7 +46,7 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, float 
 // Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
 // one certificate mask per wave (lane k certifies triangle k).
 #ifndef CG_RT_MIN_WAVES
-#define CG_RT_MIN_WAVES 6   // 80 VGPRs: 6 waves per SIMD without spills (measured best; 7 spills)
+#define CG_RT_MIN_WAVES 6   // 80 VGPRs + 36 B/lane scratch; measured fastest (5: 86 VGPRs, no scratch)
 #endif
 template <bool CULL>
 __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
