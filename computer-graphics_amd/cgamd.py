@@ -92,6 +92,7 @@ _SIGS = {
                                       C.POINTER(RtShard), P, P]),
     "cg_rt_shard_rows": (C.c_int, [C.c_int, C.POINTER(RtShard)]),
     "cg_rt_unstripe_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
+    "cg_rt_unstripe_batch_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "cg_rt_probe_closest": (C.c_int, [P, C.POINTER(Vec4), C.POINTER(Vec4), C.c_int,
                                       C.POINTER(Isect), C.POINTER(C.c_int)]),
     "cg_rt_probe_direct_light": (C.c_int, [P, C.POINTER(Isect), C.POINTER(Light), C.c_int,
@@ -316,6 +317,12 @@ class Context:
         self._check(self.lib.cg_rt_unstripe_device(self.h, P(d_gathered), width, height, nranks,
                                                    stripe_h, P(d_frame), P(stream) if stream else None),
                     "cg_rt_unstripe_device")
+
+    def rt_unstripe_batch_device(self, d_gathered, width, height, nranks, stripe_h, nframes, d_frames,
+                                 stream=None):
+        self._check(self.lib.cg_rt_unstripe_batch_device(self.h, P(d_gathered), width, height, nranks, stripe_h,
+                                                         nframes, P(d_frames), P(stream) if stream else None),
+                    "cg_rt_unstripe_batch_device")
 
     def rt_probe_closest(self, starts, dirs):
         n = len(starts)

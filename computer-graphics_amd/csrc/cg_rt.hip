@@ -127,17 +127,19 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
     out[(size_t)L * F.W + u] = px;
 }
 
-// Reassemble a striped frame after the gather (multi-GPU path).
+// Reassemble striped frames after the gather (multi-GPU path): g holds, per
+// rank, `nframes` shards of rows_per_rank rows; frame f of the output is
+// [f][H][W].
 __global__ void rt_unstripe_kernel(const uint32_t *__restrict__ g, int W, int H, int nranks,
-                                   int stripe_h, int rows_per_rank, uint32_t *__restrict__ frame)
+                                   int stripe_h, int rows_per_rank, int nframes, uint32_t *__restrict__ frames)
 {
     int x = blockIdx.x * blockDim.x + threadIdx.x;
-    int y = blockIdx.y;
+    int y = blockIdx.y, f = blockIdx.z;
     if (x >= W || y >= H) return;
     int k = y / stripe_h;
     int r = k % nranks;
     int L = (k / nranks) * stripe_h + (y - k * stripe_h);
-    frame[(size_t)y * W + x] = g[((size_t)r * rows_per_rank + L) * W + x];
+    frames[((size_t)f * H + y) * W + x] = g[(((size_t)r * nframes + f) * rows_per_rank + L) * W + x];
 }
 
 // Probe kernels (known-answer tests of ClosestIntersection / DirectLight on
@@ -237,11 +239,11 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
 }
 
 hipError_t launch_rt_unstripe(const uint32_t *d_g, int W, int H, int nranks, int stripe_h,
-                              int rows_per_rank, uint32_t *d_frame, hipStream_t st)
+                              int rows_per_rank, int nframes, uint32_t *d_frames, hipStream_t st)
 {
-    dim3 grid((W + 255) / 256, H);
+    dim3 grid((W + 255) / 256, H, nframes);
     hipLaunchKernelGGL(rt_unstripe_kernel, grid, dim3(256), 0, st, d_g, W, H, nranks, stripe_h,
-                       rows_per_rank, d_frame);
+                       rows_per_rank, nframes, d_frames);
     return hipGetLastError();
 }
 

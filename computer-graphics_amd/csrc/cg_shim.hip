@@ -22,7 +22,7 @@ hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const 
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &);
 void rt_big_diag(const RtFrame &, void *, hipStream_t);
-hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, uint32_t *, hipStream_t);
+hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
 hipError_t launch_rt_probe_closest(const RtFrame &, const cg_tri *, const RtSphere *,
                                    const cg_vec4 *, const cg_vec4 *, int, cg_isect *, int *,
                                    hipStream_t);
@@ -369,17 +369,24 @@ extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, con
     return CG_OK;
 }
 
-extern "C" int cg_rt_unstripe_device(cg_ctx *c, const uint32_t *d_gathered, int width, int height,
-                                     int nranks, int stripe_h, uint32_t *d_frame, void *stream)
+extern "C" int cg_rt_unstripe_batch_device(cg_ctx *c, const uint32_t *d_gathered, int width, int height,
+                                           int nranks, int stripe_h, int nframes, uint32_t *d_frames, void *stream)
 {
-    if (!c || !d_gathered || !d_frame || width <= 0 || height <= 0 || nranks < 1 || stripe_h <= 0)
+    if (!c || !d_gathered || !d_frames || width <= 0 || height <= 0 || nranks < 1 || stripe_h <= 0 ||
+        nframes < 1 || nframes > 65535)
         return CG_E_INVALID;
     cg_rt_shard s{0, nranks, stripe_h};
     int rows = cg_rt_shard_rows(height, &s);
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    CG_TRY(c, launch_rt_unstripe(d_gathered, width, height, nranks, stripe_h, rows, d_frame,
+    CG_TRY(c, launch_rt_unstripe(d_gathered, width, height, nranks, stripe_h, rows, nframes, d_frames,
                                  stream ? (hipStream_t)stream : c->stream), "unstripe launch");
     return CG_OK;
+}
+
+extern "C" int cg_rt_unstripe_device(cg_ctx *c, const uint32_t *d_gathered, int width, int height,
+                                     int nranks, int stripe_h, uint32_t *d_frame, void *stream)
+{
+    return cg_rt_unstripe_batch_device(c, d_gathered, width, height, nranks, stripe_h, 1, d_frame, stream);
 }
 
 extern "C" int cg_rt_probe_closest(cg_ctx *c, const cg_vec4 *starts, const cg_vec4 *dirs, int n,

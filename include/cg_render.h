@@ -136,6 +136,11 @@ int cg_rt_shard_rows(int height, const cg_rt_shard *shard);
  * cg_rt_shard_rows() rows each, in rank order. */
 int cg_rt_unstripe_device(cg_ctx *ctx, const uint32_t *d_gathered, int width, int height,
                           int nranks, int stripe_h, uint32_t *d_frame, void *stream);
+/* Batched form: d_gathered holds, per rank in rank order, `nframes` shards of
+ * cg_rt_shard_rows() rows each (frame-major); d_frames receives nframes
+ * frames of W*H.  Lets a caller gather several frames per collective. */
+int cg_rt_unstripe_batch_device(cg_ctx *ctx, const uint32_t *d_gathered, int width, int height,
+                                int nranks, int stripe_h, int nframes, uint32_t *d_frames, void *stream);
 /* Single-ray probes for known-answer tests: device evaluation of
  * ClosestIntersection (:263-363) and DirectLight (:366-415) on n rays. */
 int cg_rt_probe_closest(cg_ctx *ctx, const cg_vec4 *starts, const cg_vec4 *dirs, int n,

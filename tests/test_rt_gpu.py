@@ -118,6 +118,29 @@ def test_rt_sharded_device_path_reassembles(rt):
         assert np.array_equal(frame.cpu().numpy().view(np.uint32), full), n
 
 
+def test_rt_batched_unstripe(rt):
+    """cg_rt_unstripe_batch_device: per-rank shards of several frames (frame-major
+    per rank, as one gather of K frames lays them out) == each frame rendered whole."""
+    torch = pytest.importorskip("torch")
+    W, H, n, S = 320, 256, 3, cgdist.DEFAULT_STRIPE
+    cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, z, 1.0)) for z in (-3.0, -2.9, -2.6)]
+    fulls = [rt.rt_render(c)[0] for c in cams]
+    st = torch.cuda.Stream()
+    rows = cgdist.shard_rows(H, n, S)
+    K = len(cams)
+    g = torch.zeros(n * K * rows * W, dtype=torch.int32, device="cuda")
+    for r in range(n):
+        for k, cam in enumerate(cams):
+            off = ((r * K + k) * rows * W) * 4
+            rt.rt_render_device(cam, g.data_ptr() + off, cgamd.RtShard(r, n, S), st.cuda_stream)
+    frames = torch.zeros(K * H * W, dtype=torch.int32, device="cuda")
+    rt.rt_unstripe_batch_device(g.data_ptr(), W, H, n, S, K, frames.data_ptr(), st.cuda_stream)
+    st.synchronize()
+    got = frames.cpu().numpy().view(np.uint32).reshape(K, H * W)
+    for k in range(K):
+        assert np.array_equal(got[k], fulls[k]), k
+
+
 def test_rt_full_1080p_vs_oracle(rt, golden):
     """North-star config C2 at full size: the oracle's frame hash, itself pinned
     to the reference build's fingerprint."""
