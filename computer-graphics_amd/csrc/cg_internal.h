@@ -71,6 +71,7 @@ struct RtFrame {
     // of the positions, a centre lc and rho >= max_k |L_k - lc| (FP64, rounded up).
     float lmin[3], lmax[3], lc[3];
     double lrho;
+    float nbound;   // >= |component| of every hit normal (triangle normals; spheres <= 1 + 2^-20)
 };
 
 // ---- RAST --------------------------------------------------------------

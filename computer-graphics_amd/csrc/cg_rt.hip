@@ -46,7 +46,10 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, float 
 // Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
 // one certificate mask per wave (lane k certifies triangle k).
 #ifndef CG_RT_MIN_WAVES
-#define CG_RT_MIN_WAVES 6   // 80 VGPRs + 36 B/lane scratch; measured fastest (5: 86 VGPRs, no scratch)
+#define CG_RT_MIN_WAVES 6   // 80 VGPRs + some scratch; measured fastest (5: no scratch, ~1% slower)
+#endif
+#ifndef CG_RT_POSBOX
+#define CG_RT_POSBOX 1
 #endif
 template <bool CULL>
 __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
@@ -74,33 +77,73 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
         if (lane < F.n_tris && x0 <= x1 && y0 <= y1) keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
         mask = __ballot(keep && lane < F.n_tris);
     }
-    if (!inside) return;
+    // every lane stays to the end: the certificates' wave reductions read all 64
     uint32_t px = 0u;
-    // Pass 1: the 9 primary rays (:134-140); hits staged in LDS (bi, t) so the
-    // shadow certificate of light 0 covers the whole wave's hits at once.
+    // Pass 1: the 9 primary rays (:134-140); hits staged in LDS (bi, t) so one
+    // shadow certificate covers the whole wave's hits and all lights at once.
     __shared__ int s_bi[9][kRtThreads];
     __shared__ float s_t[9][kRtThreads];
     const float m = 0.5f;
-    LaneShadowBox sb;
-    sb.init();
-    const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
     if (active) {
-        for (int k = 0; k < 9; ++k) {
-            const int i = k / 3 - 1, j = k % 3 - 1;
-            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);       // :137
-            float t;
-            int bi = closest_primary<CULL>(F, tc, sph, nd, t, mask);                     // :140
-            s_bi[k][threadIdx.x] = bi;
-            s_t[k][threadIdx.x] = t;
-            if (CULL && F.cull_shadow && F.n_lights > 0 && bi != INT_MIN) {
-                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
-                shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, bi, pos));
+        // sub-ray k = 3 (i + 1) + (j + 1): d = (dir.x + m i, dir.y + m j, focal)  (:137),
+        // walked in three groups sharing d.y (closest_primary_group)
+        float dx[3], dy[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            dx[q] = dir.x + (m * (float)(q - 1));
+            dy[q] = dir.y + (m * (float)(q - 1));
+        }
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+            int bi[3];
+            float t[3];
+            const float dyj[1] = {dy[jj]};
+            closest_primary_group<CULL, 3, 1>(F, tc, sph, dx, dyj, mask, bi, t);         // :140
+#pragma unroll
+            for (int ii = 0; ii < 3; ++ii) {
+                s_bi[3 * ii + jj][threadIdx.x] = bi[ii];
+                s_t[3 * ii + jj][threadIdx.x] = t[ii];
             }
         }
     }
     // one mask for every light of the set (the mask walk must stop at n_tris)
     unsigned long long smask = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
-    if (CULL && F.cull_shadow && F.n_lights > 0) smask = shadow_mask_of(F, tc, sb, lane);
+    if (CULL && F.cull_shadow && F.n_lights > 0) {
+#if CG_RT_POSBOX
+        LanePosBox pb;
+        pb.init();
+        if (active)
+            for (int k = 0; k < 9; ++k) {
+                const int bi = s_bi[k][threadIdx.x];
+                if (bi == INT_MIN) continue;
+                const float t = s_t[k][threadIdx.x];
+                const int i = k / 3 - 1, j = k % 3 - 1;
+                vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+                pb.add(v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z));   // :326/:345
+            }
+        smask = shadow_mask_box(F, tc, shadow_box_of_positions(F, pb), lane);
+#else
+        LaneShadowBox sb;
+        sb.init();
+        const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
+        if (active)
+            for (int k = 0; k < 9; ++k) {
+                const int bi = s_bi[k][threadIdx.x];
+                if (bi == INT_MIN) continue;
+                const float t = s_t[k][threadIdx.x];
+                const int i = k / 3 - 1, j = k % 3 - 1;
+                vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+                shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, bi, pos));
+            }
+        smask = shadow_mask_of(F, tc, sb, lane);
+#endif
+    }
+#ifdef CG_ABLATE_SHADE
+    if (active)
+        for (int k = 0; k < 9; ++k) px += (uint32_t)s_bi[k][threadIdx.x] + __float_as_uint(s_t[k][threadIdx.x]);
+    if (0)
+#endif
     if (active) {
         // Pass 2: shading in the reference's order (:143-157)
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
@@ -124,7 +167,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 #ifdef CG_RT_DIAG_MASKS
     px = ((uint32_t)__popcll(mask) << 8) | (uint32_t)__popcll(smask);   // diagnostics build only
 #endif
-    out[(size_t)L * F.W + u] = px;
+    if (inside) out[(size_t)L * F.W + u] = px;
 }
 
 // Reassemble striped frames after the gather (multi-GPU path): g holds, per

@@ -2,6 +2,14 @@
 // (cg_rt.hip, <= 64 triangles, one certificate mask per wave) and the
 // large-scene binned kernels (cg_rt_big.hip).  Every float op follows
 // raytracer/Source/skeleton.cpp + GLM 0.9.7.2 association (see cg_math.h).
+//
+// Cost-attribution switches (scripts/build_variant.sh only; the images they
+// render are wrong by design and no shipped build defines them):
+//   CG_ABLATE_SPHERE  skip the sphere in primary and shadow tests
+//   CG_ABLATE_SHADOW  skip shadow rays
+//   CG_ABLATE_SHADOW_TESTS  skip the shadow tests but keep their certificate
+//   CG_ABLATE_SHADE   (cg_rt.hip) skip pass 2: closest hits only
+//   CG_RT_DIAG_MASKS  (cg_rt.hip) write certificate-mask popcounts as pixels
 #pragma once
 
 #include <float.h>
@@ -12,14 +20,8 @@ namespace cg {
 
 // ---------------------------------------------------------------------------
 // Sphere::intersect + solveQuadratic (raytracer/Source/TestModelH.h:24-66).
-__device__ __forceinline__ bool sphere_intersect_pre(vec3 L, float c, vec3 dir, float &t);
-__device__ __forceinline__ bool sphere_intersect(const RtSphere &S, vec3 start, vec3 dir, float &t)
-{
-    vec3 L = start - v3(S.cx, S.cy, S.cz);            // :48
-    return sphere_intersect_pre(L, dot(L, L) - S.r2, dir, t);   // :51
-}
-// the same test with start-dependent terms computed by the caller:
-// L = start - centre (:48), c = dot(L, L) - r^2 (:51)
+// The start-dependent terms come from the caller: L = start - centre (:48),
+// c = dot(L, L) - r^2 (:51), so a primary ray's camera terms are hoisted.
 __device__ __forceinline__ bool sphere_intersect_pre(vec3 L, float c, vec3 dir, float &t)
 {
     float a = dot(dir, dir);                           // :49
@@ -44,6 +46,12 @@ __device__ __forceinline__ bool sphere_intersect_pre(vec3 L, float c, vec3 dir, 
     }
     t = x0;
     return true;
+}
+
+__device__ __forceinline__ bool sphere_intersect(const RtSphere &S, vec3 start, vec3 dir, float &t)
+{
+    vec3 L = start - v3(S.cx, S.cy, S.cz);            // :48
+    return sphere_intersect_pre(L, dot(L, L) - S.r2, dir, t);   // :51
 }
 
 __device__ __forceinline__ vec3 object_colour(const RtShade *__restrict__ shade,
@@ -82,6 +90,16 @@ __device__ __forceinline__ vec3 hit_normal(const RtShade *__restrict__ shade, co
 // enough in FP64 and each float det3 evaluation is bounded by 16*eps times the
 // sum of its |triple products| (gamma_4 suffices), so a skipped triangle
 // could never have been accepted: results are bit-identical to testing all.
+// Upper bound of sqrt(x), x >= 0, without the FP64 square-root sequence:
+// the argument is rounded up into float, v_sqrt_f32 (<= 1 ulp) is widened by
+// 2^-20 relative plus 1e-18 absolute (covers float underflow).  Overflow
+// gives +inf, which the certificates' isfinite checks turn into "keep".
+__device__ __forceinline__ double sqrt_ub(double x)
+{
+    const float xf = (float)(x * 1.0000019073486328125);   // 1 + 2^-19
+    return (double)__builtin_amdgcn_sqrtf(xf) * 1.00000095367431640625 + 1e-18;   // 1 + 2^-20
+}
+
 __device__ __forceinline__ void lin_range(double cx, double cy, double hx, double hy, double f,
                                           double X, double Y, double Z, double &lo, double &hi)
 {
@@ -121,6 +139,19 @@ __device__ __forceinline__ bool sign_free_reject(double dlo, double dhi, double 
     if (dhi + Ed > 0.0 && !((uhi + Eu < -tiny) || (vhi + Ev < -tiny) || (blo > Ew))) return false;
     if (dlo - Ed < 0.0 && !((ulo - Eu > tiny) || (vlo - Ev > tiny) || (bhi < -Ew))) return false;
     return true;
+}
+
+// u + v > 1 certain (sg = sign of det, |det| in [dmin, dmax], b = detU +
+// detV - det in [blo, bhi] +- Eb, X >= |detU| + |detV|): b/det > 4 eps
+// (X/dmin + 1), multiplied out by dmin * dmax > 0 so no FP64 divide sits on
+// the certificate's dependency chain; the 2^-40 factor covers the FP64
+// rounding of both sides.
+__device__ __forceinline__ bool uv_sum_reject(int sg, double blo, double bhi, double Eb, double X, double dmin,
+                                              double dmax)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double num = sg > 0 ? blo - Eb : -(bhi + Eb);
+    return num > 0.0 && num * dmin > (4.0 * eps) * (X + dmin) * dmax * (1.0 + 0x1p-40);
 }
 
 __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f)
@@ -166,12 +197,15 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
     if (sg > 0 ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) return true;
     // u + v > 1 after float rounding of u, v and their sum: certain when
     // (U + V - 1) > 4 eps (|U| + |V| + 1), U = detU/det, V = detV/det
-    double K = (fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev) / dmin + 1.0;
-    double margin = 4.0 * eps * K;
-    if (sg > 0 ? ((blo - Eb) / dmax > margin) : ((-(bhi + Eb)) / dmax > margin)) return true;
+    if (uv_sum_reject(sg, blo, bhi, Eb, fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev,
+                      dmin, dmax))
+        return true;
     return false;
 }
 
+// Wave-wide min / max (ds_bpermute butterflies; a DPP row version measured
+// slower here).  Callers keep all 64 lanes alive and give lanes that do not
+// contribute the identity (+-FLT_MAX).
 __device__ __forceinline__ float wave_min(float v)
 {
 #pragma unroll
@@ -225,13 +259,13 @@ __device__ static bool cull_shadow(const RtTri &c, vec3 L, double rho, const Sha
     double Dx = fmax(fabs((double)B.lo[0]), fabs((double)B.hi[0]));
     double Dy = fmax(fabs((double)B.lo[1]), fabs((double)B.hi[1]));
     double Dz = fmax(fabs((double)B.lo[2]), fabs((double)B.hi[2]));
-    double dn = sqrt(Dx * Dx + Dy * Dy + Dz * Dz);
+    double dn = sqrt_ub(Dx * Dx + Dy * Dy + Dz * Dz);
     // |s| <= |a| + |d| + |p| componentwise; p also absorbs s's own rounding
     double Sx = fabs(ax) + rho + Dx + B.pn, Sy = fabs(ay) + rho + Dy + B.pn, Sz = fabs(az) + rho + Dz + B.pn;
-    double pn = (double)B.pn + eps * sqrt(Sx * Sx + Sy * Sy + Sz * Sz) + 1e-12;
-    double n1 = sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
-    double n2 = sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
-    double nN = sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+    double pn = (double)B.pn + eps * sqrt_ub(Sx * Sx + Sy * Sy + Sz * Sz) + 1e-12;
+    double n1 = sqrt_ub((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+    double n2 = sqrt_ub((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+    double nN = sqrt_ub(Nx * Nx + Ny * Ny + Nz * Nz);
     double dlo, dhi, ulo, uhi, vlo, vhi, blo, bhi;
     lin(Nx, Ny, Nz, dlo, dhi);
     lin(Ax, Ay, Az, ulo, uhi);
@@ -261,7 +295,7 @@ __device__ static bool cull_shadow(const RtTri &c, vec3 L, double rho, const Sha
     const double dmax = sg > 0 ? dhi + Ed : -(dlo - Ed);
     const double tiny = 1e-20 * dmax;
     // detT = det + aN + (p.N): t = 1 + (detT - det)/det
-    double tlo = (aN - EaN - Et - Ed) / 1.0, thi = aN + EaN + Et + Ed;   // range of detT - det
+    double tlo = aN - EaN - Et - Ed, thi = aN + EaN + Et + Ed;   // range of detT - det
     // beyond the light: t - 1 > 1e-5 certain -> distance >= rmag (:395)
     if (sg > 0 ? (tlo > 1e-5 * dmax) : (thi < -1e-5 * dmax)) return true;
     // t < 0: detT = det + (detT - det) has the opposite sign of det, i.e.
@@ -269,9 +303,9 @@ __device__ static bool cull_shadow(const RtTri &c, vec3 L, double rho, const Sha
     if (sg > 0 ? (thi + dmax < -tiny - 1e-6 * dmax) : (tlo - dmax > tiny + 1e-6 * dmax)) return true;
     if (sg > 0 ? (uhi + Eu < -tiny) : (ulo - Eu > tiny)) return true;
     if (sg > 0 ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) return true;
-    double K = (fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev) / dmin + 1.0;
-    double margin = 4.0 * eps * K;
-    if (sg > 0 ? ((blo - Eb) / dmax > margin) : ((-(bhi + Eb)) / dmax > margin)) return true;
+    if (uv_sum_reject(sg, blo, bhi, Eb, fmax(fabs(ulo), fabs(uhi)) + Eu + fmax(fabs(vlo), fabs(vhi)) + Ev,
+                      dmin, dmax))
+        return true;
     return false;
 }
 
@@ -357,18 +391,133 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
     return best < bound ? bi : INT_MIN;                       // :357
 }
 
+// ClosestIntersection for a group of NI x NJ camera sub-rays of one pixel
+// (sub-ray (a, b) has d = (dx[a], dy[b], focal)), triangle-outer: each
+// triangle's constants are loaded once per group and the terms that depend
+// on one coordinate of -d only (Q1, Q2, e1x*Q2, e2x*Q1 on d.y; nd.x*K1 on
+// d.x) are evaluated once -- the same float ops on the same operands as
+// closest_primary, so each sub-ray's result is identical to it.  The
+// per-sub-ray divides are independent, which gives the VALU ILP.
+template <bool CULL, int NI, int NJ>
+__device__ __forceinline__ void closest_primary_group(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                      const RtSphere *__restrict__ sph,
+                                                      const float (&dx)[NI], const float (&dy)[NJ],
+                                                      unsigned long long mask, int (&bi)[NI * NJ],
+                                                      float (&bt)[NI * NJ])
+{
+    constexpr int NS = NI * NJ;
+    const float bound = FLT_MAX;
+    const float fz = F.focal, ndz = -fz;
+    float ndx[NI], ndy[NJ], best[NS], len[NS];
+#pragma unroll
+    for (int a = 0; a < NI; ++a) ndx[a] = -dx[a];
+#pragma unroll
+    for (int b = 0; b < NJ; ++b) ndy[b] = -dy[b];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        len[s] = length(v3(dx[s / NJ], dy[s % NJ], fz));      // :307
+        best[s] = bound;
+        bt[s] = 0.f;
+        bi[s] = INT_MIN;
+    }
+    for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
+        int k = it;
+        if (CULL) {
+            k = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+        }
+        const RtTri c = tc[k];
+        float A[NI], Q1[NJ], Q2[NJ], B[NJ], C[NJ];
+#pragma unroll
+        for (int a = 0; a < NI; ++a) A[a] = ndx[a] * c.K1;
+#pragma unroll
+        for (int b = 0; b < NJ; ++b) {
+            Q2[b] = ndy[b] * c.e2z - c.e2y * ndz;
+            Q1[b] = ndy[b] * c.e1z - c.e1y * ndz;
+            B[b] = c.e1x * Q2[b];
+            C[b] = c.e2x * Q1[b];
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int a = s / NJ, b = s % NJ;
+            float det = (A[a] - B[b]) + C[b];                  // det(-d, e1, e2) :289
+            float t = c.detT / det;                            // :306
+            float distance = t * len[s];                       // :307
+            if (distance < 0.0f) continue;                     // :311
+            if (distance >= best[s] || distance > bound) continue;   // :313
+            float Q3 = ndy[b] * c.sz - c.sy * ndz;
+            float detU = (ndx[a] * c.K2 - c.sx * Q2[b]) + c.e2x * Q3;   // :317
+            float detV = (ndx[a] * c.K3 - c.e1x * Q3) + c.sx * Q1[b];   // :320
+            float u = detU / det;
+            float v = detV / det;
+            if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {     // :328-335
+                best[s] = distance;
+                bt[s] = t;
+                bi[s] = k;
+            }
+        }
+    }
+    const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+#ifdef CG_ABLATE_SPHERE
+    if (0)
+#endif
+    for (int q = 0; q < F.n_sph; ++q) {                        // :341-355
+        const RtSphere S = sph[q];
+        const vec3 L = s3 - v3(S.cx, S.cy, S.cz);              // camera-constant (:48, :51)
+        const float cq = dot(L, L) - S.r2;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            float t;
+            if (sphere_intersect_pre(L, cq, v3(dx[s / NJ], dy[s % NJ], fz), t) && t < best[s]) {
+                best[s] = t;
+                bt[s] = t;
+                bi[s] = -1 - q;
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+        if (!(best[s] < bound)) bi[s] = INT_MIN;               // :357
+}
+
 // Shadow test of DirectLight (skeleton.cpp:394-398): ClosestIntersection
 // from `start` towards the light, shadowed iff its distance < rmag.  The
 // closest distance is < rmag iff SOME accepted hit is, so this is an
 // any-hit search bounded by rmag with an early exit; triangles are tested
 // with the reference's float ops (their acceptance does not depend on the
 // running minimum, only on `distance < rmag` here).
+// One triangle of the shadow test (skeleton.cpp:289-335 from a generic
+// start): an accepted hit with distance < rmag (:394-395).
+__device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 nd, float len, float rmag)
+{
+    float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
+    float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+    float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+    float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;
+    float K2 = sy * c.e2z - c.e2y * sz;
+    float K4 = sy * c.e1z - c.e1y * sz;
+    float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;                    // det(s, e1, e2)
+    float t = detT / det;
+    float distance = t * len;
+    if (distance < 0.0f) return false;
+    if (distance >= rmag || distance > FLT_MAX) return false;
+    float Q3 = nd.y * sz - sy * nd.z;
+    float K3 = c.e1y * sz - sy * c.e1z;
+    float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
+    float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
+    float u = detU / det;
+    float v = detV / det;
+    return (u >= 0) && (v >= 0) && ((u + v) <= 1);
+}
+
 template <bool CULL>
 __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restrict__ tc,
                                          const RtSphere *__restrict__ sph, vec3 start, vec3 d,
                                          float rmag, unsigned long long mask)
 {
-    const float bound = FLT_MAX;
+#ifdef CG_ABLATE_SHADOW_TESTS
+    return mask == (unsigned long long)F.W * 0x9E3779B97F4A7C15ull;   // opaque: keeps the certificate live
+#endif
     vec3 nd = -d;
     float len = length(d);
     for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
@@ -377,25 +526,7 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
             k = __builtin_ctzll(mask);
             mask &= mask - 1ull;
         }
-        const RtTri c = tc[k];
-        float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
-        float Q2 = nd.y * c.e2z - c.e2y * nd.z;
-        float Q1 = nd.y * c.e1z - c.e1y * nd.z;
-        float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;
-        float K2 = sy * c.e2z - c.e2y * sz;
-        float K4 = sy * c.e1z - c.e1y * sz;
-        float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;                    // det(s, e1, e2)
-        float t = detT / det;
-        float distance = t * len;
-        if (distance < 0.0f) continue;
-        if (distance >= rmag || distance > bound) continue;
-        float Q3 = nd.y * sz - sy * nd.z;
-        float K3 = c.e1y * sz - sy * c.e1z;
-        float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
-        float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
-        float u = detU / det;
-        float v = detV / det;
-        if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) return true;
+        if (tri_shadow_hit(tc[k], start, nd, len, rmag)) return true;
     }
 #ifdef CG_ABLATE_SPHERE
     if (0)
@@ -405,6 +536,28 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
         if (sphere_intersect(sph[k], start, d, t) && t < rmag) return true;
     }
     return false;
+}
+
+// DirectLight's lit branch (skeleton.cpp:400-412): r = light - pos, rmag its
+// FP64 magnitude (:370-371), normal at the hit (:377-387).
+__device__ __forceinline__ vec3 direct_light_lit(const RtLight &Lt, vec3 r, float rmag, vec3 normal,
+                                                 vec3 objColor)
+{
+    vec3 nd = normalize(r);                                              // :400
+    float a = dot(nd, normal);                                           // :403
+    const float b = (float)(4 * M_PI);                                   // :404
+    float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
+    if (a <= 0) a = 0.f;                                                 // :409
+    vec3 lc = v3(Lt.r, Lt.g, Lt.b);
+    return ((objColor * lc) * a) / area;                                 // :412
+}
+
+// r_magnitude (skeleton.cpp:371): the norm in FP64, rounded to float.
+__device__ __forceinline__ float light_rmag(vec3 r)
+{
+    double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
+           r2 = (double)r.z * (double)r.z;
+    return (float)sqrt((r0 + r1) + r2);
 }
 
 // DirectLight (skeleton.cpp:366-415) for a hit at `pos` on object `bi`.
@@ -417,21 +570,13 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     const RtLight Lt = F.lights[l];                                      // uniform: scalar loads
     vec3 lp = v3(Lt.x, Lt.y, Lt.z);
     vec3 r = lp - pos;                                                   // :370
-    double r0 = (double)r.x * (double)r.x, r1 = (double)r.y * (double)r.y,
-           r2 = (double)r.z * (double)r.z;
-    float rmag = (float)sqrt((r0 + r1) + r2);                            // :371
+    float rmag = light_rmag(r);                                          // :371
     vec3 normal = hit_normal(shade, sph, bi, pos);
     vec3 origin = pos + normal * 0.00001f;                              // :394
 #ifndef CG_ABLATE_SHADOW
     if (shadowed<CULL>(F, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
 #endif
-    vec3 nd = normalize(r);                                              // :400
-    float a = dot(nd, normal);                                           // :403
-    const float b = (float)(4 * M_PI);                                   // :404
-    float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
-    if (a <= 0) a = 0.f;                                                 // :409
-    vec3 lc = v3(Lt.r, Lt.g, Lt.b);
-    return ((objColor * lc) * a) / area;                                 // :412
+    return direct_light_lit(Lt, r, rmag, normal, objColor);
 }
 
 // Shadow-ray certificate for light l: per-lane box of d = L - pos and bound
@@ -464,9 +609,56 @@ __device__ __forceinline__ void shadow_box_add(LaneShadowBox &b, vec3 lmin, vec3
     b.pn = fmaxf(b.pn, pb);
 }
 
+// Cornell-box form of the shadow certificate's input: per lane only the
+// extremes of the hit positions (6 min/max per hit).  The wave then derives
+// the direction box -- d_k = fl(L_k - pos) is monotone in L_k and in pos, so
+// every d lies in [fl(lmin - pos_max), fl(lmax - pos_min)] -- and bounds
+// p = S - L + d = (S - pos) + rounding(d) without the hit normals:
+//   |S_c - pos_c| <= |fl(n_c 1e-5f)| (1 + 2^-24) + 2^-24 |pos_c|,  |n_c| <= nbound
+//   |rounding(d_c)| <= 2^-24 |d_c|
+// (S = pos + n * 0.00001f, skeleton.cpp:394; nbound = the scene's largest
+// normal component, from cg_rt_set_scene).  A non-finite position or bound
+// turns the box infinite, i.e. no triangle is culled.
+struct LanePosBox {
+    float lo[3], hi[3];
+    __device__ void init()
+    {
+        lo[0] = lo[1] = lo[2] = FLT_MAX;
+        hi[0] = hi[1] = hi[2] = -FLT_MAX;
+    }
+    __device__ void add(vec3 p)
+    {
+        if (!isfinite((p.x + p.y) + p.z)) {
+            lo[0] = lo[1] = lo[2] = -INFINITY;
+            hi[0] = hi[1] = hi[2] = INFINITY;
+            return;
+        }
+        lo[0] = fminf(lo[0], p.x); hi[0] = fmaxf(hi[0], p.x);
+        lo[1] = fminf(lo[1], p.y); hi[1] = fmaxf(hi[1], p.y);
+        lo[2] = fminf(lo[2], p.z); hi[2] = fmaxf(hi[2], p.z);
+    }
+};
+
 // Whole wave, converged control flow.
-__device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, const RtTri *__restrict__ tc,
-                                                             const LaneShadowBox &b, int lane)
+__device__ __forceinline__ ShadowBox shadow_box_of_positions(const RtFrame &F, const LanePosBox &b)
+{
+    ShadowBox B;
+    float pn = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float plo = wave_min(b.lo[c]), phi = wave_max(b.hi[c]);
+        B.lo[c] = F.lmin[c] - phi;
+        B.hi[c] = F.lmax[c] - plo;
+        const float P = fmaxf(fabsf(plo), fabsf(phi)), D = fmaxf(fabsf(B.lo[c]), fabsf(B.hi[c]));
+        pn += (F.nbound * 1.0001e-5f + (P + F.nbound * 1e-4f) * 0x1p-23f) + D * 0x1p-23f;
+    }
+    // float evaluation: < 16 rounded positive terms, covered by 1 + 2^-18
+    B.pn = pn * 1.000003814697265625f + 1e-30f;
+    return B;
+}
+
+// Whole wave, converged control flow: the wave's box of its lanes' boxes.
+__device__ __forceinline__ ShadowBox shadow_box_reduce(const LaneShadowBox &b)
 {
     ShadowBox B;
 #pragma unroll
@@ -475,10 +667,23 @@ __device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, c
         B.hi[c] = wave_max(b.hi[c]);
     }
     B.pn = wave_max(b.pn);
+    return B;
+}
+
+// Lane k certifies triangle k for every shadow ray in box B (whole wave).
+__device__ __forceinline__ unsigned long long shadow_mask_box(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                              const ShadowBox &B, int lane)
+{
     bool keep = true;
     if (lane < F.n_tris && B.lo[0] <= B.hi[0])
         keep = !cull_shadow(tc[lane], v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, B);
     return __ballot(keep && lane < F.n_tris);
+}
+
+__device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                             const LaneShadowBox &b, int lane)
+{
+    return shadow_mask_box(F, tc, shadow_box_reduce(b), lane);
 }
 
 __device__ __forceinline__ int shard_row(const RtFrame &F, int L)

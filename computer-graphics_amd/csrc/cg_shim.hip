@@ -69,6 +69,7 @@ struct cg_ctx {
     std::string err;
     // RT scene
     int n_tris = -1, n_sph = 0;
+    float nbound = 0.f;   // largest |normal component| of the scene (shadow certificate)
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
@@ -220,6 +221,14 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
         }
     }
     CG_TRY(c, hipStreamSynchronize(c->stream), "scene upload");
+    // Hit normals: the triangles' own (skeleton.cpp:378) and normalize(pos -
+    // centre) for spheres (:385), whose components are <= 1 up to rounding.
+    float nb = n_spheres > 0 ? 1.00000095367431640625f : 0.f;   // 1 + 2^-20
+    for (int i = 0; i < n_tris; ++i) {
+        const float q[3] = {tris[i].normal.x, tris[i].normal.y, tris[i].normal.z};
+        for (float x : q) nb = std::isfinite(x) ? std::max(nb, std::fabs(x)) : INFINITY;
+    }
+    c->nbound = nb;
     c->n_tris = n_tris;
     c->n_sph = n_spheres;
     return CG_OK;
@@ -282,6 +291,7 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     std::memcpy(F.R, cam->R, sizeof(F.R));
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
+    F.nbound = c->nbound;
     cg_rt_shard one{0, 1, kRtTileH};
     const cg_rt_shard *s = shard ? shard : &one;
     if (s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0 ||
@@ -406,6 +416,7 @@ extern "C" int cg_rt_probe_closest(cg_ctx *c, const cg_vec4 *starts, const cg_ve
     std::memset(&F, 0, sizeof(F));
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
+    F.nbound = c->nbound;
     CG_TRY(c, launch_rt_probe_closest(F, (const cg_tri *)c->tris.p, (const RtSphere *)c->sph.p,
                                       (const cg_vec4 *)c->probe_a.p, (const cg_vec4 *)c->probe_b.p, n,
                                       (cg_isect *)c->probe_c.p, (int *)c->probe_d.p, c->stream), "probe");
@@ -430,6 +441,7 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     std::memset(&F, 0, sizeof(F));
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
+    F.nbound = c->nbound;
     int rc = set_lights(c, light, 1, c->stream, F);
     if (rc) return rc;
     // shadow rays use generic starts: RtTri constants are camera-independent
