@@ -15,7 +15,8 @@ from __future__ import annotations
 
 import numpy as np
 
-DEFAULT_STRIPE = 8   # = the RT workgroup tile height (cg_internal.h kRtTileH)
+DEFAULT_STRIPE = 8   # = the general RT kernel's tile height (cg_internal.h kRtTileH)
+LATTICE_STRIPE = 15  # = the lattice kernel's tile height (cg_rt.hip kLatTileH): C2's stripes
 
 
 def shard_rows(height: int, nranks: int, stripe_h: int = DEFAULT_STRIPE) -> int:

@@ -8,6 +8,7 @@
 // skeleton.cpp + GLM 0.9.7.2 association, compiled with -ffp-contract=off,
 // IEEE div/sqrt and denormals on, FP64 where the reference promotes.
 #include <float.h>
+#include <stdlib.h>
 
 #include "cg_rt_dev.h"
 
@@ -170,6 +171,163 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
     if (inside) out[(size_t)L * F.W + u] = px;
 }
 
+// ---------------------------------------------------------------------------
+// Lattice form of Draw (skeleton.cpp:104-169) for an unrotated camera and one
+// light -- the C2 configuration.  With R the identity, a pixel's direction is
+// (u - W/2, v - H/2) exactly (mat4_mul adds only +-0 terms), and sub-ray
+// (i, j) is (x + 0.5 i, y + 0.5 j), exactly representable: the 9 sub-rays of
+// all pixels lie on a half-pixel lattice, and pixel (u, v)'s sub-ray (i, j) IS
+// the lattice ray (2u + i, 2v + j) of its neighbours, bit for bit.  A sub-ray's
+// whole contribution -- closest hit (:140), DirectLight (:151-153) and the
+// ambient term (:156) -- depends only on the ray, so each lattice ray is traced
+// once per tile (65 x 17 rays for 32 x 8 pixels instead of 2304) and every
+// pixel then adds its nine contributions in the reference's order
+// (pc += DirectLight; pc += objColor * indirect, k = 0..8), so the float sums
+// are formed exactly as the reference forms them.
+#ifndef CG_RT_LAT_WGCERT
+#define CG_RT_LAT_WGCERT 1   // 1: one primary and one shadow certificate per tile (wave 0)
+#endif
+constexpr int kLatTileW = 16, kLatTileH = 15;   // 240 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
+constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
+
+__global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                                  const RtShade *__restrict__ shade,
+                                                                  const RtSphere *__restrict__ sph,
+                                                                  uint32_t *__restrict__ out)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int u0 = blockIdx.x * kLatTileW, L0 = blockIdx.y * kLatTileH;
+    const int v0 = shard_row(F, L0);   // the tile's rows v0 .. v0 + 14 lie in one stripe
+    const int nu = min(kLatTileW, F.W - u0);
+    const int nv = max(0, min(min(kLatTileH, F.rows_out - L0), F.H - v0));
+    __shared__ int s_bi[kLatN];
+    __shared__ float s_r[kLatN], s_g[kLatN], s_b[kLatN];   // DirectLight; s_r holds t after pass 1
+    __shared__ RtShade s_shade[64];
+    if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
+    // lattice point (cx, cy) <-> ray d = (0.5 (ax0 + cx), 0.5 (ay0 + cy), focal)
+    const int ax0 = 2 * (u0 - F.W / 2) - 1, ay0 = 2 * (v0 - F.H / 2) - 1;
+    // the needed points (2 nu + 1) x (2 nv + 1), row-major; wave w takes the w-th quarter
+    const int cols = 2 * nu + 1, rows = nv > 0 ? 2 * nv + 1 : 0, npts = cols * rows;
+    const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
+#if CG_RT_LAT_WGCERT
+    // primary certificate over the tile's lattice box (exact extremes), by wave 0
+    __shared__ unsigned long long s_mask;
+    if (wave == 0) {
+        bool keep = false;
+        if (npts > 0 && lane < F.n_tris) {
+            const float x0 = 0.5f * (float)ax0, x1 = 0.5f * (float)(ax0 + cols - 1);
+            const float y0 = 0.5f * (float)ay0, y1 = 0.5f * (float)(ay0 + rows - 1);
+            keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (lane == 0) s_mask = m;
+    }
+    __syncthreads();
+    const unsigned long long mask = s_mask;
+#else
+    // primary certificate over the wave's lattice box (exact extremes, no reduction needed)
+    unsigned long long mask = 0ull;
+    {
+        bool keep = false;
+        if (p_lo < p_hi && lane < F.n_tris) {
+            const int r0 = p_lo / cols, r1 = (p_hi - 1) / cols;
+            const int c0 = r0 == r1 ? p_lo % cols : 0, c1 = r0 == r1 ? (p_hi - 1) % cols : cols - 1;
+            const float x0 = 0.5f * (float)(ax0 + c0), x1 = 0.5f * (float)(ax0 + c1);
+            const float y0 = 0.5f * (float)(ay0 + r0), y1 = 0.5f * (float)(ay0 + r1);
+            keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
+        }
+        mask = __ballot(keep);
+    }
+#endif
+    // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
+    LanePosBox pb;
+    pb.init();
+    for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
+        const int p = p0 + lane;
+        if (p < p_hi) {
+            const int cy = p / cols, cx = p - cy * cols, idx = cy * kLatW + cx;
+            const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
+            float t;
+            const int bi = closest_primary<true>(F, tc, sph, v3(X, Y, F.focal), t, mask);
+            s_bi[idx] = bi;
+            s_r[idx] = t;
+            if (bi != INT_MIN) pb.add(v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal));   // :326/:345
+        }
+    }
+    unsigned long long smask = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
+#if CG_RT_LAT_WGCERT
+    if (F.cull_shadow) {   // one shadow certificate for the tile's hits, by wave 0
+        __shared__ float s_pbox[4][6];
+        float lo[3], hi[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = wave_min(pb.lo[c]);
+            hi[c] = wave_max(pb.hi[c]);
+        }
+        if (lane == 0)
+            for (int c = 0; c < 3; ++c) {
+                s_pbox[wave][c] = lo[c];
+                s_pbox[wave][3 + c] = hi[c];
+            }
+        __syncthreads();
+        if (wave == 0) {
+            LanePosBox tb;   // the tile's box, the same in every lane
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                tb.lo[c] = fminf(fminf(s_pbox[0][c], s_pbox[1][c]), fminf(s_pbox[2][c], s_pbox[3][c]));
+                tb.hi[c] = fmaxf(fmaxf(s_pbox[0][3 + c], s_pbox[1][3 + c]), fmaxf(s_pbox[2][3 + c], s_pbox[3][3 + c]));
+            }
+            const unsigned long long m = shadow_mask_box(F, tc, shadow_box_of_positions(F, tb), lane);
+            if (lane == 0) s_mask = m;
+        }
+        __syncthreads();
+        smask = s_mask;
+    }
+#else
+    if (F.cull_shadow) smask = shadow_mask_box(F, tc, shadow_box_of_positions(F, pb), lane);
+#endif
+    // Pass 2: DirectLight of each lattice ray that hit (:151-153)
+#ifdef CG_ABLATE_SHADE
+    if (smask == 12345ull)
+#endif
+    for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
+        const int p = p0 + lane;
+        if (p < p_hi) {
+            const int cy = p / cols, cx = p - cy * cols, idx = cy * kLatW + cx;
+            const int bi = s_bi[idx];
+            if (bi != INT_MIN) {
+                const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
+                const float t = s_r[idx];
+                const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
+                const vec3 dl = direct_light<true>(F, tc, shade, sph, bi, pos, object_colour(shade, sph, bi), 0, smask);
+                s_r[idx] = dl.x;
+                s_g[idx] = dl.y;
+                s_b[idx] = dl.z;
+            }
+        }
+    }
+    __syncthreads();
+    // Pixels: the nine contributions in the reference's order (:134-166)
+    const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+    if (tx < nu && ty < nv) {
+        vec3 pc = v3(0.0f, 0.0f, 0.0f);
+        bool valid = false;
+        const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int i = k / 3 - 1, j = k % 3 - 1;
+            const int idx = (2 * ty + 1 + j) * kLatW + (2 * tx + 1 + i);
+            const int bi = s_bi[idx];
+            if (bi == INT_MIN) continue;
+            valid = true;
+            pc = pc + v3(s_r[idx], s_g[idx], s_b[idx]);                                   // :151-153
+            pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
+        }
+        const uint32_t px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
+        out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
+    }
+}
+
 // Reassemble striped frames after the gather (multi-GPU path): g holds, per
 // rank, `nframes` shards of rows_per_rank rows; frame f of the output is
 // [f][H][W].
@@ -268,11 +426,32 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const float cam[4], Rt
     return hipGetLastError();
 }
 
+// The lattice kernel's precondition: R is the identity up to the sign of its
+// zeros (then mat4_mul returns (x, y) bit for bit), pixel offsets stay far
+// inside float's exact integer range, and tiles do not straddle stripes.
+static bool rt_lattice_ok(const RtFrame &F)
+{
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) {
+            const float e = F.R[4 * c + r];
+            if (r == c ? e != 1.0f : e != 0.0f) return false;
+        }
+    return F.W < (1 << 20) && F.H < (1 << 20) && (F.nranks == 1 || F.stripe_h % kLatTileH == 0);
+}
+
 hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
                             const RtSphere *d_sph, uint32_t *d_out, hipStream_t st)
 {
     dim3 grid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    if (F.n_tris <= 64 && F.cull_primary)
+    static const bool lattice_on = [] {
+        const char *e = getenv("CG_RT_LATTICE");
+        return !e || atoi(e) != 0;
+    }();
+    if (lattice_on && F.n_tris <= 64 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F))
+        hipLaunchKernelGGL(rt_lattice_kernel,
+                           dim3((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH),
+                           dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_out);
+    else if (F.n_tris <= 64 && F.cull_primary)
         hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     else

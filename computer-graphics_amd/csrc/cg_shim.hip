@@ -294,9 +294,7 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     F.nbound = c->nbound;
     cg_rt_shard one{0, 1, kRtTileH};
     const cg_rt_shard *s = shard ? shard : &one;
-    if (s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0 ||
-        s->stripe_h % kRtTileH)
-        return CG_E_INVALID;
+    if (s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0) return CG_E_INVALID;
     F.rank = s->rank;
     F.nranks = s->nranks;
     F.stripe_h = s->stripe_h;

@@ -59,7 +59,9 @@ typedef struct {
 
 /* Row sharding for the multi-GPU path: stripes of `stripe_h` rows are dealt
  * round-robin over `nranks`; this rank renders stripes k with
- * k % nranks == rank, packed in order into its output. */
+ * k % nranks == rank, packed in order into its output.  Any stripe_h >= 1 is
+ * exact; for speed use a multiple of 15 for the unrotated one-light camera
+ * (the lattice kernel's tile height) and of 8 otherwise. */
 typedef struct { int rank, nranks, stripe_h; } cg_rt_shard;
 
 /* rasteriser/Source/TestModelH.h:13-42 `Triangle` (84 B). */

@@ -8,7 +8,7 @@ quad-cycles and WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY = WAVE_CYCLES.
 import collections, csv, glob, json, os, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = sys.argv[1] if len(sys.argv) > 1 else "rt_pixel_kernel"
+KERNEL = sys.argv[1] if len(sys.argv) > 1 else "rt_lattice_kernel"
 SRC = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "sq_*", "sq_counter_collection.csv")
 SECTION = sys.argv[3] if len(sys.argv) > 3 else "rt"
 SIMDS = 256 * 4

@@ -64,12 +64,15 @@ def test_stripe_gather_unstripe_gloo(world, stripe):
     assert q.get(timeout=5) is True
 
 
-def test_row_maps_partition_the_frame():
+@pytest.mark.parametrize("S", [cgdist.DEFAULT_STRIPE, cgdist.LATTICE_STRIPE, 32])
+def test_row_maps_partition_the_frame(S):
     for H_ in (64, 256, 1080, 2160, 1001):
         for n in (1, 2, 3, 4, 8):
-            rows = np.concatenate([cgdist.shard_row_map(H_, r, n) for r in range(n)])
+            rows = np.concatenate([cgdist.shard_row_map(H_, r, n, S) for r in range(n)])
             real = np.sort(rows[rows < H_])
             assert np.array_equal(real, np.arange(H_))
             # equal-size shards, balanced to within one stripe
-            sizes = [int((cgdist.shard_row_map(H_, r, n) < H_).sum()) for r in range(n)]
-            assert max(sizes) - min(sizes) <= cgdist.DEFAULT_STRIPE
+            sizes = [int((cgdist.shard_row_map(H_, r, n, S) < H_).sum()) for r in range(n)]
+            assert max(sizes) - min(sizes) <= S
+    # C2 at 8 GPUs: 15-row stripes split 1080 rows exactly (9 stripes per rank)
+    assert cgdist.shard_rows(1080, 8, cgdist.LATTICE_STRIPE) * 8 == 1080

@@ -105,17 +105,19 @@ def test_rt_sharded_device_path_reassembles(rt):
     full, _ = rt.rt_render(cam)
     st = torch.cuda.Stream()
     torch.cuda.set_stream(st)
-    for n in (2, 3, 8):
-        rows = cgdist.shard_rows(H, n)
-        g = torch.zeros(n * rows * W, dtype=torch.int32, device="cuda")
-        for r in range(n):
-            sh = cgamd.RtShard(r, n, cgdist.DEFAULT_STRIPE)
-            rt.rt_render_device(cam, g.data_ptr() + r * rows * W * 4, sh, st.cuda_stream)
-        frame = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-        rt.rt_unstripe_device(g.data_ptr(), W, H, n, cgdist.DEFAULT_STRIPE, frame.data_ptr(),
-                              st.cuda_stream)
-        st.synchronize()
-        assert np.array_equal(frame.cpu().numpy().view(np.uint32), full), n
+    # 8-row stripes (general kernel's tiles), 15-row (lattice kernel's tiles: the
+    # unrotated one-light camera), and a height that matches neither
+    for S in (cgdist.DEFAULT_STRIPE, cgdist.LATTICE_STRIPE, 12):
+        for n in (2, 3, 8):
+            rows = cgdist.shard_rows(H, n, S)
+            g = torch.zeros(n * rows * W, dtype=torch.int32, device="cuda")
+            for r in range(n):
+                sh = cgamd.RtShard(r, n, S)
+                rt.rt_render_device(cam, g.data_ptr() + r * rows * W * 4, sh, st.cuda_stream)
+            frame = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+            rt.rt_unstripe_device(g.data_ptr(), W, H, n, S, frame.data_ptr(), st.cuda_stream)
+            st.synchronize()
+            assert np.array_equal(frame.cpu().numpy().view(np.uint32), full), (S, n)
 
 
 def test_rt_batched_unstripe(rt):
