@@ -206,8 +206,10 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
     // lattice point (cx, cy) <-> ray d = (0.5 (ax0 + cx), 0.5 (ay0 + cy), focal)
     const int ax0 = 2 * (u0 - F.W / 2) - 1, ay0 = 2 * (v0 - F.H / 2) - 1;
-    // the needed points (2 nu + 1) x (2 nv + 1), row-major; wave w takes the w-th quarter
-    const int cols = 2 * nu + 1, rows = nv > 0 ? 2 * nv + 1 : 0, npts = cols * rows;
+    // the needed points: (2 nu + 1) x (2 nv + 1), walked row-major at the full
+    // pitch kLatW (columns >= cols exist only in tiles cut by the right edge);
+    // wave w takes the w-th quarter
+    const int cols = 2 * nu + 1, rows = nv > 0 ? 2 * nv + 1 : 0, npts = kLatW * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
 #if CG_RT_LAT_WGCERT
     // primary certificate over the tile's lattice box (exact extremes), by wave 0
@@ -223,15 +225,16 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         if (lane == 0) s_mask = m;
     }
     __syncthreads();
-    const unsigned long long mask = s_mask;
+    const unsigned long long mask = uniform_u64(s_mask);
 #else
     // primary certificate over the wave's lattice box (exact extremes, no reduction needed)
     unsigned long long mask = 0ull;
     {
         bool keep = false;
         if (p_lo < p_hi && lane < F.n_tris) {
-            const int r0 = p_lo / cols, r1 = (p_hi - 1) / cols;
-            const int c0 = r0 == r1 ? p_lo % cols : 0, c1 = r0 == r1 ? (p_hi - 1) % cols : cols - 1;
+            const int r0 = p_lo / kLatW, r1 = (p_hi - 1) / kLatW;
+            const int c0 = r0 == r1 ? min(p_lo % kLatW, cols - 1) : 0;
+            const int c1 = r0 == r1 ? min((p_hi - 1) % kLatW, cols - 1) : cols - 1;
             const float x0 = 0.5f * (float)(ax0 + c0), x1 = 0.5f * (float)(ax0 + c1);
             const float y0 = 0.5f * (float)(ay0 + r0), y1 = 0.5f * (float)(ay0 + r1);
             keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
@@ -244,8 +247,8 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     pb.init();
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
-        if (p < p_hi) {
-            const int cy = p / cols, cx = p - cy * cols, idx = cy * kLatW + cx;
+        const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
+        if (p < p_hi && cx < cols) {
             const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
             float t;
             const int bi = closest_primary<true>(F, tc, sph, v3(X, Y, F.focal), t, mask);
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             if (lane == 0) s_mask = m;
         }
         __syncthreads();
-        smask = s_mask;
+        smask = uniform_u64(s_mask);
     }
 #else
     if (F.cull_shadow) smask = shadow_mask_box(F, tc, shadow_box_of_positions(F, pb), lane);
@@ -292,8 +295,8 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 #endif
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
-        if (p < p_hi) {
-            const int cy = p / cols, cx = p - cy * cols, idx = cy * kLatW + cx;
+        const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
+        if (p < p_hi && cx < cols) {
             const int bi = s_bi[idx];
             if (bi != INT_MIN) {
                 const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);

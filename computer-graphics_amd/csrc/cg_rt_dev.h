@@ -206,6 +206,15 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
 // Wave-wide min / max (ds_bpermute butterflies; a DPP row version measured
 // slower here).  Callers keep all 64 lanes alive and give lanes that do not
 // contribute the identity (+-FLT_MAX).
+// A wave-uniform 64-bit value (e.g. a mask read from LDS) moved to SGPRs, so
+// loops over its bits are scalar.
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v)
+{
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ float wave_min(float v)
 {
 #pragma unroll
