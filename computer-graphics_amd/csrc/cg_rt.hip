@@ -184,6 +184,9 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 // pixel then adds its nine contributions in the reference's order
 // (pc += DirectLight; pc += objColor * indirect, k = 0..8), so the float sums
 // are formed exactly as the reference forms them.
+#ifndef CG_RT_LAT_PAIR
+#define CG_RT_LAT_PAIR 1   // pass 1 traces two lattice points per lane per step
+#endif
 #ifndef CG_RT_LAT_WGCERT
 #define CG_RT_LAT_WGCERT 1   // 1: one primary and one shadow certificate per tile (wave 0)
 #endif
@@ -245,6 +248,34 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
     LanePosBox pb;
     pb.init();
+#if CG_RT_LAT_PAIR
+    // two points per lane per step (p and p + 64): one triangle load for both rays
+    for (int p0 = p_lo; p0 < p_hi; p0 += 128) {
+        float X[2], Y[2];
+        bool live[2];
+        int pp[2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            const int p = p0 + 64 * n + lane;
+            const int cy = p / kLatW, cx = p - cy * kLatW;
+            pp[n] = p;
+            live[n] = p < p_hi && cx < cols;
+            X[n] = 0.5f * (float)(ax0 + cx);
+            Y[n] = 0.5f * (float)(ay0 + cy);
+        }
+        int bi[2];
+        float t[2];
+        closest_primary_n<2>(F, tc, sph, X, Y, live, mask, bi, t);                         // :140
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            if (!live[n]) continue;
+            s_bi[pp[n]] = bi[n];
+            s_r[pp[n]] = t[n];
+            if (bi[n] != INT_MIN)
+                pb.add(v3(F.cam[0] + t[n] * X[n], F.cam[1] + t[n] * Y[n], F.cam[2] + t[n] * F.focal));   // :326/:345
+        }
+    }
+#else
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
         const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
@@ -257,6 +288,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             if (bi != INT_MIN) pb.add(v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal));   // :326/:345
         }
     }
+#endif
     unsigned long long smask = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
 #if CG_RT_LAT_WGCERT
     if (F.cull_shadow) {   // one shadow certificate for the tile's hits, by wave 0

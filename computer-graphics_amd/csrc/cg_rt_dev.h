@@ -400,6 +400,73 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
     return best < bound ? bi : INT_MIN;                       // :357
 }
 
+// ClosestIntersection for N independent camera rays of one lane (ray n: d =
+// (X[n], Y[n], focal), traced iff live[n]), triangle-outer: each triangle's
+// constants are loaded once for the N rays and their divides are
+// independent.  Each ray's result equals closest_primary's for it.
+template <int N>
+__device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                  const RtSphere *__restrict__ sph, const float (&X)[N],
+                                                  const float (&Y)[N], const bool (&live)[N],
+                                                  unsigned long long mask, int (&bi)[N], float (&bt)[N])
+{
+    const float bound = FLT_MAX;
+    const float fz = F.focal;
+    float best[N], len[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        len[n] = length(v3(X[n], Y[n], fz));                  // :307
+        best[n] = bound;
+        bt[n] = 0.f;
+        bi[n] = INT_MIN;
+    }
+    while (mask != 0ull) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1ull;
+        const RtTri c = tc[k];
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            if (!live[n]) continue;
+            const vec3 nd = -v3(X[n], Y[n], fz);
+            float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+            float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+            float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;  // det(-d, e1, e2) :289
+            float t = c.detT / det;                               // :306
+            float distance = t * len[n];                          // :307
+            if (distance < 0.0f) continue;                        // :311
+            if (distance >= best[n] || distance > bound) continue;   // :313
+            float Q3 = nd.y * c.sz - c.sy * nd.z;
+            float detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;  // :317
+            float detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;  // :320
+            float u = detU / det;
+            float v = detV / det;
+            if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {        // :328-335
+                best[n] = distance;
+                bt[n] = t;
+                bi[n] = k;
+            }
+        }
+    }
+    const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+    for (int q = 0; q < F.n_sph; ++q) {                           // :341-355
+        const RtSphere S = sph[q];
+        const vec3 L = s3 - v3(S.cx, S.cy, S.cz);                 // camera-constant (:48, :51)
+        const float cq = dot(L, L) - S.r2;
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            float t;
+            if (live[n] && sphere_intersect_pre(L, cq, v3(X[n], Y[n], fz), t) && t < best[n]) {
+                best[n] = t;
+                bt[n] = t;
+                bi[n] = -1 - q;
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+        if (!(best[n] < bound)) bi[n] = INT_MIN;                  // :357
+}
+
 // ClosestIntersection for a group of NI x NJ camera sub-rays of one pixel
 // (sub-ray (a, b) has d = (dx[a], dy[b], focal)), triangle-outer: each
 // triangle's constants are loaded once per group and the terms that depend
