@@ -13,6 +13,7 @@ constexpr int kMaxLights = 4096;   // lights live in a device buffer (scalar loa
 constexpr int kRtTileW = 32;   // RT workgroup: 4 waves, each an 8x8 pixel tile
 constexpr int kRtTileH = 8;
 constexpr int kRtThreads = 256;
+constexpr int kLatTileW = 16, kLatTileH = 15;   // RT lattice kernel tile (cg_rt.hip): 33 x 31 lattice rays
 
 // Per-frame, per-triangle constants of ClosestIntersection for rays that
 // start at the camera (skeleton.cpp:279-306).  Every field is computed with

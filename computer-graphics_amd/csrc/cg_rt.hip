@@ -16,13 +16,8 @@ namespace cg {
 
 // ---------------------------------------------------------------------------
 // Per-frame setup: RtTri constants for camera-origin rays (skeleton.cpp:279-306).
-__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, float cx, float cy,
-                                  float cz, float cw, RtTri *__restrict__ out,
-                                  RtShade *__restrict__ shade)
+__device__ __forceinline__ RtTri rt_tri_const(const cg_tri &T, float cx, float cy, float cz, float cw)
 {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    cg_tri T = tris[i];
     vec3 e1 = v3(T.v1.x - T.v0.x, T.v1.y - T.v0.y, T.v1.z - T.v0.z);   // :283
     vec3 e2 = v3(T.v2.x - T.v0.x, T.v2.y - T.v0.y, T.v2.z - T.v0.z);   // :284
     vec4 sol = v4(cx, cy, cz, cw) - v4(T.v0.x, T.v0.y, T.v0.z, T.v0.w); // :296
@@ -36,11 +31,65 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, float 
     r.K2 = s.y * e2.z - e2.y * s.z;
     r.K3 = e1.y * s.z - s.y * e1.z;
     r.v0x = T.v0.x; r.v0y = T.v0.y; r.v0z = T.v0.z;
-    out[i] = r;
-    RtShade sh;
-    sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
-    sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
-    shade[i] = sh;
+    return r;
+}
+
+// A lattice tile (see rt_lattice_kernel): pixels u0 .. u0 + nu - 1 of rows
+// v0 .. v0 + nv - 1 (local rows L0 ..), lattice point (cx, cy) <-> ray
+// (0.5 (ax0 + cx), 0.5 (ay0 + cy), focal), needed points cols x rows.
+struct LatTile {
+    int u0, L0, v0, nu, nv, ax0, ay0, cols, rows;
+};
+__device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
+{
+    LatTile G;
+    G.u0 = bx * kLatTileW;
+    G.L0 = by * kLatTileH;
+    G.v0 = shard_row(F, G.L0);   // the tile's rows v0 .. v0 + 14 lie in one stripe
+    G.nu = min(kLatTileW, F.W - G.u0);
+    G.nv = max(0, min(min(kLatTileH, F.rows_out - G.L0), F.H - G.v0));
+    G.ax0 = 2 * (G.u0 - F.W / 2) - 1;
+    G.ay0 = 2 * (G.v0 - F.H / 2) - 1;
+    G.cols = 2 * G.nu + 1;
+    G.rows = G.nv > 0 ? 2 * G.nv + 1 : 0;
+    return G;
+}
+
+// Blocks [0, n_prep_blocks): RtTri / RtShade per triangle.  With lat_masks,
+// the blocks after them certify the lattice tiles' camera rays (one wave per
+// tile, lane k = triangle k, the same certificate as rt_pixel_kernel's over
+// the tile's exact lattice box), so the lattice kernel starts from its mask.
+__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, float cx, float cy,
+                                  float cz, float cw, RtTri *__restrict__ out,
+                                  RtShade *__restrict__ shade, int n_prep_blocks, RtFrame F,
+                                  unsigned long long *__restrict__ lat_masks)
+{
+    if ((int)blockIdx.x < n_prep_blocks) {
+        const int i = blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n) return;
+        const cg_tri T = tris[i];
+        out[i] = rt_tri_const(T, cx, cy, cz, cw);
+        RtShade sh;
+        sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
+        sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
+        shade[i] = sh;
+        return;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW;
+    const int tiles = tiles_x * ((F.rows_out + kLatTileH - 1) / kLatTileH);
+    const int tile = ((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave;
+    if (tile >= tiles) return;   // whole wave
+    const LatTile G = lat_tile(F, tile % tiles_x, tile / tiles_x);
+    bool keep = false;
+    if (G.rows > 0 && lane < n) {
+        const RtTri c = rt_tri_const(tris[lane], cx, cy, cz, cw);
+        const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
+        const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
+        keep = !cull_primary(c, x0, x1, y0, y1, F.focal);
+    }
+    const unsigned long long m = __ballot(keep);
+    if (lane == 0) lat_masks[tile] = m;
 }
 
 
@@ -188,63 +237,31 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 #define CG_RT_LAT_PAIR 1   // pass 1 traces two lattice points per lane per step
 #endif
 #ifndef CG_RT_LAT_WGCERT
-#define CG_RT_LAT_WGCERT 1   // 1: one primary and one shadow certificate per tile (wave 0)
+#define CG_RT_LAT_WGCERT 1   // 1: one shadow certificate per tile (wave 0); 0: one per wave
 #endif
-constexpr int kLatTileW = 16, kLatTileH = 15;   // 240 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
+// kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
 
 __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph,
+                                                                  const unsigned long long *__restrict__ lat_masks,
                                                                   uint32_t *__restrict__ out)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int u0 = blockIdx.x * kLatTileW, L0 = blockIdx.y * kLatTileH;
-    const int v0 = shard_row(F, L0);   // the tile's rows v0 .. v0 + 14 lie in one stripe
-    const int nu = min(kLatTileW, F.W - u0);
-    const int nv = max(0, min(min(kLatTileH, F.rows_out - L0), F.H - v0));
+    const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
+    const int u0 = G.u0, L0 = G.L0, nu = G.nu, nv = G.nv, ax0 = G.ax0, ay0 = G.ay0;
+    const int cols = G.cols, rows = G.rows;
     __shared__ int s_bi[kLatN];
     __shared__ float s_r[kLatN], s_g[kLatN], s_b[kLatN];   // DirectLight; s_r holds t after pass 1
     __shared__ RtShade s_shade[64];
     if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
-    // lattice point (cx, cy) <-> ray d = (0.5 (ax0 + cx), 0.5 (ay0 + cy), focal)
-    const int ax0 = 2 * (u0 - F.W / 2) - 1, ay0 = 2 * (v0 - F.H / 2) - 1;
-    // the needed points: (2 nu + 1) x (2 nv + 1), walked row-major at the full
-    // pitch kLatW (columns >= cols exist only in tiles cut by the right edge);
-    // wave w takes the w-th quarter
-    const int cols = 2 * nu + 1, rows = nv > 0 ? 2 * nv + 1 : 0, npts = kLatW * rows;
+    // the needed points, walked row-major at the full pitch kLatW (columns >=
+    // cols exist only in tiles cut by the right edge); wave w takes the w-th quarter
+    const int npts = kLatW * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
-#if CG_RT_LAT_WGCERT
-    // primary certificate over the tile's lattice box (exact extremes), by wave 0
-    __shared__ unsigned long long s_mask;
-    if (wave == 0) {
-        bool keep = false;
-        if (npts > 0 && lane < F.n_tris) {
-            const float x0 = 0.5f * (float)ax0, x1 = 0.5f * (float)(ax0 + cols - 1);
-            const float y0 = 0.5f * (float)ay0, y1 = 0.5f * (float)(ay0 + rows - 1);
-            keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
-        }
-        const unsigned long long m = __ballot(keep);
-        if (lane == 0) s_mask = m;
-    }
-    __syncthreads();
-    const unsigned long long mask = uniform_u64(s_mask);
-#else
-    // primary certificate over the wave's lattice box (exact extremes, no reduction needed)
-    unsigned long long mask = 0ull;
-    {
-        bool keep = false;
-        if (p_lo < p_hi && lane < F.n_tris) {
-            const int r0 = p_lo / kLatW, r1 = (p_hi - 1) / kLatW;
-            const int c0 = r0 == r1 ? min(p_lo % kLatW, cols - 1) : 0;
-            const int c1 = r0 == r1 ? min((p_hi - 1) % kLatW, cols - 1) : cols - 1;
-            const float x0 = 0.5f * (float)(ax0 + c0), x1 = 0.5f * (float)(ax0 + c1);
-            const float y0 = 0.5f * (float)(ay0 + r0), y1 = 0.5f * (float)(ay0 + r1);
-            keep = !cull_primary(tc[lane], x0, x1, y0, y1, F.focal);
-        }
-        mask = __ballot(keep);
-    }
-#endif
+    // the tile's primary certificate (rt_prepare_kernel)
+    const unsigned long long mask = lat_masks[blockIdx.y * gridDim.x + blockIdx.x];
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
     LanePosBox pb;
     pb.init();
@@ -293,6 +310,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 #if CG_RT_LAT_WGCERT
     if (F.cull_shadow) {   // one shadow certificate for the tile's hits, by wave 0
         __shared__ float s_pbox[4][6];
+        __shared__ unsigned long long s_mask;
         float lo[3], hi[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -452,12 +470,20 @@ __global__ void rt_probe_direct_light_kernel(RtFrame F, const RtTri *__restrict_
 // ---------------------------------------------------------------------------
 // Launch helpers (called by the shim).
 hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const float cam[4], RtTri *d_tc,
-                             RtShade *d_shade, hipStream_t st)
+                             RtShade *d_shade, hipStream_t st, const RtFrame *F,
+                             unsigned long long *d_lat_masks)
 {
     if (n <= 0) return hipSuccess;
-    int threads = 256, blocks = (n + threads - 1) / threads;
-    hipLaunchKernelGGL(rt_prepare_kernel, dim3(blocks), dim3(threads), 0, st, d_tris, n, cam[0],
-                       cam[1], cam[2], cam[3], d_tc, d_shade);
+    const int threads = kRtThreads, prep = (n + threads - 1) / threads;
+    int cert = 0;
+    RtFrame Fl{};
+    if (F && d_lat_masks) {
+        Fl = *F;
+        const int tiles = ((F->W + kLatTileW - 1) / kLatTileW) * ((F->rows_out + kLatTileH - 1) / kLatTileH);
+        cert = (tiles + threads / 64 - 1) / (threads / 64);
+    }
+    hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert), dim3(threads), 0, st, d_tris, n, cam[0],
+                       cam[1], cam[2], cam[3], d_tc, d_shade, prep, Fl, d_lat_masks);
     return hipGetLastError();
 }
 
@@ -474,18 +500,31 @@ static bool rt_lattice_ok(const RtFrame &F)
     return F.W < (1 << 20) && F.H < (1 << 20) && (F.nranks == 1 || F.stripe_h % kLatTileH == 0);
 }
 
-hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
-                            const RtSphere *d_sph, uint32_t *d_out, hipStream_t st)
+// Whether launch_rt_pixels runs the lattice kernel for this frame (then the
+// caller has rt_prepare_kernel certify its tiles first).
+bool rt_use_lattice(const RtFrame &F)
 {
-    dim3 grid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     static const bool lattice_on = [] {
         const char *e = getenv("CG_RT_LATTICE");
         return !e || atoi(e) != 0;
     }();
-    if (lattice_on && F.n_tris <= 64 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F))
+    return lattice_on && F.n_tris > 0 && F.n_tris <= 64 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
+}
+
+size_t rt_lattice_tiles(const RtFrame &F)
+{
+    return (size_t)((F.W + kLatTileW - 1) / kLatTileW) * ((F.rows_out + kLatTileH - 1) / kLatTileH);
+}
+
+hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
+                            const RtSphere *d_sph, const unsigned long long *d_lat_masks, uint32_t *d_out,
+                            hipStream_t st)
+{
+    dim3 grid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
+    if (d_lat_masks && rt_use_lattice(F))
         hipLaunchKernelGGL(rt_lattice_kernel,
                            dim3((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH),
-                           dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_out);
+                           dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks, d_out);
     else if (F.n_tris <= 64 && F.cull_primary)
         hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);

@@ -14,9 +14,12 @@
 #include "cg_internal.h"
 
 namespace cg {
-hipError_t launch_rt_prepare(const cg_tri *, int, const float *, RtTri *, RtShade *, hipStream_t);
+hipError_t launch_rt_prepare(const cg_tri *, int, const float *, RtTri *, RtShade *, hipStream_t,
+                             const RtFrame *, unsigned long long *);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
-                            uint32_t *, hipStream_t);
+                            const unsigned long long *, uint32_t *, hipStream_t);
+bool rt_use_lattice(const RtFrame &);
+size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
@@ -71,6 +74,7 @@ struct cg_ctx {
     int n_tris = -1, n_sph = 0;
     float nbound = 0.f;   // largest |normal component| of the scene (shadow certificate)
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
+    DevBuf latmask;                     // lattice tiles' primary certificates (one mask per tile)
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
@@ -321,8 +325,13 @@ extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
 
 static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
 {
+    unsigned long long *lat = nullptr;
+    if (rt_use_lattice(F)) {
+        CG_TRY(c, c->latmask.ensure(rt_lattice_tiles(F) * sizeof(unsigned long long)), "alloc lattice masks");
+        lat = (unsigned long long *)c->latmask.p;
+    }
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, F.cam, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st), "rt_prepare launch");
+                                (RtShade *)c->shade.p, st, &F, lat), "rt_prepare launch");
     if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) {
         // large scene: binned certificates (cg_rt_big.hip)
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
@@ -333,7 +342,7 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t 
         return CG_OK;
     }
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
-                               (const RtSphere *)c->sph.p, d_out, st), "rt_pixel launch");
+                               (const RtSphere *)c->sph.p, lat, d_out, st), "rt_pixel launch");
     return CG_OK;
 }
 
@@ -446,7 +455,7 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     // except s/detT/K2/K3, which the shadow path does not read.
     float zero[4] = {0, 0, 0, 1};
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, c->stream), "prepare");
+                                (RtShade *)c->shade.p, c->stream, nullptr, nullptr), "prepare");
     CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
     CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec3) + 16), "alloc");
     CG_TRY(c, hipMemcpyAsync(c->probe_c.p, isects, (size_t)n * sizeof(cg_isect), hipMemcpyHostToDevice, c->stream), "h2d");
