@@ -448,6 +448,9 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
         }
     }
     const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+#ifdef CG_ABLATE_SPHERE
+    if (0)
+#endif
     for (int q = 0; q < F.n_sph; ++q) {                           // :341-355
         const RtSphere S = sph[q];
         const vec3 L = s3 - v3(S.cx, S.cy, S.cz);                 // camera-constant (:48, :51)
