@@ -90,6 +90,8 @@ _SIGS = {
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
                                       C.POINTER(RtShard), P, P]),
+    "cg_rt_render_frames_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int,
+                                             C.POINTER(RtShard), P, C.c_size_t, P]),
     "cg_rt_shard_rows": (C.c_int, [C.c_int, C.POINTER(RtShard)]),
     "cg_rt_unstripe_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "cg_rt_unstripe_batch_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
@@ -312,6 +314,15 @@ class Context:
         self._check(self.lib.cg_rt_render_device(self.h, lights, len(lights), C.byref(cam), sh,
                                                  P(d_out), P(stream) if stream else None),
                     "cg_rt_render_device")
+
+    def rt_render_frames_device(self, cams, d_out, shard=None, stream=None, lights=None, frame_stride=0):
+        """cg_rt_render_frames_device: len(cams) frames into d_out + f * frame_stride pixels."""
+        lights = default_lights() if lights is None else lights
+        arr = (RtCamera * len(cams))(*cams)
+        sh = C.byref(shard) if shard is not None else None
+        self._check(self.lib.cg_rt_render_frames_device(self.h, lights, len(lights), arr, len(cams), sh, P(d_out),
+                                                        frame_stride, P(stream) if stream else None),
+                    "cg_rt_render_frames_device")
 
     def rt_unstripe_device(self, d_gathered, width, height, nranks, stripe_h, d_frame, stream=None):
         self._check(self.lib.cg_rt_unstripe_device(self.h, P(d_gathered), width, height, nranks,

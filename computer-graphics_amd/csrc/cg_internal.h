@@ -14,6 +14,12 @@ constexpr int kRtTileW = 32;   // RT workgroup: 4 waves, each an 8x8 pixel tile
 constexpr int kRtTileH = 8;
 constexpr int kRtThreads = 256;
 constexpr int kLatTileW = 16, kLatTileH = 15;   // RT lattice kernel tile (cg_rt.hip): 33 x 31 lattice rays
+constexpr int kMaxFrameBatch = 16;   // frames per batched RT launch (cg_rt_render_frames_device)
+
+// cameraPos of each frame of a batched launch (kernarg; blockIdx.z / .y = frame).
+struct RtFrameCams {
+    float c[kMaxFrameBatch][4];
+};
 
 // Per-frame, per-triangle constants of ClosestIntersection for rays that
 // start at the camera (skeleton.cpp:279-306).  Every field is computed with

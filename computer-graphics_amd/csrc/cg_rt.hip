@@ -59,25 +59,31 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // the blocks after them certify the lattice tiles' camera rays (one wave per
 // tile, lane k = triangle k, the same certificate as rt_pixel_kernel's over
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
-__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, float cx, float cy,
-                                  float cz, float cw, RtTri *__restrict__ out,
-                                  RtShade *__restrict__ shade, int n_prep_blocks, RtFrame F,
-                                  unsigned long long *__restrict__ lat_masks)
+// blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
+// out + frame * n, its masks at lat_masks + frame * tiles).
+__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
+                                  RtTri *__restrict__ out, RtShade *__restrict__ shade, int n_prep_blocks,
+                                  RtFrame F, unsigned long long *__restrict__ lat_masks)
 {
+    const int frame = blockIdx.y;
+    const float cx = cams.c[frame][0], cy = cams.c[frame][1], cz = cams.c[frame][2], cw = cams.c[frame][3];
     if ((int)blockIdx.x < n_prep_blocks) {
         const int i = blockIdx.x * blockDim.x + threadIdx.x;
         if (i >= n) return;
         const cg_tri T = tris[i];
-        out[i] = rt_tri_const(T, cx, cy, cz, cw);
-        RtShade sh;
-        sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
-        sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
-        shade[i] = sh;
+        out[(size_t)frame * n + i] = rt_tri_const(T, cx, cy, cz, cw);
+        if (frame == 0) {   // camera-independent
+            RtShade sh;
+            sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
+            sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
+            shade[i] = sh;
+        }
         return;
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW;
     const int tiles = tiles_x * ((F.rows_out + kLatTileH - 1) / kLatTileH);
+    lat_masks += (size_t)frame * tiles;
     const int tile = ((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave;
     if (tile >= tiles) return;   // whole wave
     const LatTile G = lat_tile(F, tile % tiles_x, tile / tiles_x);
@@ -242,12 +248,23 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
 
-__global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel(RtFrame F, const RtTri *__restrict__ tc,
+// blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
+// tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
+// out + frame * out_stride.
+__global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph,
                                                                   const unsigned long long *__restrict__ lat_masks,
+                                                                  RtFrameCams cams, size_t out_stride,
                                                                   uint32_t *__restrict__ out)
 {
+    const int frame = blockIdx.z;
+    RtFrame F = F0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
+    tc += (size_t)frame * F.n_tris;
+    lat_masks += (size_t)frame * gridDim.x * gridDim.y;
+    out += (size_t)frame * out_stride;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
     const int u0 = G.u0, L0 = G.L0, nu = G.nu, nv = G.nv, ax0 = G.ax0, ay0 = G.ay0;
@@ -383,7 +400,19 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 
 // Reassemble striped frames after the gather (multi-GPU path): g holds, per
 // rank, `nframes` shards of rows_per_rank rows; frame f of the output is
-// [f][H][W].
+// [f][H][W].  A pure copy (HBM-bound): 16 B per lane when rows are 16-B
+// aligned (W % 4 == 0), one pixel per lane otherwise.
+__global__ void rt_unstripe4_kernel(const uint4 *__restrict__ g, int W4, int H, int nranks, int stripe_h,
+                                    int rows_per_rank, int nframes, uint4 *__restrict__ frames)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y, f = blockIdx.z;
+    if (x >= W4) return;
+    const int k = y / stripe_h, r = k % nranks;
+    const int L = (k / nranks) * stripe_h + (y - k * stripe_h);
+    frames[((size_t)f * H + y) * W4 + x] = g[(((size_t)r * nframes + f) * rows_per_rank + L) * W4 + x];
+}
+
 __global__ void rt_unstripe_kernel(const uint32_t *__restrict__ g, int W, int H, int nranks,
                                    int stripe_h, int rows_per_rank, int nframes, uint32_t *__restrict__ frames)
 {
@@ -469,7 +498,7 @@ __global__ void rt_probe_direct_light_kernel(RtFrame F, const RtTri *__restrict_
 
 // ---------------------------------------------------------------------------
 // Launch helpers (called by the shim).
-hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const float cam[4], RtTri *d_tc,
+hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
                              RtShade *d_shade, hipStream_t st, const RtFrame *F,
                              unsigned long long *d_lat_masks)
 {
@@ -482,8 +511,8 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const float cam[4], Rt
         const int tiles = ((F->W + kLatTileW - 1) / kLatTileW) * ((F->rows_out + kLatTileH - 1) / kLatTileH);
         cert = (tiles + threads / 64 - 1) / (threads / 64);
     }
-    hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert), dim3(threads), 0, st, d_tris, n, cam[0],
-                       cam[1], cam[2], cam[3], d_tc, d_shade, prep, Fl, d_lat_masks);
+    hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
+                       d_tc, d_shade, prep, Fl, d_lat_masks);
     return hipGetLastError();
 }
 
@@ -516,16 +545,29 @@ size_t rt_lattice_tiles(const RtFrame &F)
     return (size_t)((F.W + kLatTileW - 1) / kLatTileW) * ((F.rows_out + kLatTileH - 1) / kLatTileH);
 }
 
+// Batched lattice launch: nframes frames of F's geometry, frame f with camera
+// cams.c[f] into d_out + f * out_stride (rt_use_lattice(F) must hold).
+hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
+                                    const RtSphere *d_sph, const unsigned long long *d_lat_masks,
+                                    const RtFrameCams &cams, int nframes, size_t out_stride, uint32_t *d_out,
+                                    hipStream_t st)
+{
+    hipLaunchKernelGGL(rt_lattice_kernel,
+                       dim3((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes),
+                       dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks, cams, out_stride, d_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
                             const RtSphere *d_sph, const unsigned long long *d_lat_masks, uint32_t *d_out,
                             hipStream_t st)
 {
     dim3 grid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    if (d_lat_masks && rt_use_lattice(F))
-        hipLaunchKernelGGL(rt_lattice_kernel,
-                           dim3((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH),
-                           dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks, d_out);
-    else if (F.n_tris <= 64 && F.cull_primary)
+    if (d_lat_masks && rt_use_lattice(F)) {
+        RtFrameCams cams{};
+        for (int c = 0; c < 4; ++c) cams.c[0][c] = F.cam[c];
+        return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, 0, d_out, st);
+    } else if (F.n_tris <= 64 && F.cull_primary)
         hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     else
@@ -537,6 +579,12 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
 hipError_t launch_rt_unstripe(const uint32_t *d_g, int W, int H, int nranks, int stripe_h,
                               int rows_per_rank, int nframes, uint32_t *d_frames, hipStream_t st)
 {
+    if (W % 4 == 0 && ((uintptr_t)d_g & 15) == 0 && ((uintptr_t)d_frames & 15) == 0) {
+        const int W4 = W / 4;
+        hipLaunchKernelGGL(rt_unstripe4_kernel, dim3((W4 + 255) / 256, H, nframes), dim3(256), 0, st,
+                           (const uint4 *)d_g, W4, H, nranks, stripe_h, rows_per_rank, nframes, (uint4 *)d_frames);
+        return hipGetLastError();
+    }
     dim3 grid((W + 255) / 256, H, nframes);
     hipLaunchKernelGGL(rt_unstripe_kernel, grid, dim3(256), 0, st, d_g, W, H, nranks, stripe_h,
                        rows_per_rank, nframes, d_frames);

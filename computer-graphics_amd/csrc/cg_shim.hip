@@ -14,8 +14,11 @@
 #include "cg_internal.h"
 
 namespace cg {
-hipError_t launch_rt_prepare(const cg_tri *, int, const float *, RtTri *, RtShade *, hipStream_t,
+hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTri *, RtShade *, hipStream_t,
                              const RtFrame *, unsigned long long *);
+hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
+                                    const unsigned long long *, const RtFrameCams &, int, size_t, uint32_t *,
+                                    hipStream_t);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             const unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
@@ -330,7 +333,9 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t 
         CG_TRY(c, c->latmask.ensure(rt_lattice_tiles(F) * sizeof(unsigned long long)), "alloc lattice masks");
         lat = (unsigned long long *)c->latmask.p;
     }
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, F.cam, (RtTri *)c->tc.p,
+    RtFrameCams cams{};
+    for (int k = 0; k < 4; ++k) cams.c[0][k] = F.cam[k];
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)c->tc.p,
                                 (RtShade *)c->shade.p, st, &F, lat), "rt_prepare launch");
     if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) {
         // large scene: binned certificates (cg_rt_big.hip)
@@ -356,6 +361,68 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
     int rc = fill_frame(c, lights, n_lights, cam, shard, st, F);
     if (rc) return rc;
     return rt_enqueue(c, F, d_out, st);
+}
+
+// Frames f0 .. f0 + nf - 1 of a batch, one prepare + one lattice launch
+// (rt_use_lattice(F) holds for every frame; they differ only in cameraPos).
+static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
+                                    uint32_t *d_out, size_t stride, hipStream_t st)
+{
+    const size_t tiles = rt_lattice_tiles(F);
+    CG_TRY(c, c->latmask.ensure((size_t)nf * tiles * sizeof(unsigned long long)), "alloc lattice masks");
+    CG_TRY(c, c->tc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
+    RtFrameCams fc{};
+    for (int f = 0; f < nf; ++f) {
+        fc.c[f][0] = cams[f].camera.x; fc.c[f][1] = cams[f].camera.y;
+        fc.c[f][2] = cams[f].camera.z; fc.c[f][3] = cams[f].camera.w;
+    }
+    unsigned long long *lat = (unsigned long long *)c->latmask.p;
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)c->tc.p,
+                                (RtShade *)c->shade.p, st, &F, lat), "rt_prepare launch");
+    CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
+                                       (const RtSphere *)c->sph.p, lat, fc, nf, stride, d_out, st),
+           "rt_lattice launch");
+    return CG_OK;
+}
+
+extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int n_lights,
+                                          const cg_rt_camera *cams, int n_frames, const cg_rt_shard *shard,
+                                          uint32_t *d_out, size_t frame_stride, void *stream)
+{
+    if (!c || !d_out || n_frames < 0 || (n_frames && !cams)) return CG_E_INVALID;
+    if (n_frames == 0) return CG_OK;
+    for (int f = 1; f < n_frames; ++f)
+        if (cams[f].width != cams[0].width || cams[f].height != cams[0].height) return CG_E_INVALID;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    RtFrame F;
+    int rc = fill_frame(c, lights, n_lights, &cams[0], shard, st, F);
+    if (rc) return rc;
+    const size_t px = (size_t)F.rows_out * F.W;
+    const size_t stride = frame_stride ? frame_stride : px;
+    if (stride < px) return CG_E_INVALID;
+    // one batched launch needs the lattice path for every frame, frames that
+    // differ only in cameraPos (same focal, R, indirect)
+    bool batch = rt_use_lattice(F);
+    for (int f = 1; batch && f < n_frames; ++f)
+        batch = cams[f].focal == cams[0].focal && cams[f].indirect == cams[0].indirect &&
+                std::memcmp(cams[f].R, cams[0].R, sizeof(cams[0].R)) == 0;
+    if (!batch) {
+        for (int f = 0; f < n_frames; ++f) {
+            if (f) {
+                rc = fill_frame(c, lights, n_lights, &cams[f], shard, st, F);
+                if (rc) return rc;
+            }
+            rc = rt_enqueue(c, F, d_out + (size_t)f * stride, st);
+            if (rc) return rc;
+        }
+        return CG_OK;
+    }
+    for (int f0 = 0; f0 < n_frames; f0 += kMaxFrameBatch) {
+        const int nf = std::min(kMaxFrameBatch, n_frames - f0);
+        rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, d_out + (size_t)f0 * stride, stride, st);
+        if (rc) return rc;
+    }
+    return CG_OK;
 }
 
 extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
@@ -453,8 +520,9 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     if (rc) return rc;
     // shadow rays use generic starts: RtTri constants are camera-independent
     // except s/detT/K2/K3, which the shadow path does not read.
-    float zero[4] = {0, 0, 0, 1};
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, (RtTri *)c->tc.p,
+    RtFrameCams zero{};
+    zero.c[0][3] = 1.0f;
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, 1, (RtTri *)c->tc.p,
                                 (RtShade *)c->shade.p, c->stream, nullptr, nullptr), "prepare");
     CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
     CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec3) + 16), "alloc");

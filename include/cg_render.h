@@ -21,6 +21,7 @@
 #ifndef CG_RENDER_H
 #define CG_RENDER_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -132,6 +133,17 @@ int cg_rt_render(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_
  * `stream`, no synchronisation.  shard may be NULL (= whole frame). */
 int cg_rt_render_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
                         const cg_rt_shard *shard, uint32_t *d_out, void *stream);
+/* n_frames successive frames (the reference's main loop: Update() moves the
+ * camera, Draw() renders, raytracer/Source/skeleton.cpp:91-94 + :104-169),
+ * frame f with camera cams[f] into d_out + f * frame_stride pixels
+ * (frame_stride 0 = cg_rt_shard_rows() * W).  All cameras share width and
+ * height; lights and the shard are common.  Frames of the unrotated one-light
+ * camera that differ only in cameraPos are rendered up to 16 per kernel
+ * launch (a whole GPU's worth of tiles even for a small shard); others are
+ * enqueued one by one.  Each frame equals cg_rt_render_device's. */
+int cg_rt_render_frames_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
+                               int n_frames, const cg_rt_shard *shard, uint32_t *d_out, size_t frame_stride,
+                               void *stream);
 /* Rows a shard renders (including padding rows of its last stripe). */
 int cg_rt_shard_rows(int height, const cg_rt_shard *shard);
 /* Reassemble a frame from gathered shards: d_gathered holds nranks blocks of

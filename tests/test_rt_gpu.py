@@ -143,6 +143,50 @@ def test_rt_batched_unstripe(rt):
         assert np.array_equal(got[k], fulls[k]), k
 
 
+def test_rt_render_frames_batched(rt, golden):
+    """cg_rt_render_frames_device: a camera path (cameraPos moving as the UP/DOWN
+    keys move it) rendered as one batched launch per 16 frames, whole and
+    sharded, == each frame rendered alone; the z = -3 / -2.9 frames also equal
+    the golden fingerprint / screenshot.bmp."""
+    torch = pytest.importorskip("torch")
+    W, H = 320, 256
+    zs = [-3.0, mg.CAM_UP] + [-3.0 + 0.05 * k for k in range(1, 18)]   # 19 frames: two launches
+    cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, z, 1.0)) for z in zs]
+    singles = [rt.rt_render(c)[0] for c in cams]
+    assert np.array_equal(singles[1], mg.screenshot_argb())
+    st = torch.cuda.Stream()
+    for S, n in ((cgdist.LATTICE_STRIPE, 1), (cgdist.LATTICE_STRIPE, 3), (60, 2)):
+        rows = cgdist.shard_rows(H, n, S)
+        stride = rows * W + 96                       # a padded frame stride
+        g = torch.zeros(n * len(cams) * stride, dtype=torch.int32, device="cuda")
+        for r in range(n):
+            rt.rt_render_frames_device(cams, g.data_ptr() + r * len(cams) * stride * 4, cgamd.RtShard(r, n, S),
+                                       st.cuda_stream, frame_stride=stride)
+        st.synchronize()
+        got = g.cpu().numpy().view(np.uint32).reshape(n, len(cams), stride)[:, :, :rows * W]
+        for k in range(len(cams)):
+            frame = cgdist.unstripe_np(got[:, k].reshape(n, rows, W), H, n, S).reshape(-1)
+            assert np.array_equal(frame, singles[k]), (S, n, k)
+
+
+def test_rt_render_frames_fallback(rt):
+    """Frames that cannot share a launch (yaw-rotated R, two lights) go one by one."""
+    torch = pytest.importorskip("torch")
+    W, H = 256, 192
+    cams = [cgamd.rt_camera(W, H, 200.0, (0.0, 0.0, -3.0, 1.0), cgamd.yaw_matrix(y)) for y in (0.0, 0.1)]
+    two = (cgamd.Light * 2)(*cgamd.default_lights(), *cgamd.default_lights())
+    two[1].position = cgamd.Vec4(0.3, -0.5, -0.2, 1.0)
+    for lights in (cgamd.default_lights(), two):
+        singles = [rt.rt_render(c, lights)[0] for c in cams]
+        g = torch.zeros(len(cams) * W * H, dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+        rt.rt_render_frames_device(cams, g.data_ptr(), None, st.cuda_stream, lights)
+        st.synchronize()
+        got = g.cpu().numpy().view(np.uint32).reshape(len(cams), -1)
+        for k in range(len(cams)):
+            assert np.array_equal(got[k], singles[k]), k
+
+
 def test_rt_full_1080p_vs_oracle(rt, golden):
     """North-star config C2 at full size: the oracle's frame hash, itself pinned
     to the reference build's fingerprint."""
