@@ -50,7 +50,12 @@ class RtCamera(C.Structure):
 
 
 class RtShard(C.Structure):
-    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("stripe_h", C.c_int)]
+    """Stripes (rows == 0): RtShard(rank, nranks, stripe_h).  Band: RtShard(row0=a, rows=n)."""
+    _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("stripe_h", C.c_int), ("row0", C.c_int),
+                ("rows", C.c_int)]
+
+
+PIX_ARGB8888, PIX_RGB24 = 0, 1   # cg_render.h CG_PIX_*
 
 
 class RTri(C.Structure):       # rasteriser Triangle, 84 B
@@ -91,7 +96,9 @@ _SIGS = {
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
                                       C.POINTER(RtShard), P, P]),
     "cg_rt_render_frames_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int,
-                                             C.POINTER(RtShard), P, C.c_size_t, P]),
+                                             C.POINTER(RtShard), P, C.c_size_t, C.c_int, P]),
+    "cg_rt_assemble_device": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
+                                        C.c_int, C.c_int, P, C.c_size_t, P]),
     "cg_rt_shard_rows": (C.c_int, [C.c_int, C.POINTER(RtShard)]),
     "cg_rt_unstripe_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "cg_rt_unstripe_batch_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
@@ -315,14 +322,24 @@ class Context:
                                                  P(d_out), P(stream) if stream else None),
                     "cg_rt_render_device")
 
-    def rt_render_frames_device(self, cams, d_out, shard=None, stream=None, lights=None, frame_stride=0):
+    def rt_render_frames_device(self, cams, d_out, shard=None, stream=None, lights=None, frame_stride=0,
+                                pix_format=PIX_ARGB8888):
         """cg_rt_render_frames_device: len(cams) frames into d_out + f * frame_stride pixels."""
         lights = default_lights() if lights is None else lights
         arr = (RtCamera * len(cams))(*cams)
         sh = C.byref(shard) if shard is not None else None
         self._check(self.lib.cg_rt_render_frames_device(self.h, lights, len(lights), arr, len(cams), sh, P(d_out),
-                                                        frame_stride, P(stream) if stream else None),
+                                                        frame_stride, pix_format, P(stream) if stream else None),
                     "cg_rt_render_frames_device")
+
+    def rt_assemble_device(self, d_src, pix_format, row0, rows, width, height, nframes, d_frames, frame_stride=0,
+                           stream=None):
+        """cg_rt_assemble_device: row blocks (row0[b], rows[b]) of nframes frames -> frames."""
+        n = len(rows)
+        r0, rs = (C.c_int * n)(*row0), (C.c_int * n)(*rows)
+        self._check(self.lib.cg_rt_assemble_device(self.h, P(d_src), pix_format, r0, rs, n, width, height, nframes,
+                                                   P(d_frames), frame_stride, P(stream) if stream else None),
+                    "cg_rt_assemble_device")
 
     def rt_unstripe_device(self, d_gathered, width, height, nranks, stripe_h, d_frame, stream=None):
         self._check(self.lib.cg_rt_unstripe_device(self.h, P(d_gathered), width, height, nranks,

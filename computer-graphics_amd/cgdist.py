@@ -40,3 +40,86 @@ def unstripe_np(gathered: np.ndarray, height: int, nranks: int, stripe_h: int = 
     r = k % nranks
     L = (k // nranks) * stripe_h + (y - k * stripe_h)
     return gathered[r, L]
+
+
+# ---- balanced bands (the default multi-GPU layout) -------------------------
+# Each rank renders one contiguous band of rows, so rank 0 can receive every
+# band straight into its row range: no unstripe pass, one p2p transfer per
+# rank per batch of frames.  Band boundaries are chosen to equalise each
+# rank's measured time (rank 0 also pays the frame assembly), re-estimated
+# from per-rank timings during warm-up (rebalance()).
+
+def equal_bands(height: int, nranks: int, align: int = 1):
+    """Contiguous bands of (near) equal height, boundaries on multiples of `align`."""
+    units = -(-height // align)
+    bounds = [min(height, (units * r // nranks) * align) for r in range(nranks + 1)]
+    bounds[-1] = height
+    return [(bounds[r], bounds[r + 1] - bounds[r]) for r in range(nranks)]
+
+
+def band_partition(row_cost, nranks: int, overhead=None):
+    """Contiguous bands minimising max_r (sum of row_cost over band r + overhead[r]).
+    Bisection on the makespan with a greedy sweep; every rank gets >= 1 row when
+    there are enough rows.  Returns [(row0, rows)] in rank order."""
+    c = np.asarray(row_cost, dtype=np.float64)
+    H = len(c)
+    o = np.zeros(nranks) if overhead is None else np.asarray(overhead, dtype=np.float64)
+    C = np.concatenate([[0.0], np.cumsum(c)])
+
+    def sweep(T):
+        b = [0]
+        for r in range(nranks - 1):
+            lo = b[-1]
+            left = nranks - 1 - r                    # ranks still to place after this one
+            hi_max = max(lo + 1, H - left) if H >= nranks else lo + (1 if lo < H else 0)
+            # largest end with cost <= T (at least one row, leaving one per later rank)
+            end = int(np.searchsorted(C, C[lo] + T - o[r], side="right")) - 1
+            end = min(max(end, lo + 1 if lo < H else lo), hi_max)
+            b.append(end)
+        b.append(H)
+        return b
+
+    lo_T, hi_T = 0.0, C[-1] + o.max() + 1.0
+    for _ in range(60):
+        T = 0.5 * (lo_T + hi_T)
+        b = sweep(T)
+        last = C[b[-1]] - C[b[-2]] + o[nranks - 1]
+        if last <= T:
+            hi_T = T
+        else:
+            lo_T = T
+    b = sweep(hi_T)
+    return [(b[r], b[r + 1] - b[r]) for r in range(nranks)]
+
+
+def rebalance(bands, render_s, overhead_s, height: int):
+    """New bands from measured per-rank render times (cost density uniform within
+    each old band) and per-rank fixed overheads (rank 0's assembly)."""
+    cost = np.zeros(height)
+    for (r0, n), t in zip(bands, render_s):
+        if n > 0:
+            cost[r0:r0 + n] = max(float(t), 1e-12) / n
+    return band_partition(cost, len(bands), overhead_s)
+
+
+def pack_rgb24_np(argb: np.ndarray) -> np.ndarray:
+    """CG_PIX_RGB24 of ARGB8888 pixels: the low three bytes (B, G, R) of each."""
+    return argb.astype("<u4").view(np.uint8).reshape(-1, 4)[:, :3].reshape(-1).copy()
+
+
+def assemble_np(src: np.ndarray, bpp: int, bands, width: int, height: int, nframes: int, frames: np.ndarray):
+    """Mirror of rt_assemble_kernel: src = blocks in order, block b = nframes x
+    rows_b rows; frames [nframes, height*width] uint32 updated in place."""
+    off = 0
+    for r0, n in bands:
+        for f in range(nframes):
+            blk = src[off:off + n * width * bpp]
+            off += n * width * bpp
+            if bpp == 4:
+                px = blk.view("<u4")
+            else:
+                b3 = blk.reshape(-1, 3).astype(np.uint32)
+                px = 0x80000000 | b3[:, 0] | (b3[:, 1] << 8) | (b3[:, 2] << 16)
+            rows = min(n, max(0, height - r0))
+            frames[f, r0 * width:(r0 + rows) * width] = px[:rows * width]
+    return frames

@@ -16,6 +16,15 @@ constexpr int kRtThreads = 256;
 constexpr int kLatTileW = 16, kLatTileH = 15;   // RT lattice kernel tile (cg_rt.hip): 33 x 31 lattice rays
 constexpr int kMaxFrameBatch = 16;   // frames per batched RT launch (cg_rt_render_frames_device)
 
+constexpr int kMaxBlocks = 64;       // row blocks of one assembly launch (cg_rt_assemble_device)
+
+// Row blocks of frames for rt_assemble_kernel: block b is rows[b] rows that
+// land at frame rows row0[b] ..; cum = prefix sums of rows.
+struct RtBlocks {
+    int n, W, H, bpp;
+    int row0[kMaxBlocks], rows[kMaxBlocks], cum[kMaxBlocks + 1];
+};
+
 // cameraPos of each frame of a batched launch (kernarg; blockIdx.z / .y = frame).
 struct RtFrameCams {
     float c[kMaxFrameBatch][4];
@@ -72,6 +81,8 @@ struct RtFrame {
     float R[16];
     int n_tris, n_sph, n_lights;
     int rank, nranks, stripe_h, rows_out;
+    int row0;      // first global row (band shards; 0 for stripes): v = row0 + stripe map of L
+    int out_fmt;   // CG_PIX_ARGB8888 (uint32 per pixel) or CG_PIX_RGB24 (3 bytes: B, G, R)
     int cull_primary, cull_shadow;   // certificates on (CG_RT_CULL env: 0 none, 1 primary, 2 both)
     const RtLight *lights;           // n_lights entries, device memory
     // The light set as the shadow certificate sees it: componentwise min/max

@@ -264,6 +264,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
     tc += (size_t)frame * F.n_tris;
     lat_masks += (size_t)frame * gridDim.x * gridDim.y;
+    uint8_t *out8 = (uint8_t *)out + (size_t)frame * out_stride * 3;   // CG_PIX_RGB24
     out += (size_t)frame * out_stride;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
@@ -379,7 +380,9 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     __syncthreads();
     // Pixels: the nine contributions in the reference's order (:134-166)
     const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
-    if (tx < nu && ty < nv) {
+    const bool have = tx < nu && ty < nv;
+    uint32_t px = 0u;
+    if (have) {
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
@@ -393,9 +396,87 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             pc = pc + v3(s_r[idx], s_g[idx], s_b[idx]);                                   // :151-153
             pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
         }
-        const uint32_t px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
-        out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
+        px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
+        if (F.out_fmt == CG_PIX_ARGB8888) out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
     }
+    if (F.out_fmt == CG_PIX_RGB24) {
+        // wire format: the pixel's low three bytes (B, G, R; alpha is always 128).
+        // Full tiles write each row's 48 bytes as 12 dwords.
+        __shared__ uint32_t s_px[kLatTileH * kLatTileW];
+        if (have) s_px[ty * kLatTileW + tx] = px;
+        __syncthreads();
+        if (nu == kLatTileW && (F.W & 3) == 0 && ((uintptr_t)out8 & 3) == 0) {
+            const int t = threadIdx.x, row = t / 12, j = t - 12 * row;
+            if (row < nv) {
+                uint32_t w = 0u;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int byte = 4 * j + b, p = byte / 3, ch = byte - 3 * p;
+                    w |= ((s_px[row * kLatTileW + p] >> (8 * ch)) & 0xffu) << (8 * b);
+                }
+                *(uint32_t *)(out8 + ((size_t)(L0 + row) * F.W + u0) * 3 + 4 * j) = w;
+            }
+        } else if (have) {
+            uint8_t *q = out8 + ((size_t)(L0 + ty) * F.W + u0 + tx) * 3;
+            q[0] = (uint8_t)px;
+            q[1] = (uint8_t)(px >> 8);
+            q[2] = (uint8_t)(px >> 16);
+        }
+    }
+}
+
+// ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): four
+// pixels per lane, three dwords out when aligned.
+__global__ void rt_pack_rgb24_kernel(const uint32_t *__restrict__ src, size_t n_px, uint8_t *__restrict__ dst)
+{
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x, i = 4 * q;
+    if (i >= n_px) return;
+    if (i + 4 <= n_px && ((uintptr_t)(dst + 3 * i) & 3) == 0) {
+        const uint4 p = *(const uint4 *)(src + i);
+        uint32_t *d = (uint32_t *)(dst + 3 * i);
+        d[0] = (p.x & 0xffffffu) | (p.y << 24);
+        d[1] = ((p.y >> 8) & 0xffffu) | (p.z << 16);
+        d[2] = ((p.z >> 16) & 0xffu) | ((p.w & 0xffffffu) << 8);
+        return;
+    }
+    for (size_t k = i; k < n_px && k < i + 4; ++k) {
+        const uint32_t p = src[k];
+        dst[3 * k] = (uint8_t)p;
+        dst[3 * k + 1] = (uint8_t)(p >> 8);
+        dst[3 * k + 2] = (uint8_t)(p >> 16);
+    }
+}
+
+// Frame assembly on the gathering rank: src holds row blocks in order, block
+// b = nframes x rows[b] rows of W pixels (bpp 4: ARGB8888, 3: RGB24 + alpha
+// 128 restored), landing at frame rows row0[b] ...  Four pixels per lane.
+__global__ void rt_assemble_kernel(const uint8_t *__restrict__ src, RtBlocks B, int nframes,
+                                   uint32_t *__restrict__ frames, size_t frame_stride)
+{
+    const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+    const int y = blockIdx.y, f = blockIdx.z;   // y: row over all blocks
+    int b = 0;
+    while (b + 1 < B.n && B.cum[b + 1] <= y) ++b;   // uniform
+    const int l = y - B.cum[b], g = B.row0[b] + l;
+    if (x >= B.W || g < 0 || g >= B.H) return;
+    const size_t srow = (size_t)nframes * B.cum[b] + (size_t)f * B.rows[b] + l;   // row index in src
+    uint32_t *d = frames + (size_t)f * frame_stride + (size_t)g * B.W + x;
+    const int n = min(4, B.W - x);
+    if (B.bpp == 4) {
+        const uint32_t *s4 = (const uint32_t *)src + srow * B.W + x;
+        if (n == 4 && ((uintptr_t)s4 & 15) == 0 && ((uintptr_t)d & 15) == 0) *(uint4 *)d = *(const uint4 *)s4;
+        else for (int k = 0; k < n; ++k) d[k] = s4[k];
+        return;
+    }
+    const uint8_t *s3 = src + (srow * B.W + x) * 3;
+    if (n == 4 && ((uintptr_t)s3 & 3) == 0 && ((uintptr_t)d & 15) == 0) {
+        const uint32_t a = ((const uint32_t *)s3)[0], bb = ((const uint32_t *)s3)[1], c = ((const uint32_t *)s3)[2];
+        *(uint4 *)d = make_uint4(0x80000000u | (a & 0xffffffu), 0x80000000u | (a >> 24) | ((bb & 0xffffu) << 8),
+                                 0x80000000u | (bb >> 16) | ((c & 0xffu) << 16), 0x80000000u | (c >> 8));
+        return;
+    }
+    for (int k = 0; k < n; ++k)
+        d[k] = 0x80000000u | (uint32_t)s3[3 * k] | ((uint32_t)s3[3 * k + 1] << 8) | ((uint32_t)s3[3 * k + 2] << 16);
 }
 
 // Reassemble striped frames after the gather (multi-GPU path): g holds, per
@@ -573,6 +654,25 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
     else
         hipLaunchKernelGGL(rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rt_pack_rgb24(const uint32_t *d_src, size_t n_px, uint8_t *d_dst, hipStream_t st)
+{
+    const size_t groups = (n_px + 3) / 4;
+    if (!groups) return hipSuccess;
+    hipLaunchKernelGGL(rt_pack_rgb24_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, d_src, n_px,
+                       d_dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_rt_assemble(const uint8_t *d_src, const RtBlocks &B, int nframes, uint32_t *d_frames,
+                              size_t frame_stride, hipStream_t st)
+{
+    const int rows = B.cum[B.n];
+    if (rows <= 0 || nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_assemble_kernel, dim3(((B.W + 3) / 4 + 255) / 256, rows, nframes), dim3(256), 0, st, d_src, B,
+                       nframes, d_frames, frame_stride);
     return hipGetLastError();
 }
 

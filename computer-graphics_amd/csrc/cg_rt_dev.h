@@ -768,7 +768,7 @@ __device__ __forceinline__ unsigned long long shadow_mask_of(const RtFrame &F, c
 __device__ __forceinline__ int shard_row(const RtFrame &F, int L)
 {
     int k = L / F.stripe_h;
-    return (k * F.nranks + F.rank) * F.stripe_h + (L - k * F.stripe_h);
+    return F.row0 + (k * F.nranks + F.rank) * F.stripe_h + (L - k * F.stripe_h);
 }
 
 }  // namespace cg

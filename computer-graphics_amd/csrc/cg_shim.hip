@@ -29,6 +29,8 @@ bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vecto
 size_t rt_big_scratch_bytes(const RtFrame &);
 void rt_big_diag(const RtFrame &, void *, hipStream_t);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
+hipError_t launch_rt_pack_rgb24(const uint32_t *, size_t, uint8_t *, hipStream_t);
+hipError_t launch_rt_assemble(const uint8_t *, const RtBlocks &, int, uint32_t *, size_t, hipStream_t);
 hipError_t launch_rt_probe_closest(const RtFrame &, const cg_tri *, const RtSphere *,
                                    const cg_vec4 *, const cg_vec4 *, int, cg_isect *, int *,
                                    hipStream_t);
@@ -299,13 +301,24 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
     F.nbound = c->nbound;
-    cg_rt_shard one{0, 1, kRtTileH};
+    cg_rt_shard one{0, 1, kRtTileH, 0, 0};
     const cg_rt_shard *s = shard ? shard : &one;
-    if (s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0) return CG_E_INVALID;
-    F.rank = s->rank;
-    F.nranks = s->nranks;
-    F.stripe_h = s->stripe_h;
-    F.rows_out = cg_rt_shard_rows(F.H, s);
+    if (s->rows > 0) {   // band: rows row0 .. row0 + rows - 1
+        if (s->row0 < 0) return CG_E_INVALID;
+        F.rank = 0;
+        F.nranks = 1;
+        F.stripe_h = s->rows;
+        F.row0 = s->row0;
+        F.rows_out = s->rows;
+    } else {
+        if (s->rows < 0 || s->nranks < 1 || s->rank < 0 || s->rank >= s->nranks || s->stripe_h <= 0)
+            return CG_E_INVALID;
+        F.rank = s->rank;
+        F.nranks = s->nranks;
+        F.stripe_h = s->stripe_h;
+        F.rows_out = cg_rt_shard_rows(F.H, s);
+    }
+    F.out_fmt = CG_PIX_ARGB8888;
     static int cull = [] {
         const char *e = getenv("CG_RT_CULL");
         return e ? atoi(e) : 2;
@@ -318,15 +331,37 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
 
 extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
 {
-    cg_rt_shard one{0, 1, kRtTileH};
+    cg_rt_shard one{0, 1, kRtTileH, 0, 0};
     const cg_rt_shard *s = shard ? shard : &one;
-    if (height <= 0 || s->nranks < 1 || s->stripe_h <= 0) return CG_E_INVALID;
+    if (height <= 0) return CG_E_INVALID;
+    if (s->rows > 0) return s->rows;
+    if (s->rows < 0 || s->nranks < 1 || s->stripe_h <= 0) return CG_E_INVALID;
     int stripes = (height + s->stripe_h - 1) / s->stripe_h;
     int per = (stripes + s->nranks - 1) / s->nranks;
     return per * s->stripe_h;
 }
 
-static int rt_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
+static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st);
+
+static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t st)
+{
+    // RGB24 output: the lattice kernel stores it directly; the other kernels
+    // render ARGB into the context's scratch frame, then one pack pass
+    RtFrame F = Fin;
+    uint32_t *d_out = (uint32_t *)d_out_v;
+    const bool pack = F.out_fmt == CG_PIX_RGB24 && !rt_use_lattice(F);
+    if (pack) {
+        CG_TRY(c, c->frame.ensure((size_t)F.rows_out * F.W * sizeof(uint32_t)), "alloc frame");
+        d_out = (uint32_t *)c->frame.p;
+        F.out_fmt = CG_PIX_ARGB8888;
+    }
+    int rc = rt_enqueue_kernels(c, F, d_out, st);
+    if (rc || !pack) return rc;
+    CG_TRY(c, launch_rt_pack_rgb24(d_out, (size_t)F.rows_out * F.W, (uint8_t *)d_out_v, st), "pack launch");
+    return CG_OK;
+}
+
+static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
 {
     unsigned long long *lat = nullptr;
     if (rt_use_lattice(F)) {
@@ -366,7 +401,7 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 // Frames f0 .. f0 + nf - 1 of a batch, one prepare + one lattice launch
 // (rt_use_lattice(F) holds for every frame; they differ only in cameraPos).
 static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
-                                    uint32_t *d_out, size_t stride, hipStream_t st)
+                                    void *d_out, size_t stride, hipStream_t st)
 {
     const size_t tiles = rt_lattice_tiles(F);
     CG_TRY(c, c->latmask.ensure((size_t)nf * tiles * sizeof(unsigned long long)), "alloc lattice masks");
@@ -380,16 +415,19 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)c->tc.p,
                                 (RtShade *)c->shade.p, st, &F, lat), "rt_prepare launch");
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
-                                       (const RtSphere *)c->sph.p, lat, fc, nf, stride, d_out, st),
+                                       (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st),
            "rt_lattice launch");
     return CG_OK;
 }
 
+static size_t pix_bytes(int fmt) { return fmt == CG_PIX_RGB24 ? 3 : 4; }
+
 extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int n_lights,
                                           const cg_rt_camera *cams, int n_frames, const cg_rt_shard *shard,
-                                          uint32_t *d_out, size_t frame_stride, void *stream)
+                                          void *d_out, size_t frame_stride, int pix_format, void *stream)
 {
     if (!c || !d_out || n_frames < 0 || (n_frames && !cams)) return CG_E_INVALID;
+    if (pix_format != CG_PIX_ARGB8888 && pix_format != CG_PIX_RGB24) return CG_E_INVALID;
     if (n_frames == 0) return CG_OK;
     for (int f = 1; f < n_frames; ++f)
         if (cams[f].width != cams[0].width || cams[f].height != cams[0].height) return CG_E_INVALID;
@@ -397,9 +435,12 @@ extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int
     RtFrame F;
     int rc = fill_frame(c, lights, n_lights, &cams[0], shard, st, F);
     if (rc) return rc;
+    F.out_fmt = pix_format;
     const size_t px = (size_t)F.rows_out * F.W;
-    const size_t stride = frame_stride ? frame_stride : px;
+    const size_t stride = frame_stride ? frame_stride : px;   // pixels
     if (stride < px) return CG_E_INVALID;
+    uint8_t *out = (uint8_t *)d_out;
+    const size_t fbytes = stride * pix_bytes(pix_format);
     // one batched launch needs the lattice path for every frame, frames that
     // differ only in cameraPos (same focal, R, indirect)
     bool batch = rt_use_lattice(F);
@@ -411,17 +452,47 @@ extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int
             if (f) {
                 rc = fill_frame(c, lights, n_lights, &cams[f], shard, st, F);
                 if (rc) return rc;
+                F.out_fmt = pix_format;
             }
-            rc = rt_enqueue(c, F, d_out + (size_t)f * stride, st);
+            rc = rt_enqueue(c, F, out + (size_t)f * fbytes, st);
             if (rc) return rc;
         }
         return CG_OK;
     }
     for (int f0 = 0; f0 < n_frames; f0 += kMaxFrameBatch) {
         const int nf = std::min(kMaxFrameBatch, n_frames - f0);
-        rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, d_out + (size_t)f0 * stride, stride, st);
+        rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, out + (size_t)f0 * fbytes, stride, st);
         if (rc) return rc;
     }
+    return CG_OK;
+}
+
+extern "C" int cg_rt_assemble_device(cg_ctx *c, const void *d_src, int pix_format, const int *row0,
+                                     const int *rows, int n_blocks, int width, int height, int n_frames,
+                                     uint32_t *d_frames, size_t frame_stride, void *stream)
+{
+    if (!c || !d_src || !d_frames || !row0 || !rows || n_blocks < 1 || n_blocks > kMaxBlocks || width <= 0 ||
+        height <= 0 || n_frames < 1 || n_frames > 65535)
+        return CG_E_INVALID;
+    if (pix_format != CG_PIX_ARGB8888 && pix_format != CG_PIX_RGB24) return CG_E_INVALID;
+    if (frame_stride == 0) frame_stride = (size_t)width * height;
+    if (frame_stride < (size_t)width * height) return CG_E_INVALID;
+    RtBlocks B{};
+    B.n = n_blocks;
+    B.W = width;
+    B.H = height;
+    B.bpp = (int)pix_bytes(pix_format);
+    B.cum[0] = 0;
+    for (int b = 0; b < n_blocks; ++b) {
+        if (rows[b] < 0 || row0[b] < 0) return CG_E_INVALID;
+        B.row0[b] = row0[b];
+        B.rows[b] = rows[b];
+        B.cum[b + 1] = B.cum[b] + rows[b];
+    }
+    if (B.cum[n_blocks] > 65535) return CG_E_INVALID;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    CG_TRY(c, launch_rt_assemble((const uint8_t *)d_src, B, n_frames, d_frames, frame_stride,
+                                 stream ? (hipStream_t)stream : c->stream), "assemble launch");
     return CG_OK;
 }
 
@@ -459,7 +530,7 @@ extern "C" int cg_rt_unstripe_batch_device(cg_ctx *c, const uint32_t *d_gathered
     if (!c || !d_gathered || !d_frames || width <= 0 || height <= 0 || nranks < 1 || stripe_h <= 0 ||
         nframes < 1 || nframes > 65535)
         return CG_E_INVALID;
-    cg_rt_shard s{0, nranks, stripe_h};
+    cg_rt_shard s{0, nranks, stripe_h, 0, 0};
     int rows = cg_rt_shard_rows(height, &s);
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     CG_TRY(c, launch_rt_unstripe(d_gathered, width, height, nranks, stripe_h, rows, nframes, d_frames,

@@ -58,12 +58,22 @@ typedef struct {
     float indirect;        /* indirectLight scale (:110), 0.5 */
 } cg_rt_camera;
 
-/* Row sharding for the multi-GPU path: stripes of `stripe_h` rows are dealt
- * round-robin over `nranks`; this rank renders stripes k with
- * k % nranks == rank, packed in order into its output.  Any stripe_h >= 1 is
- * exact; for speed use a multiple of 15 for the unrotated one-light camera
- * (the lattice kernel's tile height) and of 8 otherwise. */
-typedef struct { int rank, nranks, stripe_h; } cg_rt_shard;
+/* Row sharding for the multi-GPU path.  Stripes (rows == 0): stripes of
+ * `stripe_h` rows are dealt round-robin over `nranks`; this rank renders
+ * stripes k with k % nranks == rank, packed in order into its output.  Any
+ * stripe_h >= 1 is exact; for speed use a multiple of 15 for the unrotated
+ * one-light camera (the lattice kernel's tile height) and of 8 otherwise.
+ * Band (rows > 0): this shard renders frame rows row0 .. row0 + rows - 1
+ * (rows past the frame are padding); rank / nranks / stripe_h are ignored. */
+typedef struct { int rank, nranks, stripe_h; int row0, rows; } cg_rt_shard;
+
+/* Pixel formats of device outputs.  ARGB8888 is PutPixelSDL's uint32
+ * (SDLauxiliary.h:149-161).  RGB24 is its wire form for transfers between
+ * GPUs: the low three bytes (B, G, R) of each pixel, 3 bytes per pixel --
+ * PutPixelSDL's alpha is always 128, so cg_rt_assemble_device restores the
+ * exact uint32. */
+#define CG_PIX_ARGB8888 0
+#define CG_PIX_RGB24 1
 
 /* rasteriser/Source/TestModelH.h:13-42 `Triangle` (84 B). */
 typedef struct { cg_vec4 v0, v1, v2, normal; cg_vec3 color; int texture; int index; } cg_rtri;
@@ -136,14 +146,24 @@ int cg_rt_render_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const
 /* n_frames successive frames (the reference's main loop: Update() moves the
  * camera, Draw() renders, raytracer/Source/skeleton.cpp:91-94 + :104-169),
  * frame f with camera cams[f] into d_out + f * frame_stride pixels
- * (frame_stride 0 = cg_rt_shard_rows() * W).  All cameras share width and
- * height; lights and the shard are common.  Frames of the unrotated one-light
- * camera that differ only in cameraPos are rendered up to 16 per kernel
- * launch (a whole GPU's worth of tiles even for a small shard); others are
- * enqueued one by one.  Each frame equals cg_rt_render_device's. */
+ * (frame_stride 0 = cg_rt_shard_rows() * W) in pix_format (CG_PIX_*; for
+ * RGB24, d_out is a byte buffer and pixel offsets count 3 bytes).  All
+ * cameras share width and height; lights and the shard are common.  Frames of
+ * the unrotated one-light camera that differ only in cameraPos are rendered up
+ * to 16 per kernel launch (a whole GPU's worth of tiles even for a small
+ * shard); others are enqueued one by one.  Each frame equals
+ * cg_rt_render_device's. */
 int cg_rt_render_frames_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
-                               int n_frames, const cg_rt_shard *shard, uint32_t *d_out, size_t frame_stride,
-                               void *stream);
+                               int n_frames, const cg_rt_shard *shard, void *d_out, size_t frame_stride,
+                               int pix_format, void *stream);
+/* Frame assembly after a transfer of band shards: d_src holds n_blocks row
+ * blocks in order, block b = n_frames x rows[b] rows of `width` pixels in
+ * pix_format, landing at frame rows row0[b] .. row0[b] + rows[b] - 1 (rows
+ * outside the frame are skipped) of frame f = d_frames + f * frame_stride
+ * pixels (ARGB8888).  row0 / rows are host arrays, n_blocks <= 64. */
+int cg_rt_assemble_device(cg_ctx *ctx, const void *d_src, int pix_format, const int *row0, const int *rows,
+                          int n_blocks, int width, int height, int n_frames, uint32_t *d_frames,
+                          size_t frame_stride, void *stream);
 /* Rows a shard renders (including padding rows of its last stripe). */
 int cg_rt_shard_rows(int height, const cg_rt_shard *shard);
 /* Reassemble a frame from gathered shards: d_gathered holds nranks blocks of

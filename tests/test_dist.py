@@ -76,3 +76,83 @@ def test_row_maps_partition_the_frame(S):
             assert max(sizes) - min(sizes) <= S
     # C2 at 8 GPUs: 15-row stripes split 1080 rows exactly (9 stripes per rank)
     assert cgdist.shard_rows(1080, 8, cgdist.LATTICE_STRIPE) * 8 == 1080
+
+
+# ---- balanced bands (bench.py's default N > 1 layout) ------------------------
+
+def _band_worker(rank, world, port, q):
+    """Rank r renders its band (oracle), ranks > 0 send it as RGB24 with gloo
+    p2p, rank 0 assembles: == the single-process frame.  Bands come from a
+    rebalance of skewed timings, so they are uneven."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "computer-graphics_amd"), os.path.join(root, "oracle")]
+    import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = oracle.rt_draw(oracle.rt_params(W, H, F)).reshape(H, W)
+        bands = cgdist.rebalance(cgdist.equal_bands(H, world), [1.0 + 0.7 * r for r in range(world)],
+                                 [0.3] + [0.0] * (world - 1), H)
+        r0, nr = bands[rank]
+        mine = full[r0:r0 + nr].reshape(-1)
+        if rank == 0:
+            frames = np.zeros((1, H * W), np.uint32)
+            frames[0, r0 * W:(r0 + nr) * W] = mine
+            parts = []
+            for p in range(1, world):
+                buf = torch.empty(bands[p][1] * W * 3, dtype=torch.uint8)
+                dist.recv(buf, src=p)
+                parts.append(buf.numpy())
+            cgdist.assemble_np(np.concatenate(parts), 3, bands[1:], W, H, 1, frames)
+            q.put(bool(np.array_equal(frames[0], full.reshape(-1))))
+        else:
+            dist.send(torch.from_numpy(cgdist.pack_rgb24_np(mine)), dst=0)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_band_p2p_rgb24_assemble_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+        assert pr.exitcode == 0
+    assert q.get(timeout=5) is True
+
+
+def test_band_partition_properties():
+    rng = np.random.default_rng(3)
+    for H_ in (7, 64, 1080, 2160):
+        for n in (1, 2, 3, 8):
+            for cost in (np.ones(H_), rng.random(H_) + 0.1, np.linspace(1, 5, H_)):
+                o = rng.random(n) * cost.sum() / n * 0.2
+                bands = cgdist.band_partition(cost, n, o)
+                # contiguous, rank-ordered, covering every row exactly once
+                assert bands[0][0] == 0 and sum(nr for _, nr in bands) == H_
+                for (a, na), (b, _) in zip(bands, bands[1:]):
+                    assert a + na == b
+                if H_ >= n:
+                    assert all(nr >= 1 for _, nr in bands)
+                # makespan within one row's cost of the continuous optimum's lower bound
+                span = max(cost[a:a + na].sum() + o[r] for r, (a, na) in enumerate(bands))
+                lb = max((cost.sum() + o.sum()) / n, o.max())
+                assert span <= lb + cost.max() * 1.0001 + 1e-9
+    # equal_bands: tile-aligned boundaries (C2 at 8 GPUs: 135 = 9 lattice tiles)
+    assert cgdist.equal_bands(1080, 8, 15) == [(135 * r, 135) for r in range(8)]
+
+
+def test_rgb24_pack_assemble_roundtrip():
+    rng = np.random.default_rng(5)
+    Wd, Hd, nf = 24, 10, 3
+    frames_ref = (0x80000000 | rng.integers(0, 1 << 24, (nf, Hd * Wd), dtype=np.uint32)).astype(np.uint32)
+    bands = [(0, 3), (3, 4), (7, 3)]
+    src = np.concatenate([cgdist.pack_rgb24_np(frames_ref[f, a * Wd:(a + n) * Wd])
+                          for a, n in bands for f in range(nf)])
+    got = cgdist.assemble_np(src, 3, bands, Wd, Hd, nf, np.zeros_like(frames_ref))
+    assert np.array_equal(got, frames_ref)

@@ -169,6 +169,73 @@ def test_rt_render_frames_batched(rt, golden):
             assert np.array_equal(frame, singles[k]), (S, n, k)
 
 
+@pytest.mark.parametrize("kind", ["lattice", "yaw", "c4"])
+def test_rt_bands_rgb24_assemble(rt, kind):
+    """bench.py's N > 1 layout on one GPU: uneven bands, rank 0's band rendered
+    ARGB straight into the frames, the others in the RGB24 wire format into
+    one buffer, cg_rt_assemble_device expands them: == each frame whole."""
+    torch = pytest.importorskip("torch")
+    W, H = 320, 256
+    if kind == "lattice":   # batched lattice launches, RGB24 stored by the kernel
+        cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, z, 1.0)) for z in (-3.0, -2.95, -2.8)]
+        lights = cgamd.default_lights()
+    elif kind == "yaw":     # general kernel, one frame at a time + pack pass
+        cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, -3.0, 1.0), cgamd.yaw_matrix(y)) for y in (0.05, -0.1)]
+        lights = cgamd.default_lights()
+    else:                   # light set (general kernel)
+        cams = [cgamd.rt_camera(W, H, 256.0)]
+        lights = cgamd.area_lights(None, 0.1, 3)
+    singles = [rt.rt_render(c, lights)[0] for c in cams]
+    K = len(cams)
+    bands = cgdist.rebalance(cgdist.equal_bands(H, 4), [1.0, 2.5, 1.2, 0.6], [0.4, 0, 0, 0], H)
+    assert len({nr for _, nr in bands}) > 1          # uneven
+    st = torch.cuda.Stream()
+    frames = torch.zeros(K * H * W, dtype=torch.int32, device="cuda")
+    r0, nr = bands[0]
+    rt.rt_render_frames_device(cams, frames.data_ptr() + 4 * r0 * W, cgamd.RtShard(row0=r0, rows=nr),
+                               st.cuda_stream, lights, frame_stride=H * W)
+    rbuf = torch.zeros(K * H * W * 3 + 64, dtype=torch.uint8, device="cuda")
+    off = 0
+    for a, n in bands[1:]:
+        rt.rt_render_frames_device(cams, rbuf.data_ptr() + off, cgamd.RtShard(row0=a, rows=n), st.cuda_stream,
+                                   lights, pix_format=cgamd.PIX_RGB24)
+        off += K * n * W * 3
+    rt.rt_assemble_device(rbuf.data_ptr(), cgamd.PIX_RGB24, [a for a, _ in bands[1:]], [n for _, n in bands[1:]],
+                          W, H, K, frames.data_ptr(), 0, st.cuda_stream)
+    st.synchronize()
+    got = frames.cpu().numpy().view(np.uint32).reshape(K, -1)
+    for k in range(K):
+        assert np.array_equal(got[k], singles[k]), (kind, k)
+    # the wire bytes are exactly the low three bytes of each pixel
+    a, n = bands[1]
+    wire = rbuf[:K * n * W * 3].cpu().numpy()
+    want = np.concatenate([cgdist.pack_rgb24_np(s_[a * W:(a + n) * W]) for s_ in singles])
+    assert np.array_equal(wire, want)
+
+
+def test_rt_assemble_argb_and_ragged(rt):
+    """cg_rt_assemble_device with ARGB blocks, a width that is not a multiple of
+    4 and a block running past the frame's last row."""
+    torch = pytest.importorskip("torch")
+    W, H = 37, 11
+    rng = np.random.default_rng(9)
+    ref = (0x80000000 | rng.integers(0, 1 << 24, H * W, dtype=np.uint32)).astype(np.uint32)
+    bands = [(0, 4), (4, 5), (9, 4)]                 # last block: rows 9..12, 11.. are padding
+    for fmt, bpp in ((cgamd.PIX_ARGB8888, 4), (cgamd.PIX_RGB24, 3)):
+        blocks = []
+        for a, n in bands:
+            blk = np.zeros(n * W, np.uint32)
+            m = min(n, H - a)
+            blk[:m * W] = ref[a * W:(a + m) * W]
+            blocks.append(blk.view(np.uint8) if bpp == 4 else cgdist.pack_rgb24_np(blk))
+        src = torch.from_numpy(np.concatenate(blocks)).cuda()
+        out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        rt.rt_assemble_device(src.data_ptr(), fmt, [a for a, _ in bands], [n for _, n in bands], W, H, 1,
+                              out.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), fmt
+
+
 def test_rt_render_frames_fallback(rt):
     """Frames that cannot share a launch (yaw-rotated R, two lights) go one by one."""
     torch = pytest.importorskip("torch")
