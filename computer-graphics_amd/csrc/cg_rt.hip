@@ -10,6 +10,8 @@
 #include <float.h>
 #include <stdlib.h>
 
+#include <vector>
+
 #include "cg_rt_dev.h"
 
 namespace cg {
@@ -61,9 +63,14 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
 // blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
 // out + frame * n, its masks at lat_masks + frame * tiles).
+// Per tile it stores two masks: [0] the primary certificate (bit 63: a
+// sphere may be hit), [1] the shadow certificate for every hit the tile's
+// rays can produce (primary_hit_box / sphere_hit_box), so the lattice kernel
+// needs no certificate pass of its own.
 __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
                                   RtTri *__restrict__ out, RtShade *__restrict__ shade, int n_prep_blocks,
-                                  RtFrame F, unsigned long long *__restrict__ lat_masks)
+                                  RtFrame F, const RtSphere *__restrict__ sph,
+                                  unsigned long long *__restrict__ lat_masks)
 {
     const int frame = blockIdx.y;
     const float cx = cams.c[frame][0], cy = cams.c[frame][1], cz = cams.c[frame][2], cw = cams.c[frame][3];
@@ -83,19 +90,40 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW;
     const int tiles = tiles_x * ((F.rows_out + kLatTileH - 1) / kLatTileH);
-    lat_masks += (size_t)frame * tiles;
+    lat_masks += (size_t)frame * tiles * 2;
     const int tile = ((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave;
     if (tile >= tiles) return;   // whole wave
     const LatTile G = lat_tile(F, tile % tiles_x, tile / tiles_x);
-    bool keep = false;
+    const float camf[4] = {cx, cy, cz, cw};
+    const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
+    const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
+    bool keep = false, sphere = false;
+    RtTri c{};
+    LanePosBox pb;   // this lane's share of the tile's possible hit positions
+    pb.init();
     if (G.rows > 0 && lane < n) {
-        const RtTri c = rt_tri_const(tris[lane], cx, cy, cz, cw);
-        const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
-        const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
-        keep = !cull_primary(c, x0, x1, y0, y1, F.focal);
+        c = rt_tri_const(tris[lane], cx, cy, cz, cw);
+        PrimDet pd;
+        keep = !cull_primary(c, x0, x1, y0, y1, F.focal, &pd);
+        if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi))
+            for (int k = 0; k < 3; ++k) {
+                pb.lo[k] = -INFINITY;
+                pb.hi[k] = INFINITY;
+            }
     }
-    const unsigned long long m = __ballot(keep);
-    if (lane == 0) lat_masks[tile] = m;
+    if (G.rows > 0 && lane == 63)   // spheres (lattice scenes have n <= 63 triangles)
+        for (int q = 0; q < F.n_sph; ++q)
+            if (!sphere_surely_missed(sph[q], camf, x0, x1, y0, y1, F.focal)) {
+                sphere = true;
+                sphere_hit_box(sph[q], camf, pb.lo, pb.hi);
+            }
+    const unsigned long long m = __ballot(keep) | (__ballot(sphere) ? (1ull << 63) : 0ull);
+    unsigned long long sm = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
+    if (F.cull_shadow && F.n_lights > 0) sm = shadow_mask_lane(F, c, shadow_box_of_positions(F, pb), lane);
+    if (lane == 0) {
+        lat_masks[2 * tile] = m;
+        lat_masks[2 * tile + 1] = sm;
+    }
 }
 
 
@@ -242,8 +270,21 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 #ifndef CG_RT_LAT_PAIR
 #define CG_RT_LAT_PAIR 1   // pass 1 traces two lattice points per lane per step
 #endif
-#ifndef CG_RT_LAT_WGCERT
-#define CG_RT_LAT_WGCERT 1   // 1: one shadow certificate per tile (wave 0); 0: one per wave
+// Phase timing of the lattice kernel (diagnostic builds only: -DCG_RT_LAT_STAMPS):
+// per wave, s_memtime deltas accumulated into cg_lat_stamps[phase].
+#ifdef CG_RT_LAT_STAMPS
+constexpr int kStampWaves = 16 * 8640 * 4;   // one 16-frame 1080p batch
+__device__ unsigned int cg_lat_stamps[kStampWaves][6];
+#define LAT_STAMP(ph)                                                                  \
+    do {                                                                               \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                  \
+        stamps_[ph] = (unsigned int)(now_ - stamp_);                                   \
+        stamp_ = now_;                                                                 \
+    } while (0)
+#else
+#define LAT_STAMP(ph) \
+    do {              \
+    } while (0)
 #endif
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
@@ -263,7 +304,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 #pragma unroll
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
     tc += (size_t)frame * F.n_tris;
-    lat_masks += (size_t)frame * gridDim.x * gridDim.y;
+    lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
     uint8_t *out8 = (uint8_t *)out + (size_t)frame * out_stride * 3;   // CG_PIX_RGB24
     out += (size_t)frame * out_stride;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -278,11 +319,20 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     // cols exist only in tiles cut by the right edge); wave w takes the w-th quarter
     const int npts = kLatW * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
-    // the tile's primary certificate (rt_prepare_kernel)
-    const unsigned long long mask = lat_masks[blockIdx.y * gridDim.x + blockIdx.x];
+    // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
+    // sphere may be hit) and shadow mask for every hit the tile can produce
+#ifdef CG_RT_LAT_STAMPS
+    unsigned long long stamp_ = __builtin_amdgcn_s_memtime();
+    unsigned int stamps_[6] = {0, 0, 0, 0, 0, 0};
+#endif
+    const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
+    const unsigned long long smask = uniform_u64(lat_masks[2 * tix + 1]);
+    const unsigned long long mask = m0 & ~(1ull << 63);
+    RtFrame Fp = F;                        // pass 1: spheres only where one may be hit
+    if (!(m0 >> 63)) Fp.n_sph = 0;
+    __syncthreads();                       // s_shade
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
-    LanePosBox pb;
-    pb.init();
 #if CG_RT_LAT_PAIR
     // two points per lane per step (p and p + 64): one triangle load for both rays
     for (int p0 = p_lo; p0 < p_hi; p0 += 128) {
@@ -300,14 +350,12 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         }
         int bi[2];
         float t[2];
-        closest_primary_n<2>(F, tc, sph, X, Y, live, mask, bi, t);                         // :140
+        closest_primary_n<2>(Fp, tc, sph, X, Y, live, mask, bi, t);                        // :140
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
             if (!live[n]) continue;
             s_bi[pp[n]] = bi[n];
             s_r[pp[n]] = t[n];
-            if (bi[n] != INT_MIN)
-                pb.add(v3(F.cam[0] + t[n] * X[n], F.cam[1] + t[n] * Y[n], F.cam[2] + t[n] * F.focal));   // :326/:345
         }
     }
 #else
@@ -317,47 +365,15 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         if (p < p_hi && cx < cols) {
             const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
             float t;
-            const int bi = closest_primary<true>(F, tc, sph, v3(X, Y, F.focal), t, mask);
+            const int bi = closest_primary<true>(Fp, tc, sph, v3(X, Y, F.focal), t, mask);
             s_bi[idx] = bi;
             s_r[idx] = t;
-            if (bi != INT_MIN) pb.add(v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal));   // :326/:345
         }
     }
 #endif
-    unsigned long long smask = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
-#if CG_RT_LAT_WGCERT
-    if (F.cull_shadow) {   // one shadow certificate for the tile's hits, by wave 0
-        __shared__ float s_pbox[4][6];
-        __shared__ unsigned long long s_mask;
-        float lo[3], hi[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            lo[c] = wave_min(pb.lo[c]);
-            hi[c] = wave_max(pb.hi[c]);
-        }
-        if (lane == 0)
-            for (int c = 0; c < 3; ++c) {
-                s_pbox[wave][c] = lo[c];
-                s_pbox[wave][3 + c] = hi[c];
-            }
-        __syncthreads();
-        if (wave == 0) {
-            LanePosBox tb;   // the tile's box, the same in every lane
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                tb.lo[c] = fminf(fminf(s_pbox[0][c], s_pbox[1][c]), fminf(s_pbox[2][c], s_pbox[3][c]));
-                tb.hi[c] = fmaxf(fmaxf(s_pbox[0][3 + c], s_pbox[1][3 + c]), fmaxf(s_pbox[2][3 + c], s_pbox[3][3 + c]));
-            }
-            const unsigned long long m = shadow_mask_box(F, tc, shadow_box_of_positions(F, tb), lane);
-            if (lane == 0) s_mask = m;
-        }
-        __syncthreads();
-        smask = uniform_u64(s_mask);
-    }
-#else
-    if (F.cull_shadow) smask = shadow_mask_box(F, tc, shadow_box_of_positions(F, pb), lane);
-#endif
-    // Pass 2: DirectLight of each lattice ray that hit (:151-153)
+    LAT_STAMP(0);   // pass 1
+    // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
+    // attributes from the LDS copy
 #ifdef CG_ABLATE_SHADE
     if (smask == 12345ull)
 #endif
@@ -370,14 +386,16 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
                 const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
                 const float t = s_r[idx];
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                const vec3 dl = direct_light<true>(F, tc, shade, sph, bi, pos, object_colour(shade, sph, bi), 0, smask);
+                const vec3 dl = direct_light<true>(F, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
                 s_r[idx] = dl.x;
                 s_g[idx] = dl.y;
                 s_b[idx] = dl.z;
             }
         }
     }
+    LAT_STAMP(3);   // pass 2
     __syncthreads();
+    LAT_STAMP(4);   // pass-2 barrier
     // Pixels: the nine contributions in the reference's order (:134-166)
     const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
     const bool have = tx < nu && ty < nv;
@@ -423,6 +441,15 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             q[2] = (uint8_t)(px >> 16);
         }
     }
+    LAT_STAMP(5);   // pixels + stores
+#ifdef CG_RT_LAT_STAMPS
+    const size_t wid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave;
+    if (lane < 6 && wid < (size_t)kStampWaves) {
+        unsigned int v = 0;
+        for (int k = 0; k < 6; ++k) v = lane == k ? stamps_[k] : v;
+        cg_lat_stamps[wid][lane] = v;
+    }
+#endif
 }
 
 // ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): four
@@ -580,7 +607,7 @@ __global__ void rt_probe_direct_light_kernel(RtFrame F, const RtTri *__restrict_
 // ---------------------------------------------------------------------------
 // Launch helpers (called by the shim).
 hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
-                             RtShade *d_shade, hipStream_t st, const RtFrame *F,
+                             RtShade *d_shade, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
                              unsigned long long *d_lat_masks)
 {
     if (n <= 0) return hipSuccess;
@@ -593,7 +620,7 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         cert = (tiles + threads / 64 - 1) / (threads / 64);
     }
     hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
-                       d_tc, d_shade, prep, Fl, d_lat_masks);
+                       d_tc, d_shade, prep, Fl, d_sph, d_lat_masks);
     return hipGetLastError();
 }
 
@@ -618,7 +645,7 @@ bool rt_use_lattice(const RtFrame &F)
         const char *e = getenv("CG_RT_LATTICE");
         return !e || atoi(e) != 0;
     }();
-    return lattice_on && F.n_tris > 0 && F.n_tris <= 64 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
+    return lattice_on && F.n_tris > 0 && F.n_tris <= 63 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
 }
 
 size_t rt_lattice_tiles(const RtFrame &F)
@@ -655,6 +682,24 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         hipLaunchKernelGGL(rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     return hipGetLastError();
+}
+
+// Diagnostic builds: read and clear the lattice phase stamps (cycles summed over waves).
+bool rt_lat_stamps(unsigned long long out[8], hipStream_t st)
+{
+#ifdef CG_RT_LAT_STAMPS
+    if (hipStreamSynchronize(st) != hipSuccess) return false;
+    std::vector<unsigned int> v((size_t)kStampWaves * 6);
+    if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(cg_lat_stamps), v.size() * 4) != hipSuccess) return false;
+    for (int k = 0; k < 8; ++k) out[k] = 0;
+    for (size_t w = 0; w < (size_t)kStampWaves; ++w)
+        for (int k = 0; k < 6; ++k) out[k] += v[w * 6 + k];
+    return true;
+#else
+    (void)out;
+    (void)st;
+    return false;
+#endif
 }
 
 hipError_t launch_rt_pack_rgb24(const uint32_t *d_src, size_t n_px, uint8_t *d_dst, hipStream_t st)

@@ -154,7 +154,13 @@ __device__ __forceinline__ bool uv_sum_reject(int sg, double blo, double bhi, do
     return num > 0.0 && num * dmin > (4.0 * eps) * (X + dmin) * dmax * (1.0 + 0x1p-40);
 }
 
-__device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f)
+// The float det's range over a bundle (cull_primary): [dlo - Ed, dhi + Ed].
+struct PrimDet {
+    double dlo, dhi, Ed;
+};
+
+__device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f,
+                                    PrimDet *pd = nullptr)
 {
     const double eps = 5.9604644775390625e-8;   // 2^-24
     const double g = 16.0 * eps;
@@ -179,6 +185,7 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
     double Eu = g * det3_bound(Dx, Dy, Dz, s, e2) + 1e-12 * (fabs(ulo) + fabs(uhi));
     double Ev = g * det3_bound(Dx, Dy, Dz, e1, s) + 1e-12 * (fabs(vlo) + fabs(vhi));
     double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
+    if (pd) *pd = PrimDet{dlo, dhi, Ed};
     if (!(isfinite(dlo) && isfinite(dhi) && isfinite(Ed + Eu + Ev + Eb) && isfinite(ulo + uhi + vlo + vhi + blo + bhi)))
         return false;
     int sg;
@@ -201,6 +208,91 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
                       dmin, dmax))
         return true;
     return false;
+}
+
+// Box of the positions (:326) of every hit a triangle can give to the camera
+// rays d = (x, y, f), x in [x0, x1], y in [y0, y1] (cull_primary's bundle),
+// from the float det's range pd: t = fl(detT / det) lies in
+// [|detT| / dmax, |detT| / dmin] (widened by 2^-20; accepted hits have t >= 0
+// and t of det's sign) when det's sign is certain, and position = fl(cam +
+// fl(t d)) is widened by 2^-20 (|cam| + |t d|) per component for its two
+// roundings.  Returns false (unbounded) when det's sign is uncertain.
+__device__ static bool primary_hit_box(const RtTri &c, const PrimDet &pd, const float cam[4], float x0, float x1,
+                                       float y0, float y1, float f, float lo[3], float hi[3])
+{
+    double dmin, dmax;
+    if (pd.dlo - pd.Ed > 0) {
+        dmin = pd.dlo - pd.Ed;
+        dmax = pd.dhi + pd.Ed;
+    } else if (pd.dhi + pd.Ed < 0) {
+        dmin = -(pd.dhi + pd.Ed);
+        dmax = -(pd.dlo - pd.Ed);
+    } else {
+        return false;
+    }
+    const double aT = fabs((double)c.detT);
+    double tlo = aT / dmax * (1.0 - 0x1p-20);
+    const double thi = aT / dmin * (1.0 + 0x1p-20);
+    if (tlo < 0x1p-100) tlo = 0.0;   // t may round to 0: the box then contains cam
+    if (!(isfinite(thi) && thi < 1e30)) return false;
+    const double dl[3] = {(double)x0, (double)y0, (double)f}, dh[3] = {(double)x1, (double)y1, (double)f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double a = tlo * dl[k], b = tlo * dh[k], e = thi * dl[k], g = thi * dh[k];
+        const double mn = fmin(fmin(a, b), fmin(e, g)), mx = fmax(fmax(a, b), fmax(e, g));
+        const double w = 0x1p-20 * (fabs((double)cam[k]) + fmax(fabs(mn), fabs(mx))) + 1e-30;
+        lo[k] = (float)((cam[k] + mn) - w);
+        hi[k] = (float)((cam[k] + mx) + w);
+    }
+    return true;
+}
+
+// Sphere::intersect (TestModelH.h:43-66) certainly misses every camera ray of
+// the bundle: the float discriminant (:27) is negative.  With L = cam - centre,
+// a = d.d, b = 2 d.L and c_f = fl(L.L - r^2) > 0 (camera outside), the float
+// evaluation of b^2 - 4 a c_f is < 0 when (max|d.L| + 4 eps sum|d_i L_i|)^2 <
+// min(d.d) c_f (1 - 2^-18): a_f >= d.d (1 - 3 eps), |b_f| <= 2 (|d.L| + 3 eps
+// sum|d_i L_i|)(1 + eps), and the three rounded products / difference cost
+// < 2^-18 relative.  max |d.L| over the box is at a corner; min d.d at the
+// point of the box nearest the origin.
+__device__ static bool sphere_surely_missed(const RtSphere &S, const float cam[4], float x0, float x1, float y0,
+                                            float y1, float f)
+{
+    const vec3 L = v3(cam[0], cam[1], cam[2]) - v3(S.cx, S.cy, S.cz);   // :48 (float, as the kernels form it)
+    const float cf = dot(L, L) - S.r2;                                   // :51
+    if (!(cf > 0.0f)) return false;
+    double mdl = 0.0, msum = 0.0;
+    const double xs[2] = {(double)x0, (double)x1}, ys[2] = {(double)y0, (double)y1};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const double dL = xs[i] * L.x + ys[j] * L.y + (double)f * L.z;
+            mdl = fmax(mdl, fabs(dL));
+            msum = fmax(msum, fabs(xs[i] * L.x) + fabs(ys[j] * L.y) + fabs((double)f * L.z));
+        }
+    const double nx = x0 > 0 ? (double)x0 : (x1 < 0 ? (double)x1 : 0.0);
+    const double ny = y0 > 0 ? (double)y0 : (y1 < 0 ? (double)y1 : 0.0);
+    const double dd = nx * nx + ny * ny + (double)f * f;
+    const double U = mdl * (1.0 + 1e-12) + 4.0 * 5.9604644775390625e-8 * msum;
+    return isfinite(U) && U * U < dd * (double)cf * (1.0 - 0x1p-18);
+}
+
+// Box of the positions of sphere hits (:345): a hit's float t carries an
+// absolute error below sqrt(20 eps) |L| / |d| near tangency (the root of a
+// discriminant perturbed by ~10 eps b^2), so the float position lies within
+// 1.1e-3 |L| of the sphere; the box is widened by 4e-3 |L|.
+__device__ static void sphere_hit_box(const RtSphere &S, const float cam[4], float lo[3], float hi[3])
+{
+    const double Lx = (double)cam[0] - S.cx, Ly = (double)cam[1] - S.cy, Lz = (double)cam[2] - S.cz;
+    const double w = sqrt((double)S.r2) * (1.0 + 1e-6) + 4e-3 * sqrt(Lx * Lx + Ly * Ly + Lz * Lz) + 1e-6;
+    const double C[3] = {(double)S.cx, (double)S.cy, (double)S.cz};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double m = 0x1p-20 * (fabs(C[k]) + w + fabs((double)cam[k]));
+        lo[k] = fminf(lo[k], (float)(C[k] - w - m));
+        hi[k] = fmaxf(hi[k], (float)(C[k] + w + m));
+    }
 }
 
 // Wave-wide min / max (ds_bpermute butterflies; a DPP row version measured
@@ -340,6 +432,111 @@ __device__ __forceinline__ bool surely_beyond(float detT, float det, float len, 
     return rhs <= FLT_MAX && rhs >= 0x1p-100f && fabsf(detT) * len >= rhs;
 }
 
+// Divide-free decisions of the reference's quotient tests.  ClosestIntersection
+// (skeleton.cpp:306-335) forms t = detT/det, u = detU/det, v = detV/det with
+// IEEE divides, but only the comparisons of their rounded values decide
+// anything except the accepted hit's t.  Each function below returns 1 / 0
+// when the comparison's outcome is certain from the operands' magnitudes
+// (rounding errors bounded, margins 2^-18 against at most a few 2^-24
+// relative errors) and -1 otherwise; a -1 sends the caller down the
+// reference's own divide path, so results are bit-identical either way.
+// Domain of the fast paths: finite operands with 2^-20 <= |det| <= 2^40,
+// |detT|, |detU|, |detV| <= 2^40, 2^-20 <= len <= 2^20 -- the quotients and
+// distances then stay in the normal range (no underflow, no overflow);
+// anything else (NaN, det = 0, extreme scales) is undecided.
+#ifndef CG_RT_PREFETCH
+#define CG_RT_PREFETCH 0
+#endif
+#ifndef CG_RT_DIVFREE
+#define CG_RT_DIVFREE 0   // 1: bit-exact too, but measured slower (C2 85.6 -> 98 us/frame, C4 20 -> 25 ms)
+#endif
+__device__ __forceinline__ bool fsign(float x) { return (__float_as_uint(x) >> 31) != 0u; }
+
+// distance = fl(fl(detT/det) * len) against the reference's tests
+// `distance < 0` (:311) and `distance >= bound || distance > FLT_MAX`
+// (:313 with bound = the running best; :395 with bound = r_magnitude):
+// 1 = passes both (0 <= distance < bound), 0 = fails one, -1 undecided.
+//  * t < 0 certain: signs differ, detT != 0 and |detT| >= 2^-80 |det|, so
+//    |t| >= 2^-80 and |distance| >= 2^-100: strictly negative (no -0).
+//  * detT = +-0 or same signs: t >= 0 or t = -0; distance is then >= 0 or -0,
+//    and `-0 < 0` is false, so the first test passes.
+//  * X = fl(|detT| len), Y = fl(|det| bound): X <= fl(Y (1 - 2^-18)) gives
+//    t len <= bound (1 - 2^-18)(1 + 2^-24)^3 < bound (1 - 2^-19), so the
+//    rounded distance (two more roundings) is < bound; X >= fl(Y (1 + 2^-18))
+//    gives t len > bound (1 + 2^-19) and a rounded distance >= bound.
+//    bound > 2^100 is beyond any distance of the domain (< 2^81).
+__device__ __forceinline__ int t_decide(float detT, float det, float len, float bound)
+{
+    const float ad = fabsf(det), at = fabsf(detT);
+    if (!(ad >= 0x1p-20f && ad <= 0x1p40f && at <= 0x1p40f && len >= 0x1p-20f && len <= 0x1p20f &&
+          bound >= 0x1p-20f))
+        return -1;   // also NaN / inf operands
+    if (detT != 0.0f && fsign(detT) != fsign(det)) return at >= ad * 0x1p-80f ? 0 : -1;
+    if (bound > 0x1p100f) return 1;
+    const float X = at * len, Y = ad * bound;
+    if (X <= Y * (1.0f - 0x1p-18f)) return 1;
+    if (X >= Y * (1.0f + 0x1p-18f)) return 0;
+    return -1;
+}
+
+// (u >= 0) && (v >= 0) && ((u + v) <= 1) with u = fl(detU/det), v = fl(detV/det)
+// (:328-335): 1 accept, 0 reject, -1 undecided.
+//  * u < 0 certain: signs of detU and det differ, detU != 0, |detU| >= 2^-80 |det|
+//    (|u| >= 2^-80: no rounding to -0).  u >= 0 certain: detU = +-0 or same signs.
+//  * both >= 0: u + v = (|detU| + |detV|) / |det| exactly; P = fl(|detU| + |detV|)
+//    <= fl(|det| (1 - 2^-18)) gives u + v < 1 - 2^-20, so fl(fl(u) + fl(v)) <= 1;
+//    P >= fl(|det| (1 + 2^-18)) gives u + v > 1 + 2^-20 and a rounded sum > 1.
+__device__ __forceinline__ int uv_decide(float det, float detU, float detV)
+{
+    const float ad = fabsf(det), au = fabsf(detU), av = fabsf(detV);
+    if (!(ad >= 0x1p-20f && ad <= 0x1p40f && au <= 0x1p40f && av <= 0x1p40f)) return -1;
+    const bool sd = fsign(det);
+    const float tiny = ad * 0x1p-80f;
+    const bool uneg = detU != 0.0f && fsign(detU) != sd, vneg = detV != 0.0f && fsign(detV) != sd;
+    if ((uneg && au >= tiny) || (vneg && av >= tiny)) return 0;
+    if (uneg || vneg) return -1;
+    const float P = au + av;
+    if (P <= ad * (1.0f - 0x1p-18f)) return 1;
+    if (P >= ad * (1.0f + 0x1p-18f)) return 0;
+    return -1;
+}
+
+// One triangle of ClosestIntersection (:306-335): whether it becomes the new
+// closest hit, given det, detT, |d| and the running best; uvf(detU, detV)
+// supplies the u / v numerators.  On acceptance t and distance are the
+// reference's rounded values (one IEEE divide).  Rejections are decided
+// divide-free whenever t_decide / uv_decide are certain.
+template <class UV>
+__device__ __forceinline__ bool tri_accept(float detT, float det, float len, float best, UV uvf, float &t_out,
+                                           float &dist_out)
+{
+    const float bound = FLT_MAX;
+    float detU, detV;
+#if CG_RT_DIVFREE
+    const int td = t_decide(detT, det, len, best);
+    if (td == 0) return false;
+    uvf(detU, detV);
+    const int ud = td == 1 ? uv_decide(det, detU, detV) : -1;
+    if (ud == 0) return false;
+#endif
+    const float t = detT / det;                               // :306
+    const float distance = t * len;                           // :307
+    if (distance < 0.0f) return false;                        // :311
+    if (distance >= best || distance > bound) return false;   // :313
+#if CG_RT_DIVFREE
+    if (ud < 0)
+#else
+    uvf(detU, detV);
+#endif
+    {
+        const float u = detU / det, v = detV / det;           // :317-321
+        if (!((u >= 0) && (v >= 0) && ((u + v) <= 1))) return false;   // :328-335
+    }
+    t_out = t;
+    dist_out = distance;
+    return true;
+}
+
 // ClosestIntersection for camera-origin rays (skeleton.cpp:263-363).
 // Returns best index: >= 0 triangle, -1 - k sphere k, INT_MIN no hit; t out.
 // Triangles are visited in index order; with CULL only those whose bit is set
@@ -365,16 +562,13 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
         float Q2 = nd.y * c.e2z - c.e2y * nd.z;
         float Q1 = nd.y * c.e1z - c.e1y * nd.z;
         float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;  // det(-d, e1, e2) :289
-        float t = c.detT / det;                               // :306
-        float distance = t * len;                             // :307
-        if (distance < 0.0f) continue;                        // :311
-        if (distance >= best || distance > bound) continue;   // :313
-        float Q3 = nd.y * c.sz - c.sy * nd.z;
-        float detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;  // det(-d, s, e2) :317
-        float detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;  // det(-d, e1, s) :320
-        float u = detU / det;
-        float v = detV / det;
-        if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {        // :328-335
+        float t, distance;
+        auto uvf = [&](float &detU, float &detV) {
+            float Q3 = nd.y * c.sz - c.sy * nd.z;
+            detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;    // det(-d, s, e2) :317
+            detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;    // det(-d, e1, s) :320
+        };
+        if (tri_accept(c.detT, det, len, best, uvf, t, distance)) {
             best = distance;
             bt = t;
             bi = k;
@@ -420,10 +614,26 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
         bt[n] = 0.f;
         bi[n] = INT_MIN;
     }
+#if CG_RT_PREFETCH
+    // software pipelining: the next triangle's constants are loaded while
+    // this one is tested
+    int kn = mask ? __builtin_ctzll(mask) : 0;
+    RtTri cn = tc[kn];
+#endif
     while (mask != 0ull) {
+#if CG_RT_PREFETCH
+        const int k = kn;
+        const RtTri c = cn;
+        mask &= mask - 1ull;
+        if (mask) {
+            kn = __builtin_ctzll(mask);
+            cn = tc[kn];
+        }
+#else
         const int k = __builtin_ctzll(mask);
         mask &= mask - 1ull;
         const RtTri c = tc[k];
+#endif
 #pragma unroll
         for (int n = 0; n < N; ++n) {
             if (!live[n]) continue;
@@ -431,16 +641,13 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
             float Q2 = nd.y * c.e2z - c.e2y * nd.z;
             float Q1 = nd.y * c.e1z - c.e1y * nd.z;
             float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;  // det(-d, e1, e2) :289
-            float t = c.detT / det;                               // :306
-            float distance = t * len[n];                          // :307
-            if (distance < 0.0f) continue;                        // :311
-            if (distance >= best[n] || distance > bound) continue;   // :313
-            float Q3 = nd.y * c.sz - c.sy * nd.z;
-            float detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;  // :317
-            float detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;  // :320
-            float u = detU / det;
-            float v = detV / det;
-            if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {        // :328-335
+            float t, distance;
+            auto uvf = [&](float &detU, float &detV) {
+                float Q3 = nd.y * c.sz - c.sy * nd.z;
+                detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;    // :317
+                detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;    // :320
+            };
+            if (tri_accept(c.detT, det, len[n], best[n], uvf, t, distance)) {
                 best[n] = distance;
                 bt[n] = t;
                 bi[n] = k;
@@ -520,16 +727,13 @@ __device__ __forceinline__ void closest_primary_group(const RtFrame &F, const Rt
         for (int s = 0; s < NS; ++s) {
             const int a = s / NJ, b = s % NJ;
             float det = (A[a] - B[b]) + C[b];                  // det(-d, e1, e2) :289
-            float t = c.detT / det;                            // :306
-            float distance = t * len[s];                       // :307
-            if (distance < 0.0f) continue;                     // :311
-            if (distance >= best[s] || distance > bound) continue;   // :313
-            float Q3 = ndy[b] * c.sz - c.sy * ndz;
-            float detU = (ndx[a] * c.K2 - c.sx * Q2[b]) + c.e2x * Q3;   // :317
-            float detV = (ndx[a] * c.K3 - c.e1x * Q3) + c.sx * Q1[b];   // :320
-            float u = detU / det;
-            float v = detV / det;
-            if ((u >= 0) && (v >= 0) && ((u + v) <= 1)) {     // :328-335
+            float t, distance;
+            auto uvf = [&](float &detU, float &detV) {
+                float Q3 = ndy[b] * c.sz - c.sy * ndz;
+                detU = (ndx[a] * c.K2 - c.sx * Q2[b]) + c.e2x * Q3;   // :317
+                detV = (ndx[a] * c.K3 - c.e1x * Q3) + c.sx * Q1[b];   // :320
+            };
+            if (tri_accept(c.detT, det, len[s], best[s], uvf, t, distance)) {
                 best[s] = distance;
                 bt[s] = t;
                 bi[s] = k;
@@ -576,6 +780,19 @@ __device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 
     float K2 = sy * c.e2z - c.e2y * sz;
     float K4 = sy * c.e1z - c.e1y * sz;
     float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;                    // det(s, e1, e2)
+#if CG_RT_DIVFREE
+    // the shadow verdict needs only the comparisons: divide-free when certain
+    {
+        const int td = t_decide(detT, det, len, rmag);
+        if (td == 0) return false;
+        if (td == 1) {
+            float Q3 = nd.y * sz - sy * nd.z;
+            float K3 = c.e1y * sz - sy * c.e1z;
+            const int ud = uv_decide(det, (nd.x * K2 - sx * Q2) + c.e2x * Q3, (nd.x * K3 - c.e1x * Q3) + sx * Q1);
+            if (ud >= 0) return ud == 1;
+        }
+    }
+#endif
     float t = detT / det;
     float distance = t * len;
     if (distance < 0.0f) return false;
@@ -756,6 +973,15 @@ __device__ __forceinline__ unsigned long long shadow_mask_box(const RtFrame &F, 
     bool keep = true;
     if (lane < F.n_tris && B.lo[0] <= B.hi[0])
         keep = !cull_shadow(tc[lane], v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, B);
+    return __ballot(keep && lane < F.n_tris);
+}
+
+// As shadow_mask_box, lane k holding triangle k's constants in `c`.
+__device__ __forceinline__ unsigned long long shadow_mask_lane(const RtFrame &F, const RtTri &c, const ShadowBox &B,
+                                                               int lane)
+{
+    bool keep = true;
+    if (lane < F.n_tris && B.lo[0] <= B.hi[0]) keep = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, B);
     return __ballot(keep && lane < F.n_tris);
 }
 

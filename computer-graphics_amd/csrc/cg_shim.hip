@@ -15,13 +15,14 @@
 
 namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTri *, RtShade *, hipStream_t,
-                             const RtFrame *, unsigned long long *);
+                             const RtFrame *, const RtSphere *, unsigned long long *);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                     const unsigned long long *, const RtFrameCams &, int, size_t, uint32_t *,
                                     hipStream_t);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             const unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
+bool rt_lat_stamps(unsigned long long out[8], hipStream_t st);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t);
@@ -365,13 +366,13 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
 {
     unsigned long long *lat = nullptr;
     if (rt_use_lattice(F)) {
-        CG_TRY(c, c->latmask.ensure(rt_lattice_tiles(F) * sizeof(unsigned long long)), "alloc lattice masks");
+        CG_TRY(c, c->latmask.ensure(rt_lattice_tiles(F) * 2 * sizeof(unsigned long long)), "alloc lattice masks");
         lat = (unsigned long long *)c->latmask.p;
     }
     RtFrameCams cams{};
     for (int k = 0; k < 4; ++k) cams.c[0][k] = F.cam[k];
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st, &F, lat), "rt_prepare launch");
+                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat), "rt_prepare launch");
     if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) {
         // large scene: binned certificates (cg_rt_big.hip)
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
@@ -404,7 +405,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                                     void *d_out, size_t stride, hipStream_t st)
 {
     const size_t tiles = rt_lattice_tiles(F);
-    CG_TRY(c, c->latmask.ensure((size_t)nf * tiles * sizeof(unsigned long long)), "alloc lattice masks");
+    CG_TRY(c, c->latmask.ensure((size_t)nf * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
     CG_TRY(c, c->tc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
     RtFrameCams fc{};
     for (int f = 0; f < nf; ++f) {
@@ -413,10 +414,40 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     }
     unsigned long long *lat = (unsigned long long *)c->latmask.p;
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st, &F, lat), "rt_prepare launch");
+                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat), "rt_prepare launch");
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                        (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st),
            "rt_lattice launch");
+    static const bool diag = getenv("CG_RT_LAT_DIAG") != nullptr;
+    if (diag) {   // certificate statistics of frame 0's tiles (diagnostics only: synchronises)
+        std::vector<unsigned long long> m(2 * tiles);
+        if (hipMemcpyAsync(m.data(), lat, tiles * 16, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+            for (int which = 0; which < 2; ++which) {
+                long long sum = 0, sph = 0;
+                int mx = 0, hist[65] = {0};
+                for (size_t t = 0; t < tiles; ++t) {
+                    const unsigned long long x = m[2 * t + which] & (which ? ~0ull : ~(1ull << 63));
+                    sph += which ? 0 : (long long)(m[2 * t] >> 63);
+                    const int p = __builtin_popcountll(x);
+                    sum += p;
+                    mx = std::max(mx, p);
+                    ++hist[p];
+                }
+                fprintf(stderr, "[cg_rt_lattice] tiles %zu: %s triangles per tile mean %.2f max %d%s; histogram",
+                        tiles, which ? "shadow-certified" : "primary-certified", (double)sum / tiles, mx,
+                        which ? "" : (std::string(", sphere in ") + std::to_string(sph)).c_str());
+                for (int p = 0; p <= mx; ++p) fprintf(stderr, " %d", hist[p]);
+                fprintf(stderr, "\n");
+            }
+        }
+        unsigned long long ph[8];
+        if (rt_lat_stamps(ph, st)) {
+            const double waves = (double)nf * tiles * (kRtThreads / 64);
+            fprintf(stderr, "[cg_rt_lattice] cycles per wave: pass1 %.0f, pass2 %.0f, barrier %.0f, pixels %.0f\n",
+                    ph[0] / waves, ph[3] / waves, ph[4] / waves, ph[5] / waves);
+        }
+    }
     return CG_OK;
 }
 
@@ -594,7 +625,7 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     RtFrameCams zero{};
     zero.c[0][3] = 1.0f;
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, 1, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, c->stream, nullptr, nullptr), "prepare");
+                                (RtShade *)c->shade.p, c->stream, nullptr, nullptr, nullptr), "prepare");
     CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
     CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec3) + 16), "alloc");
     CG_TRY(c, hipMemcpyAsync(c->probe_c.p, isects, (size_t)n * sizeof(cg_isect), hipMemcpyHostToDevice, c->stream), "h2d");
