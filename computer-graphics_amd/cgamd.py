@@ -129,6 +129,10 @@ def load(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise RuntimeError(f"libcgamd.so not built at {path}; run __graft_entry__.build()")
+    try:   # one HIP runtime per process: torch's (it bundles libamdhip64) must load first
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)

@@ -63,6 +63,9 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
 // blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
 // out + frame * n, its masks at lat_masks + frame * tiles).
+#ifndef CG_RT_SPH_SHADOW_CERT
+#define CG_RT_SPH_SHADOW_CERT 1
+#endif
 // Per tile it stores two masks: [0] the primary certificate (bit 63: a
 // sphere may be hit), [1] the shadow certificate for every hit the tile's
 // rays can produce (primary_hit_box / sphere_hit_box), so the lattice kernel
@@ -87,13 +90,19 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
         }
         return;
     }
+    // Tile certificates: lpt lanes per tile (lane k = triangle k; the last lane
+    // takes the spheres), two tiles per wave when the scene has <= 31 triangles.
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW;
     const int tiles = tiles_x * ((F.rows_out + kLatTileH - 1) / kLatTileH);
     lat_masks += (size_t)frame * tiles * 2;
-    const int tile = ((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave;
-    if (tile >= tiles) return;   // whole wave
-    const LatTile G = lat_tile(F, tile % tiles_x, tile / tiles_x);
+    const int tpw = n <= 31 ? 2 : 1, lpt = 64 / tpw;
+    const int sub = lane / lpt, sl = lane - sub * lpt;
+    const int tile = (((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave) * tpw + sub;
+    if (__ballot(tile < tiles) == 0ull) return;   // whole wave
+    const bool tv = tile < tiles;
+    const LatTile G = lat_tile(F, tv ? tile % tiles_x : 0, tv ? tile / tiles_x : 0);
+    const bool act = tv && G.rows > 0;
     const float camf[4] = {cx, cy, cz, cw};
     const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
     const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
@@ -101,8 +110,8 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     RtTri c{};
     LanePosBox pb;   // this lane's share of the tile's possible hit positions
     pb.init();
-    if (G.rows > 0 && lane < n) {
-        c = rt_tri_const(tris[lane], cx, cy, cz, cw);
+    if (act && sl < n) {
+        c = rt_tri_const(tris[sl], cx, cy, cz, cw);
         PrimDet pd;
         keep = !cull_primary(c, x0, x1, y0, y1, F.focal, &pd);
         if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi))
@@ -111,18 +120,46 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
                 pb.hi[k] = INFINITY;
             }
     }
-    if (G.rows > 0 && lane == 63)   // spheres (lattice scenes have n <= 63 triangles)
+    if (act && sl == lpt - 1)   // spheres (lattice scenes have n <= 63 triangles)
         for (int q = 0; q < F.n_sph; ++q)
             if (!sphere_surely_missed(sph[q], camf, x0, x1, y0, y1, F.focal)) {
                 sphere = true;
                 sphere_hit_box(sph[q], camf, pb.lo, pb.hi);
             }
-    const unsigned long long m = __ballot(keep) | (__ballot(sphere) ? (1ull << 63) : 0ull);
-    unsigned long long sm = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
-    if (F.cull_shadow && F.n_lights > 0) sm = shadow_mask_lane(F, c, shadow_box_of_positions(F, pb), lane);
-    if (lane == 0) {
-        lat_masks[2 * tile] = m;
-        lat_masks[2 * tile + 1] = sm;
+    const unsigned long long half = tpw == 2 ? 0xffffffffull : ~0ull;
+    const unsigned long long m = ((__ballot(keep) >> (sub * lpt)) & half) |
+                                 (((__ballot(sphere) >> (sub * lpt)) & half) ? (1ull << 63) : 0ull);
+    // the tile's box of possible hit positions (reduction within its lanes)
+    float blo[3], bhi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float lo = pb.lo[k], hi = pb.hi[k];
+        for (int o = lpt >> 1; o > 0; o >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, o, 64));
+            hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+        }
+        blo[k] = lo;
+        bhi[k] = hi;
+    }
+    const bool cert = F.cull_shadow && F.n_lights > 0;
+    bool keep_s = true;
+    if (cert && act && m != 0ull && sl < n && blo[0] <= bhi[0])
+        keep_s = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, blo, bhi));
+    unsigned long long sm = (__ballot(keep_s && sl < n) >> (sub * lpt)) & half;
+    bool sph_shadow = F.n_sph > 0;   // bit 63 of the shadow mask: a sphere may block a shadow ray
+    if (m == 0ull) {
+        sm = 0ull;                   // no ray of the tile can hit anything: no shadow rays
+        sph_shadow = false;
+    } else if (CG_RT_SPH_SHADOW_CERT && cert && F.n_lights == 1 && blo[0] <= bhi[0]) {
+        const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // one light: lc = its position
+        bool any = false;
+        for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed(sph[q], Lp, blo, bhi);
+        sph_shadow = any;
+    }
+    sm = (sm & ~(1ull << 63)) | (sph_shadow ? (1ull << 63) : 0ull);
+    if (tv && sl == 0) {
+        lat_masks[2 * tile] = act ? m : 0ull;
+        lat_masks[2 * tile + 1] = act ? sm : 0ull;
     }
 }
 
@@ -311,8 +348,9 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
     const int u0 = G.u0, L0 = G.L0, nu = G.nu, nv = G.nv, ax0 = G.ax0, ay0 = G.ay0;
     const int cols = G.cols, rows = G.rows;
-    __shared__ int s_bi[kLatN];
-    __shared__ float s_r[kLatN], s_g[kLatN], s_b[kLatN];   // DirectLight; s_r holds t after pass 1
+    // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
+    // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
+    __shared__ float4 s_pt[kLatN];
     __shared__ RtShade s_shade[64];
     if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
     // the needed points, walked row-major at the full pitch kLatW (columns >=
@@ -327,10 +365,12 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 #endif
     const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
-    const unsigned long long smask = uniform_u64(lat_masks[2 * tix + 1]);
-    const unsigned long long mask = m0 & ~(1ull << 63);
+    const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
+    const unsigned long long mask = m0 & ~(1ull << 63), smask = s0 & ~(1ull << 63);
     RtFrame Fp = F;                        // pass 1: spheres only where one may be hit
     if (!(m0 >> 63)) Fp.n_sph = 0;
+    RtFrame Fs = F;                        // pass 2: spheres only where one may block a shadow ray
+    if (!(s0 >> 63)) Fs.n_sph = 0;
     __syncthreads();                       // s_shade
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
 #if CG_RT_LAT_PAIR
@@ -354,8 +394,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
             if (!live[n]) continue;
-            s_bi[pp[n]] = bi[n];
-            s_r[pp[n]] = t[n];
+            s_pt[pp[n]] = make_float4(t[n], 0.0f, 0.0f, __int_as_float(bi[n]));
         }
     }
 #else
@@ -366,8 +405,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
             float t;
             const int bi = closest_primary<true>(Fp, tc, sph, v3(X, Y, F.focal), t, mask);
-            s_bi[idx] = bi;
-            s_r[idx] = t;
+            s_pt[idx] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
         }
     }
 #endif
@@ -381,15 +419,14 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         const int p = p0 + lane;
         const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
         if (p < p_hi && cx < cols) {
-            const int bi = s_bi[idx];
+            const float4 q = s_pt[idx];
+            const int bi = __float_as_int(q.w);
             if (bi != INT_MIN) {
                 const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
-                const float t = s_r[idx];
+                const float t = q.x;
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                const vec3 dl = direct_light<true>(F, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
-                s_r[idx] = dl.x;
-                s_g[idx] = dl.y;
-                s_b[idx] = dl.z;
+                const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
+                s_pt[idx] = make_float4(dl.x, dl.y, dl.z, q.w);
             }
         }
     }
@@ -408,10 +445,11 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         for (int k = 0; k < 9; ++k) {
             const int i = k / 3 - 1, j = k % 3 - 1;
             const int idx = (2 * ty + 1 + j) * kLatW + (2 * tx + 1 + i);
-            const int bi = s_bi[idx];
+            const float4 q = s_pt[idx];
+            const int bi = __float_as_int(q.w);
             if (bi == INT_MIN) continue;
             valid = true;
-            pc = pc + v3(s_r[idx], s_g[idx], s_b[idx]);                                   // :151-153
+            pc = pc + v3(q.x, q.y, q.z);                                                  // :151-153
             pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
@@ -617,7 +655,8 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
     if (F && d_lat_masks) {
         Fl = *F;
         const int tiles = ((F->W + kLatTileW - 1) / kLatTileW) * ((F->rows_out + kLatTileH - 1) / kLatTileH);
-        cert = (tiles + threads / 64 - 1) / (threads / 64);
+        const int tpw = n <= 31 ? 2 : 1;   // tiles per wave (rt_prepare_kernel)
+        cert = (tiles + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
     }
     hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
                        d_tc, d_shade, prep, Fl, d_sph, d_lat_masks);

@@ -295,6 +295,37 @@ __device__ static void sphere_hit_box(const RtSphere &S, const float cam[4], flo
     }
 }
 
+// The sphere certainly blocks none of the shadow rays (:394-395) cast from hit
+// positions in the box [lo, hi] towards the light at Lp: Sphere::intersect's
+// float discriminant (TestModelH.h:27) is negative for all of them.  Exactly,
+// disc / 4a = r^2 - dist(C, line)^2 for the line through the start S with
+// direction d = Lp - pos; that line runs within ~3e-5 of the line through Lp
+// and pos (S = pos + n 1e-5 and the roundings of d), and the float evaluation
+// moves r^2 - dist^2 by < 20 eps (|S - C|^2 + r^2).  Certain when, over the box,
+// dist(C, line(Lp, pos)) >= r + 2e-3 with |pos - Lp| >= 0.05 (so the 3e-5
+// shifts move the distance by < 1e-3), using dist^2 = |w|^2 - (w.u)^2 / |u|^2,
+// w = C - Lp, u = pos - Lp, max (w.u)^2 at a corner of the box, min |u|^2 at
+// the point of the box nearest Lp.
+__device__ static bool sphere_shadow_surely_missed(const RtSphere &S, const double Lp[3], const float lo[3],
+                                                   const float hi[3])
+{
+    const double w[3] = {(double)S.cx - Lp[0], (double)S.cy - Lp[1], (double)S.cz - Lp[2]};
+    double ulo[3], uhi[3], n2 = 0.0, wu = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        ulo[k] = (double)lo[k] - Lp[k];
+        uhi[k] = (double)hi[k] - Lp[k];
+        const double nk = ulo[k] > 0 ? ulo[k] : (uhi[k] < 0 ? uhi[k] : 0.0);
+        n2 += nk * nk;
+        wu += fmax(fabs(w[k] * ulo[k]), fabs(w[k] * uhi[k]));
+    }
+    if (!(isfinite(wu) && n2 >= 0.0025)) return false;
+    const double w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const double r = sqrt((double)S.r2) + 2e-3;
+    // wu >= max |w.u| (sum of per-component maxima of |w_k u_k|)
+    return w2 - (wu * wu) / n2 * (1.0 + 1e-9) > r * r * (1.0 + 1e-9) + 1e-4;
+}
+
 // Wave-wide min / max (ds_bpermute butterflies; a DPP row version measured
 // slower here).  Callers keep all 64 lanes alive and give lanes that do not
 // contribute the identity (+-FLT_MAX).
@@ -936,13 +967,13 @@ struct LanePosBox {
 };
 
 // Whole wave, converged control flow.
-__device__ __forceinline__ ShadowBox shadow_box_of_positions(const RtFrame &F, const LanePosBox &b)
+__device__ __forceinline__ ShadowBox shadow_box_of_range(const RtFrame &F, const float (&lo)[3], const float (&hi)[3])
 {
     ShadowBox B;
     float pn = 0.0f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float plo = wave_min(b.lo[c]), phi = wave_max(b.hi[c]);
+        const float plo = lo[c], phi = hi[c];
         B.lo[c] = F.lmin[c] - phi;
         B.hi[c] = F.lmax[c] - plo;
         const float P = fmaxf(fabsf(plo), fabsf(phi)), D = fmaxf(fabsf(B.lo[c]), fabsf(B.hi[c]));
@@ -951,6 +982,17 @@ __device__ __forceinline__ ShadowBox shadow_box_of_positions(const RtFrame &F, c
     // float evaluation: < 16 rounded positive terms, covered by 1 + 2^-18
     B.pn = pn * 1.000003814697265625f + 1e-30f;
     return B;
+}
+
+__device__ __forceinline__ ShadowBox shadow_box_of_positions(const RtFrame &F, const LanePosBox &b)
+{
+    float lo[3], hi[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        lo[c] = wave_min(b.lo[c]);
+        hi[c] = wave_max(b.hi[c]);
+    }
+    return shadow_box_of_range(F, lo, hi);
 }
 
 // Whole wave, converged control flow: the wave's box of its lanes' boxes.
