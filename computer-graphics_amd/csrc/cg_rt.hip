@@ -371,6 +371,23 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     if (!(m0 >> 63)) Fp.n_sph = 0;
     RtFrame Fs = F;                        // pass 2: spheres only where one may block a shadow ray
     if (!(s0 >> 63)) Fs.n_sph = 0;
+    if (m0 == 0ull) {
+        // no ray of the tile can hit anything (certified): every pixel is
+        // PutPixelSDL(0, 0, 0) = 0x80000000 (:160-166)
+        const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+        if (tx < nu && ty < nv) {
+            const uint32_t px = put_pixel(v3(0.0f, 0.0f, 0.0f));
+            const size_t o = (size_t)(L0 + ty) * F.W + u0 + tx;
+            if (F.out_fmt == CG_PIX_ARGB8888) {
+                out[o] = px;
+            } else {
+                out8[3 * o] = (uint8_t)px;
+                out8[3 * o + 1] = (uint8_t)(px >> 8);
+                out8[3 * o + 2] = (uint8_t)(px >> 16);
+            }
+        }
+        return;                            // the whole workgroup (m0 is uniform)
+    }
     __syncthreads();                       // s_shade
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
 #if CG_RT_LAT_PAIR
