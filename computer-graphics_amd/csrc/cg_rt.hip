@@ -63,6 +63,9 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
 // blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
 // out + frame * n, its masks at lat_masks + frame * tiles).
+#ifndef CG_RT_OCCLUSION
+#define CG_RT_OCCLUSION 1
+#endif
 #ifndef CG_RT_SPH_SHADOW_CERT
 #define CG_RT_SPH_SHADOW_CERT 1
 #endif
@@ -110,16 +113,32 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     RtTri c{};
     LanePosBox pb;   // this lane's share of the tile's possible hit positions
     pb.init();
+    PrimDet pd;
+    double tlo = 0.0, thi = INFINITY;
     if (act && sl < n) {
         c = rt_tri_const(tris[sl], cx, cy, cz, cw);
-        PrimDet pd;
         keep = !cull_primary(c, x0, x1, y0, y1, F.focal, &pd);
-        if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi))
-            for (int k = 0; k < 3; ++k) {
-                pb.lo[k] = -INFINITY;
-                pb.hi[k] = INFINITY;
-            }
+        if (keep && !primary_t_range(c, pd, tlo, thi)) {
+            tlo = 0.0;
+            thi = INFINITY;
+        }
     }
+#if CG_RT_OCCLUSION
+    // Occlusion: a triangle A that every ray of the tile certainly hits
+    // (primary_covers) hides every triangle B whose t certainly exceeds A's:
+    // t_B >= tlo_B > thi_A (1 + 2^-18) gives distance_B > distance_A for every
+    // ray, so B is never the closest hit (:313 keeps the strictly closer one)
+    // and is dropped from the mask and from the box of hit positions.  (The
+    // sphere is never dropped: its test compares a parametric t, :348.)
+    double occ = (keep && primary_covers(c, pd)) ? thi : INFINITY;
+    for (int o = lpt >> 1; o > 0; o >>= 1) occ = fmin(occ, __shfl_xor(occ, o, 64));
+    if (keep && tlo > occ * (1.0 + 0x1p-18)) keep = false;
+#endif
+    if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi))
+        for (int k = 0; k < 3; ++k) {
+            pb.lo[k] = -INFINITY;
+            pb.hi[k] = INFINITY;
+        }
     if (act && sl == lpt - 1)   // spheres (lattice scenes have n <= 63 triangles)
         for (int q = 0; q < F.n_sph; ++q)
             if (!sphere_surely_missed(sph[q], camf, x0, x1, y0, y1, F.focal)) {
@@ -305,7 +324,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 // (pc += DirectLight; pc += objColor * indirect, k = 0..8), so the float sums
 // are formed exactly as the reference forms them.
 #ifndef CG_RT_LAT_PAIR
-#define CG_RT_LAT_PAIR 1   // pass 1 traces two lattice points per lane per step
+#define CG_RT_LAT_PAIR 1   // pass 1 traces CG_RT_LAT_PAIR + 1 lattice points per lane per step
 #endif
 // Phase timing of the lattice kernel (diagnostic builds only: -DCG_RT_LAT_STAMPS):
 // per wave, s_memtime deltas accumulated into cg_lat_stamps[phase].
@@ -391,13 +410,15 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     __syncthreads();                       // s_shade
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
 #if CG_RT_LAT_PAIR
-    // two points per lane per step (p and p + 64): one triangle load for both rays
-    for (int p0 = p_lo; p0 < p_hi; p0 += 128) {
-        float X[2], Y[2];
-        bool live[2];
-        int pp[2];
+    // CG_RT_LAT_PAIR + 1 points per lane per step (p, p + 64, ...): one triangle
+    // load for all of them
+    constexpr int NP = CG_RT_LAT_PAIR + 1;
+    for (int p0 = p_lo; p0 < p_hi; p0 += 64 * NP) {
+        float X[NP], Y[NP];
+        bool live[NP];
+        int pp[NP];
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
+        for (int n = 0; n < NP; ++n) {
             const int p = p0 + 64 * n + lane;
             const int cy = p / kLatW, cx = p - cy * kLatW;
             pp[n] = p;
@@ -405,11 +426,11 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             X[n] = 0.5f * (float)(ax0 + cx);
             Y[n] = 0.5f * (float)(ay0 + cy);
         }
-        int bi[2];
-        float t[2];
-        closest_primary_n<2>(Fp, tc, sph, X, Y, live, mask, bi, t);                        // :140
+        int bi[NP];
+        float t[NP];
+        closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t);                       // :140
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
+        for (int n = 0; n < NP; ++n) {
             if (!live[n]) continue;
             s_pt[pp[n]] = make_float4(t[n], 0.0f, 0.0f, __int_as_float(bi[n]));
         }

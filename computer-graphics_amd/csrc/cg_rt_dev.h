@@ -156,7 +156,10 @@ __device__ __forceinline__ bool uv_sum_reject(int sg, double blo, double bhi, do
 
 // The float det's range over a bundle (cull_primary): [dlo - Ed, dhi + Ed].
 struct PrimDet {
-    double dlo, dhi, Ed;
+    double dlo, dhi, Ed;   // det
+    double ulo, uhi, Eu;   // detU
+    double vlo, vhi, Ev;   // detV
+    double blo, bhi, Eb;   // detU + detV - det
 };
 
 __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0, float y1, float f,
@@ -185,7 +188,7 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
     double Eu = g * det3_bound(Dx, Dy, Dz, s, e2) + 1e-12 * (fabs(ulo) + fabs(uhi));
     double Ev = g * det3_bound(Dx, Dy, Dz, e1, s) + 1e-12 * (fabs(vlo) + fabs(vhi));
     double Eb = Ed + Eu + Ev + 1e-12 * (fabs(blo) + fabs(bhi));
-    if (pd) *pd = PrimDet{dlo, dhi, Ed};
+    if (pd) *pd = PrimDet{dlo, dhi, Ed, ulo, uhi, Eu, vlo, vhi, Ev, blo, bhi, Eb};
     if (!(isfinite(dlo) && isfinite(dhi) && isfinite(Ed + Eu + Ev + Eb) && isfinite(ulo + uhi + vlo + vhi + blo + bhi)))
         return false;
     int sg;
@@ -276,6 +279,45 @@ __device__ static bool sphere_surely_missed(const RtSphere &S, const float cam[4
     const double dd = nx * nx + ny * ny + (double)f * f;
     const double U = mdl * (1.0 + 1e-12) + 4.0 * 5.9604644775390625e-8 * msum;
     return isfinite(U) && U * U < dd * (double)cf * (1.0 - 0x1p-18);
+}
+
+// The float t = fl(detT / det) of every ray of the bundle lies in [tlo, thi]
+// (det's sign certain, both >= 0 as for primary_hit_box); false otherwise.
+__device__ __forceinline__ bool primary_t_range(const RtTri &c, const PrimDet &pd, double &tlo, double &thi)
+{
+    double dmin, dmax;
+    if (pd.dlo - pd.Ed > 0) {
+        dmin = pd.dlo - pd.Ed;
+        dmax = pd.dhi + pd.Ed;
+    } else if (pd.dhi + pd.Ed < 0) {
+        dmin = -(pd.dhi + pd.Ed);
+        dmax = -(pd.dlo - pd.Ed);
+    } else {
+        return false;
+    }
+    const double aT = fabs((double)c.detT);
+    tlo = aT / dmax * (1.0 - 0x1p-20);
+    thi = aT / dmin * (1.0 + 0x1p-20);
+    return isfinite(thi);
+}
+
+// Every ray of the bundle certainly passes the reference's acceptance tests
+// for this triangle except the running-best comparison (:311, :328-335): det's
+// sign is certain, detT has that sign (t > 0), detU and detV have it or vanish
+// (u, v >= 0 after rounding, including -0), and u + v - 1 = b / det <
+// -2^-20, so fl(fl(u) + fl(v)) <= 1 (three roundings of 2^-24 each).
+__device__ __forceinline__ bool primary_covers(const RtTri &c, const PrimDet &pd)
+{
+    const double dT = c.detT;
+    if (pd.dlo - pd.Ed > 0) {
+        const double dmax = pd.dhi + pd.Ed;
+        return dT > 0 && pd.ulo - pd.Eu >= 0 && pd.vlo - pd.Ev >= 0 && pd.bhi + pd.Eb < -0x1p-20 * dmax;
+    }
+    if (pd.dhi + pd.Ed < 0) {
+        const double dmax = -(pd.dlo - pd.Ed);
+        return dT < 0 && pd.uhi + pd.Eu <= 0 && pd.vhi + pd.Ev <= 0 && pd.blo - pd.Eb > 0x1p-20 * dmax;
+    }
+    return false;
 }
 
 // Box of the positions of sphere hits (:345): a hit's float t carries an

@@ -440,6 +440,15 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                 for (int p = 0; p <= mx; ++p) fprintf(stderr, " %d", hist[p]);
                 fprintf(stderr, "\n");
             }
+            if (getenv("CG_RT_LAT_DIAG_MAP")) {   // per-tile popcounts (primary/shadow), 0-9 then a-z
+                const int tx = (F.W + kLatTileW - 1) / kLatTileW;
+                for (int which = 0; which < 2; ++which)
+                    for (size_t t = 0; t < tiles; ++t) {
+                        const int p = __builtin_popcountll(m[2 * t + which]);
+                        fputc(p < 10 ? '0' + p : 'a' + std::min(25, p - 10), stderr);
+                        if ((int)(t % tx) == tx - 1) fputc('\n', stderr);
+                    }
+            }
         }
         unsigned long long ph[8];
         if (rt_lat_stamps(ph, st)) {
