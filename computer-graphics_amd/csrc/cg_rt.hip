@@ -63,6 +63,9 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
 // blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
 // out + frame * n, its masks at lat_masks + frame * tiles).
+#ifndef CG_RT_TRI_CLIP
+#define CG_RT_TRI_CLIP 1
+#endif
 #ifndef CG_RT_OCCLUSION
 #define CG_RT_OCCLUSION 1
 #endif
@@ -134,7 +137,8 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     for (int o = lpt >> 1; o > 0; o >>= 1) occ = fmin(occ, __shfl_xor(occ, o, 64));
     if (keep && tlo > occ * (1.0 + 0x1p-18)) keep = false;
 #endif
-    if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi))
+    const cg_tri *Tp = (act && sl < n) ? &tris[sl] : nullptr;
+    if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi, CG_RT_TRI_CLIP ? Tp : nullptr))
         for (int k = 0; k < 3; ++k) {
             pb.lo[k] = -INFINITY;
             pb.hi[k] = INFINITY;
@@ -143,7 +147,7 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
         for (int q = 0; q < F.n_sph; ++q)
             if (!sphere_surely_missed(sph[q], camf, x0, x1, y0, y1, F.focal)) {
                 sphere = true;
-                sphere_hit_box(sph[q], camf, pb.lo, pb.hi);
+                sphere_hit_box(sph[q], camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi);
             }
     const unsigned long long half = tpw == 2 ? 0xffffffffull : ~0ull;
     const unsigned long long m = ((__ballot(keep) >> (sub * lpt)) & half) |

@@ -220,8 +220,17 @@ __device__ static bool cull_primary(const RtTri &c, float x0, float x1, float y0
 // and t of det's sign) when det's sign is certain, and position = fl(cam +
 // fl(t d)) is widened by 2^-20 (|cam| + |t d|) per component for its two
 // roundings.  Returns false (unbounded) when det's sign is uncertain.
+// The box is then clipped to the triangle's own box: an accepted hit has float
+// u, v >= 0 and u + v <= 1, so the exact plane point X has barycentrics >=
+// -sig and sum <= 1 + sig with sig = 2 (Ed + Eu + Ev) / dmin + 2^-21 (PrimDet's
+// error bounds), i.e. X lies in the box of (v0, v0 + e1, v0 + e2) widened by
+// sig (|e1| + |e2|) per component; and the float position differs from X by
+// the relative error of t (ET / |detT| + Ed / dmin + 2^-22, ET = the float
+// detT's error bound) times |t d| plus its own two roundings.  This makes the
+// box of a hit on an axis-aligned wall flat instead of the t-range's slab.
 __device__ static bool primary_hit_box(const RtTri &c, const PrimDet &pd, const float cam[4], float x0, float x1,
-                                       float y0, float y1, float f, float lo[3], float hi[3])
+                                       float y0, float y1, float f, float lo[3], float hi[3],
+                                       const cg_tri *T = nullptr)
 {
     double dmin, dmax;
     if (pd.dlo - pd.Ed > 0) {
@@ -246,6 +255,27 @@ __device__ static bool primary_hit_box(const RtTri &c, const PrimDet &pd, const 
         const double w = 0x1p-20 * (fabs((double)cam[k]) + fmax(fabs(mn), fabs(mx))) + 1e-30;
         lo[k] = (float)((cam[k] + mn) - w);
         hi[k] = (float)((cam[k] + mx) + w);
+    }
+    if (T) {
+        const double eps = 5.9604644775390625e-8;   // 2^-24
+        const vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z);
+        const double ET = 16.0 * eps * det3_bound(fabs((double)c.sx), fabs((double)c.sy), fabs((double)c.sz), e1, e2);
+        const double aT = fabs((double)c.detT);
+        const double sig = 2.0 * (pd.Ed + pd.Eu + pd.Ev) / dmin + 0x1p-21;
+        const double trel = ET / aT + pd.Ed / dmin + 0x1p-22;
+        if (!(aT > 0.0 && isfinite(sig) && isfinite(trel) && sig < 1e-3 && trel < 1e-3)) return true;
+        const double v0[3] = {(double)T->v0.x, (double)T->v0.y, (double)T->v0.z};
+        const double a1[3] = {(double)e1.x, (double)e1.y, (double)e1.z}, a2[3] = {(double)e2.x, (double)e2.y, (double)e2.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double p1 = v0[k] + a1[k], p2 = v0[k] + a2[k];
+            const double td = thi * fmax(fabs(dl[k]), fabs(dh[k]));
+            const double m = sig * (fabs(a1[k]) + fabs(a2[k])) + trel * td + 0x1p-21 * (fabs((double)cam[k]) + td) +
+                             0x1p-40 * (fabs(v0[k]) + fabs(a1[k]) + fabs(a2[k])) + 1e-30;
+            const float tl = (float)(fmin(v0[k], fmin(p1, p2)) - m), th = (float)(fmax(v0[k], fmax(p1, p2)) + m);
+            lo[k] = fmaxf(lo[k], tl);
+            hi[k] = fminf(hi[k], th);
+        }
     }
     return true;
 }
@@ -324,16 +354,33 @@ __device__ __forceinline__ bool primary_covers(const RtTri &c, const PrimDet &pd
 // absolute error below sqrt(20 eps) |L| / |d| near tangency (the root of a
 // discriminant perturbed by ~10 eps b^2), so the float position lies within
 // 1.1e-3 |L| of the sphere; the box is widened by 4e-3 |L|.
-__device__ static void sphere_hit_box(const RtSphere &S, const float cam[4], float lo[3], float hi[3])
+// Clipped to the bundle's frustum: the exact hit X = cam + t d lies on the
+// sphere, so |X - cam| is within r of |L| and the float t (1.1e-3 |L| / |d|
+// from X's t, as above) lies in [(|L| - r - 4e-3 |L|) / |d|max,
+// (|L| + r + 4e-3 |L|) / |d|min]; the position fl(cam + fl(t d)) then lies in
+// cam + [t] x [d] (widened for its two roundings).
+__device__ static void sphere_hit_box(const RtSphere &S, const float cam[4], float x0, float x1, float y0, float y1,
+                                      float f, float lo[3], float hi[3])
 {
     const double Lx = (double)cam[0] - S.cx, Ly = (double)cam[1] - S.cy, Lz = (double)cam[2] - S.cz;
-    const double w = sqrt((double)S.r2) * (1.0 + 1e-6) + 4e-3 * sqrt(Lx * Lx + Ly * Ly + Lz * Lz) + 1e-6;
+    const double Ln = sqrt(Lx * Lx + Ly * Ly + Lz * Lz), r = sqrt((double)S.r2) * (1.0 + 1e-6);
+    const double w = r + 4e-3 * Ln + 1e-6;
     const double C[3] = {(double)S.cx, (double)S.cy, (double)S.cz};
+    const double dl[3] = {(double)x0, (double)y0, (double)f}, dh[3] = {(double)x1, (double)y1, (double)f};
+    const double nx = x0 > 0 ? (double)x0 : (x1 < 0 ? (double)x1 : 0.0);
+    const double ny = y0 > 0 ? (double)y0 : (y1 < 0 ? (double)y1 : 0.0);
+    const double dmin = sqrt(nx * nx + ny * ny + (double)f * f) * (1.0 - 1e-12);
+    const double ax = fmax(fabs((double)x0), fabs((double)x1)), ay = fmax(fabs((double)y0), fabs((double)y1));
+    const double dmax = sqrt(ax * ax + ay * ay + (double)f * f) * (1.0 + 1e-12);
+    const double tlo = fmax(0.0, (Ln - w) / dmax), thi = (Ln + w) / dmin;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double m = 0x1p-20 * (fabs(C[k]) + w + fabs((double)cam[k]));
-        lo[k] = fminf(lo[k], (float)(C[k] - w - m));
-        hi[k] = fmaxf(hi[k], (float)(C[k] + w + m));
+        const double a = tlo * dl[k], b = tlo * dh[k], e = thi * dl[k], g = thi * dh[k];
+        const double mn = fmin(fmin(a, b), fmin(e, g)), mx = fmax(fmax(a, b), fmax(e, g));
+        const double m = 0x1p-20 * (fabs(C[k]) + w + fabs((double)cam[k]) + fmax(fabs(mn), fabs(mx)));
+        const double blo = fmax(C[k] - w, cam[k] + mn) - m, bhi = fmin(C[k] + w, cam[k] + mx) + m;
+        lo[k] = fminf(lo[k], (float)blo);
+        hi[k] = fmaxf(hi[k], (float)bhi);
     }
 }
 

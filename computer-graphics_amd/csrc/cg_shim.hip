@@ -440,6 +440,16 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                 for (int p = 0; p <= mx; ++p) fprintf(stderr, " %d", hist[p]);
                 fprintf(stderr, "\n");
             }
+            {
+                int shown = 0;
+                const int tx = (F.W + kLatTileW - 1) / kLatTileW;
+                for (size_t t = 0; t < tiles && shown < 12; ++t)
+                    if (__builtin_popcountll(m[2 * t + 1]) >= 11 && (t % 7 == 0)) {
+                        fprintf(stderr, "[cg_rt_lattice] tile (%d,%d) primary %016llx shadow %016llx\n", (int)(t % tx),
+                                (int)(t / tx), m[2 * t], m[2 * t + 1]);
+                        ++shown;
+                    }
+            }
             if (getenv("CG_RT_LAT_DIAG_MAP")) {   // per-tile popcounts (primary/shadow), 0-9 then a-z
                 const int tx = (F.W + kLatTileW - 1) / kLatTileW;
                 for (int which = 0; which < 2; ++which)
