@@ -63,6 +63,9 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
 // blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
 // out + frame * n, its masks at lat_masks + frame * tiles).
+#ifndef CG_RT_OWN_SHADOW
+#define CG_RT_OWN_SHADOW 1
+#endif
 #ifndef CG_RT_TRI_CLIP
 #define CG_RT_TRI_CLIP 1
 #endif
@@ -168,6 +171,13 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     bool keep_s = true;
     if (cert && act && m != 0ull && sl < n && blo[0] <= bhi[0])
         keep_s = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, blo, bhi));
+#if CG_RT_OWN_SHADOW
+    // a tile whose every hit lies on one triangle k: k never shadows its own hits
+    if (cert && keep && keep_s && m == (1ull << sl) && F.n_lights == 1) {
+        const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};
+        if (own_shadow_rejects(tris[sl], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, blo, bhi)) keep_s = false;
+    }
+#endif
     unsigned long long sm = (__ballot(keep_s && sl < n) >> (sub * lpt)) & half;
     bool sph_shadow = F.n_sph > 0;   // bit 63 of the shadow mask: a sphere may block a shadow ray
     if (m == 0ull) {

@@ -350,6 +350,63 @@ __device__ __forceinline__ bool primary_covers(const RtTri &c, const PrimDet &pd
     return false;
 }
 
+// The shadow ray of a hit ON triangle k never hits k itself (:394-395): it
+// starts at S = pos + n 1e-5f, off k's plane on the side of k's stored normal
+// n, and the light lies on the same side.  With N = e1 x e2 (exact), X the
+// exact plane point of the ray (|pos - X| <= Delta: t's relative error times
+// |t d| plus two roundings, as in primary_hit_box), (S - v0).N =
+// 1e-5f (n.N) + (pos - X).N + roundings, and the float det3 (s, e1, e2) adds
+// at most 16 eps sum|triple products|: its sign is that of n.N when
+// 1e-5 |n.N| exceeds that noise (each term is an upper bound; 5 % slack).  det = -d.N with d = L - pos:
+// -(L - v0).N up to (Delta + rounding of d) |N| + its det3 error.  Opposite
+// certain signs give t < 0 (|t| far from underflow): rejected at :311, for
+// every hit position in the box [blo, bhi] of hits on k.
+__device__ static bool own_shadow_rejects(const cg_tri &T, const RtTri &c, const PrimDet &pd, double thi,
+                                          const float cam[4], float x0, float x1, float y0, float y1, float f,
+                                          const double Lp[3], const float blo[3], const float bhi[3])
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    double dmin;
+    if (pd.dlo - pd.Ed > 0) dmin = pd.dlo - pd.Ed;
+    else if (pd.dhi + pd.Ed < 0) dmin = -(pd.dhi + pd.Ed);
+    else return false;
+    const vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z);
+    const double N[3] = {(double)e1.y * e2.z - (double)e2.y * e1.z, (double)e1.z * e2.x - (double)e2.z * e1.x,
+                         (double)e1.x * e2.y - (double)e2.x * e1.y};
+    const double Nn = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]) * (1.0 + 1e-12);
+    const double aT = fabs((double)c.detT);
+    const double ET = 16.0 * eps * det3_bound(fabs((double)c.sx), fabs((double)c.sy), fabs((double)c.sz), e1, e2);
+    const double trel = ET / aT + pd.Ed / dmin + 0x1p-22;
+    if (!(aT > 0.0 && isfinite(trel) && isfinite(thi))) return false;
+    const double dl[3] = {(double)x0, (double)y0, (double)f}, dh[3] = {(double)x1, (double)y1, (double)f};
+    const double v0[3] = {(double)T.v0.x, (double)T.v0.y, (double)T.v0.z};
+    const double n[3] = {(double)T.normal.x, (double)T.normal.y, (double)T.normal.z};
+    const double o = (double)0.00001f;
+    double D2 = 0.0, rho2 = 0.0, S2 = 0.0, d2 = 0.0, Sa[3], da[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double td = thi * fmax(fabs(dl[k]), fabs(dh[k]));
+        const double dk = trel * td + 0x1p-22 * (fabs((double)cam[k]) + td);
+        D2 += dk * dk;
+        const double pmax = fmax(fabs((double)blo[k]), fabs((double)bhi[k]));
+        const double rk = 0x1p-23 * (pmax + o * fabs(n[k]) + 1.0) ;
+        rho2 += rk * rk;
+        Sa[k] = fmax(fabs((double)blo[k] - v0[k]), fabs((double)bhi[k] - v0[k])) + o * fabs(n[k]) + rk;
+        S2 += Sa[k] * Sa[k];
+        da[k] = fmax(fabs(Lp[k] - (double)blo[k]), fabs(Lp[k] - (double)bhi[k]));
+        d2 += da[k] * da[k];
+    }
+    const double Delta = sqrt(D2), rho = sqrt(rho2);
+    const double nN = n[0] * N[0] + n[1] * N[1] + n[2] * N[2];
+    const double noiseT = (Delta + rho + eps * sqrt(S2)) * Nn + 16.0 * eps * det3_bound(Sa[0], Sa[1], Sa[2], e1, e2);
+    if (!(o * fabs(nN) * (1.0 - 1e-9) > 1.05 * noiseT)) return false;   // every term above is an upper bound
+    const double aN = (Lp[0] - v0[0]) * N[0] + (Lp[1] - v0[1]) * N[1] + (Lp[2] - v0[2]) * N[2];
+    const double noiseD = (Delta + eps * sqrt(d2)) * Nn + 16.0 * eps * det3_bound(da[0], da[1], da[2], e1, e2) +
+                          1e-12 * fabs(aN);
+    if (!(fabs(aN) > 1.05 * noiseD)) return false;
+    return (nN > 0) != (-aN > 0);   // detT and det of opposite signs: t < 0
+}
+
 // Box of the positions of sphere hits (:345): a hit's float t carries an
 // absolute error below sqrt(20 eps) |L| / |d| near tangency (the root of a
 // discriminant perturbed by ~10 eps b^2), so the float position lies within

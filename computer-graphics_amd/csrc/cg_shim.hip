@@ -444,7 +444,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                 int shown = 0;
                 const int tx = (F.W + kLatTileW - 1) / kLatTileW;
                 for (size_t t = 0; t < tiles && shown < 12; ++t)
-                    if (__builtin_popcountll(m[2 * t + 1]) >= 11 && (t % 7 == 0)) {
+                    if (__builtin_popcountll(m[2 * t + 1]) >= (getenv("CG_RT_LAT_DIAG_MIN") ? atoi(getenv("CG_RT_LAT_DIAG_MIN")) : 11) && (t % 37 == 0)) {
                         fprintf(stderr, "[cg_rt_lattice] tile (%d,%d) primary %016llx shadow %016llx\n", (int)(t % tx),
                                 (int)(t / tx), m[2 * t], m[2 * t + 1]);
                         ++shown;
