@@ -57,6 +57,13 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
     return G;
 }
 
+// Certificate units of a frame: tiles, or super-tiles of kSup x kSup tiles.
+__host__ __device__ __forceinline__ int rt_cert_units(const RtFrame &F, int sup)
+{
+    const int tx = (F.W + kLatTileW - 1) / kLatTileW, ty = (F.rows_out + kLatTileH - 1) / kLatTileH;
+    return sup ? ((tx + kSup - 1) / kSup) * ((ty + kSup - 1) / kSup) : tx * ty;
+}
+
 // Blocks [0, n_prep_blocks): RtTri / RtShade per triangle.  With lat_masks,
 // the blocks after them certify the lattice tiles' camera rays (one wave per
 // tile, lane k = triangle k, the same certificate as rt_pixel_kernel's over
@@ -79,10 +86,44 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 // sphere may be hit), [1] the shadow certificate for every hit the tile's
 // rays can produce (primary_hit_box / sphere_hit_box), so the lattice kernel
 // needs no certificate pass of its own.
+// With sup = 1 the certified units are super-tiles of kSup x kSup tiles (the
+// bundle: the box of all their lattice rays) and the masks go to the
+// super-tile buffer; rt_tile_cert_kernel then refines them per tile.
+__device__ __forceinline__ bool unit_bundle(const RtFrame &F, int unit, int sup, float &x0, float &x1, float &y0,
+                                            float &y1)
+{
+    const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW, tiles_y = (F.rows_out + kLatTileH - 1) / kLatTileH;
+    int bx0 = unit, bx1 = unit, by0 = 0, by1 = 0;
+    if (sup) {
+        const int sx = (tiles_x + kSup - 1) / kSup;
+        bx0 = (unit % sx) * kSup;
+        bx1 = min(bx0 + kSup, tiles_x) - 1;
+        by0 = (unit / sx) * kSup;
+        by1 = min(by0 + kSup, tiles_y) - 1;
+    } else {
+        bx0 = bx1 = unit % tiles_x;
+        by0 = by1 = unit / tiles_x;
+    }
+    const LatTile A = lat_tile(F, bx0, by0), B = lat_tile(F, bx1, by0);
+    x0 = 0.5f * (float)A.ax0;
+    x1 = 0.5f * (float)(B.ax0 + B.cols - 1);
+    bool any = false;
+    y0 = FLT_MAX;
+    y1 = -FLT_MAX;
+    for (int by = by0; by <= by1; ++by) {   // rows of a shard need not be contiguous
+        const LatTile G = lat_tile(F, bx0, by);
+        if (G.rows <= 0) continue;
+        any = true;
+        y0 = fminf(y0, 0.5f * (float)G.ay0);
+        y1 = fmaxf(y1, 0.5f * (float)(G.ay0 + G.rows - 1));
+    }
+    return any;
+}
+
 __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
                                   RtTri *__restrict__ out, RtShade *__restrict__ shade, int n_prep_blocks,
                                   RtFrame F, const RtSphere *__restrict__ sph,
-                                  unsigned long long *__restrict__ lat_masks)
+                                  unsigned long long *__restrict__ lat_masks, int sup)
 {
     const int frame = blockIdx.y;
     const float cx = cams.c[frame][0], cy = cams.c[frame][1], cz = cams.c[frame][2], cw = cams.c[frame][3];
@@ -102,19 +143,16 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     // Tile certificates: lpt lanes per tile (lane k = triangle k; the last lane
     // takes the spheres), two tiles per wave when the scene has <= 31 triangles.
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW;
-    const int tiles = tiles_x * ((F.rows_out + kLatTileH - 1) / kLatTileH);
+    const int tiles = rt_cert_units(F, sup);
     lat_masks += (size_t)frame * tiles * 2;
     const int tpw = n <= 31 ? 2 : 1, lpt = 64 / tpw;
     const int sub = lane / lpt, sl = lane - sub * lpt;
     const int tile = (((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave) * tpw + sub;
     if (__ballot(tile < tiles) == 0ull) return;   // whole wave
     const bool tv = tile < tiles;
-    const LatTile G = lat_tile(F, tv ? tile % tiles_x : 0, tv ? tile / tiles_x : 0);
-    const bool act = tv && G.rows > 0;
+    float x0, x1, y0, y1;
+    const bool act = unit_bundle(F, tv ? tile : 0, sup, x0, x1, y0, y1) && tv;
     const float camf[4] = {cx, cy, cz, cw};
-    const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
-    const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
     bool keep = false, sphere = false;
     RtTri c{};
     LanePosBox pb;   // this lane's share of the tile's possible hit positions
@@ -193,6 +231,175 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     if (tv && sl == 0) {
         lat_masks[2 * tile] = act ? m : 0ull;
         lat_masks[2 * tile + 1] = act ? sm : 0ull;
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Second level of the tile certificates: one wave per super-tile refines its
+// masks for each of its kSup x kSup tiles.  Only the super-tile's candidates
+// are certified again -- a certificate over the super-tile's bundle (or box of
+// hit positions) is a proof for every tile inside it -- and the (tile,
+// candidate) pairs are packed densely into the wave's lanes: cp lanes per tile
+// (cp = the candidate count rounded up to a power of two), segments aligned, so
+// the per-tile reductions are xor butterflies within a segment.  Phase 1:
+// primary certificate, occlusion, hit-position box, sphere; phase 2: shadow
+// certificate of the tile's box.  Same functions and exactness arguments as
+// rt_prepare_kernel's single-level path.
+
+__device__ __forceinline__ int pow2_at_least(int c)
+{
+    int p = 1;
+    while (p < c) p <<= 1;
+    return p;
+}
+// index of the i-th set bit of m (m has more than i bits)
+__device__ __forceinline__ int nth_bit(unsigned long long m, int i)
+{
+    for (int k = 0; k < i; ++k) m &= m - 1ull;
+    return __builtin_ctzll(m);
+}
+__device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int cp)
+{
+    for (int o = cp >> 1; o > 0; o >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)v, o, 64), hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+        v |= ((unsigned long long)hi << 32) | lo;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
+                                                          RtFrame F, const RtSphere *__restrict__ sph,
+                                                          const unsigned long long *__restrict__ sup_masks,
+                                                          unsigned long long *__restrict__ lat_masks)
+{
+    constexpr int kT = kSup * kSup;
+    const int frame = blockIdx.y, lane = threadIdx.x, unit = blockIdx.x;
+    const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
+    const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW, tiles_y = (F.rows_out + kLatTileH - 1) / kLatTileH;
+    const int sx = (tiles_x + kSup - 1) / kSup;
+    lat_masks += (size_t)frame * tiles_x * tiles_y * 2;
+    sup_masks += ((size_t)frame * rt_cert_units(F, 1) + unit) * 2;
+    const unsigned long long SP = sup_masks[0], SS = sup_masks[1];
+    const unsigned long long SPt = SP & ~(1ull << 63), SSt = SS & ~(1ull << 63);
+    const bool cert = F.cull_shadow && F.n_lights > 0;
+    const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // one light: lc = its position
+    __shared__ unsigned long long s_pm[kT], s_own[kT];
+    __shared__ float s_box[kT][6];
+    __shared__ int s_sphsh[kT];
+    auto tile_of = [&](int tl, int &t, LatTile &G) {
+        const int bx = (unit % sx) * kSup + tl % kSup, by = (unit / sx) * kSup + tl / kSup;
+        const bool in = tl < kT && bx < tiles_x && by < tiles_y;
+        G = lat_tile(F, in ? bx : 0, in ? by : 0);
+        t = in ? by * tiles_x + bx : -1;
+        return in && G.rows > 0;
+    };
+    // Phase 1: primary candidates (triangles of SP, then the sphere if flagged)
+    const int ntp = __popcll(SPt), cand = ntp + (int)(SP >> 63);
+    const int cp = pow2_at_least(max(cand, 1)), tpi = 64 / cp;
+    for (int it = 0; it * tpi < kT; ++it) {
+        const int seg = lane / cp, ci = lane - seg * cp, tl = it * tpi + seg;
+        int t;
+        LatTile G;
+        const bool act = tile_of(tl, t, G) && ci < cand;
+        const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
+        const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
+        const bool is_tri = act && ci < ntp;
+        const int k = is_tri ? nth_bit(SPt, ci) : 0;
+        bool keep = false, sphere = false;
+        RtTri c{};
+        PrimDet pd;
+        double tlo = 0.0, thi = INFINITY;
+        LanePosBox pb;
+        pb.init();
+        if (is_tri) {
+            c = rt_tri_const(tris[k], camf[0], camf[1], camf[2], camf[3]);
+            keep = !cull_primary(c, x0, x1, y0, y1, F.focal, &pd);
+            if (keep && !primary_t_range(c, pd, tlo, thi)) {
+                tlo = 0.0;
+                thi = INFINITY;
+            }
+        }
+#if CG_RT_OCCLUSION
+        double occ = (keep && primary_covers(c, pd)) ? thi : INFINITY;
+        for (int o = cp >> 1; o > 0; o >>= 1) occ = fmin(occ, __shfl_xor(occ, o, 64));
+        if (keep && tlo > occ * (1.0 + 0x1p-18)) keep = false;
+#endif
+        if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi,
+                                     CG_RT_TRI_CLIP ? &tris[k] : nullptr))
+            for (int q = 0; q < 3; ++q) {
+                pb.lo[q] = -INFINITY;
+                pb.hi[q] = INFINITY;
+            }
+        if (act && !is_tri)   // the sphere candidate
+            for (int q = 0; q < F.n_sph; ++q)
+                if (!sphere_surely_missed(sph[q], camf, x0, x1, y0, y1, F.focal)) {
+                    sphere = true;
+                    sphere_hit_box(sph[q], camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi);
+                }
+        const unsigned long long m = seg_or((keep ? (1ull << k) : 0ull) | (sphere ? (1ull << 63) : 0ull), cp);
+        float blo[3], bhi[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            float lo = pb.lo[q], hi = pb.hi[q];
+            for (int o = cp >> 1; o > 0; o >>= 1) {
+                lo = fminf(lo, __shfl_xor(lo, o, 64));
+                hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+            }
+            blo[q] = lo;
+            bhi[q] = hi;
+        }
+        bool own = false;
+#if CG_RT_OWN_SHADOW
+        if (cert && keep && m == (1ull << k) && F.n_lights == 1)
+            own = own_shadow_rejects(tris[k], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, blo, bhi);
+#endif
+        const unsigned long long ownm = seg_or(own ? (1ull << k) : 0ull, cp);
+        if (tl < kT && ci == 0) {
+            const bool live = tile_of(tl, t, G);
+            s_pm[tl] = live ? m : 0ull;
+            s_own[tl] = ownm;
+            for (int q = 0; q < 3; ++q) {
+                s_box[tl][q] = blo[q];
+                s_box[tl][3 + q] = bhi[q];
+            }
+            bool sphsh = F.n_sph > 0 && (SS >> 63);
+            if (live && m != 0ull && CG_RT_SPH_SHADOW_CERT && cert && F.n_lights == 1 && blo[0] <= bhi[0] && sphsh) {
+                bool any = false;
+                for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed(sph[q], Lp, blo, bhi);
+                sphsh = any;
+            }
+            s_sphsh[tl] = sphsh ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    // Phase 2: shadow candidates (triangles of SS)
+    const int nts = __popcll(SSt);
+    const int sp = pow2_at_least(max(nts, 1)), tpi2 = 64 / sp;
+    for (int it = 0; it * tpi2 < kT; ++it) {
+        const int seg = lane / sp, ci = lane - seg * sp, tl = it * tpi2 + seg;
+        int t;
+        LatTile G;
+        const bool live = tile_of(tl, t, G);
+        const unsigned long long pm = tl < kT ? s_pm[tl] : 0ull;
+        const bool act = live && ci < nts && pm != 0ull;
+        const int k = act ? nth_bit(SSt, ci) : 0;
+        bool keep_s = false;
+        if (act) {
+            keep_s = true;
+            const float blo[3] = {s_box[tl][0], s_box[tl][1], s_box[tl][2]};
+            const float bhi[3] = {s_box[tl][3], s_box[tl][4], s_box[tl][5]};
+            if (cert && blo[0] <= bhi[0]) {
+                const RtTri c = rt_tri_const(tris[k], camf[0], camf[1], camf[2], camf[3]);
+                keep_s = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, blo, bhi));
+            }
+            if ((s_own[tl] >> k) & 1ull) keep_s = false;
+        }
+        const unsigned long long sm = seg_or(keep_s ? (1ull << k) : 0ull, sp);
+        if (tl < kT && ci == 0 && t >= 0) {
+            lat_masks[2 * t] = live ? pm : 0ull;
+            lat_masks[2 * t + 1] = (live && pm != 0ull) ? (sm | (s_sphsh[tl] ? (1ull << 63) : 0ull)) : 0ull;
+        }
     }
 }
 
@@ -696,24 +903,35 @@ __global__ void rt_probe_direct_light_kernel(RtFrame F, const RtTri *__restrict_
 
 // ---------------------------------------------------------------------------
 // Launch helpers (called by the shim).
+// d_sup_masks (optional): two-level certificates -- rt_prepare_kernel certifies
+// super-tiles into d_sup_masks, rt_tile_cert_kernel refines them per tile.
 hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
                              RtShade *d_shade, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
-                             unsigned long long *d_lat_masks)
+                             unsigned long long *d_lat_masks, unsigned long long *d_sup_masks)
 {
     if (n <= 0) return hipSuccess;
     const int threads = kRtThreads, prep = (n + threads - 1) / threads;
     int cert = 0;
     RtFrame Fl{};
+    const int sup = d_sup_masks ? 1 : 0;
     if (F && d_lat_masks) {
         Fl = *F;
-        const int tiles = ((F->W + kLatTileW - 1) / kLatTileW) * ((F->rows_out + kLatTileH - 1) / kLatTileH);
-        const int tpw = n <= 31 ? 2 : 1;   // tiles per wave (rt_prepare_kernel)
-        cert = (tiles + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
+        const int units = rt_cert_units(*F, sup);
+        const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
+        cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
     }
     hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
-                       d_tc, d_shade, prep, Fl, d_sph, d_lat_masks);
+                       d_tc, d_shade, prep, Fl, d_sph, sup ? d_sup_masks : d_lat_masks, sup);
+    if (sup && F && d_lat_masks) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(rt_cert_units(*F, 1), nframes), dim3(64), 0, st, d_tris, n,
+                           cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks);
+    }
     return hipGetLastError();
 }
+
+size_t rt_sup_units(const RtFrame &F) { return (size_t)rt_cert_units(F, 1); }
 
 // The lattice kernel's precondition: R is the identity up to the sign of its
 // zeros (then mat4_mul returns (x, y) bit for bit), pixel offsets stay far

@@ -15,7 +15,8 @@
 
 namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTri *, RtShade *, hipStream_t,
-                             const RtFrame *, const RtSphere *, unsigned long long *);
+                             const RtFrame *, const RtSphere *, unsigned long long *, unsigned long long *);
+size_t rt_sup_units(const RtFrame &);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                     const unsigned long long *, const RtFrameCams &, int, size_t, uint32_t *,
                                     hipStream_t);
@@ -80,7 +81,8 @@ struct cg_ctx {
     int n_tris = -1, n_sph = 0;
     float nbound = 0.f;   // largest |normal component| of the scene (shadow certificate)
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
-    DevBuf latmask;                     // lattice tiles' primary certificates (one mask per tile)
+    DevBuf latmask;                     // lattice tiles' certificates (two masks per tile)
+    DevBuf supmask;                     // their super-tiles' certificates (two-level path)
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
@@ -344,6 +346,17 @@ extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
 
 static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st);
 
+// Two-level tile certificates (super-tiles, then tiles); CG_RT_TWO_LEVEL=0
+// selects the single-level path (A/B only: both are exact).
+static bool rt_two_level()
+{
+    static const bool on = [] {
+        const char *e = getenv("CG_RT_TWO_LEVEL");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t st)
 {
     // RGB24 output: the lattice kernel stores it directly; the other kernels
@@ -371,8 +384,13 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
     }
     RtFrameCams cams{};
     for (int k = 0; k < 4; ++k) cams.c[0][k] = F.cam[k];
+    unsigned long long *supm = nullptr;
+    if (lat && rt_two_level()) {
+        CG_TRY(c, c->supmask.ensure(rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
+        supm = (unsigned long long *)c->supmask.p;
+    }
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat), "rt_prepare launch");
+                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
     if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) {
         // large scene: binned certificates (cg_rt_big.hip)
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
@@ -413,8 +431,15 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
         fc.c[f][2] = cams[f].camera.z; fc.c[f][3] = cams[f].camera.w;
     }
     unsigned long long *lat = (unsigned long long *)c->latmask.p;
+    unsigned long long *supm = nullptr;
+    if (rt_two_level()) {
+        CG_TRY(c, c->supmask.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)),
+               "alloc super-tile masks");
+        supm = (unsigned long long *)c->supmask.p;
+    }
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat), "rt_prepare launch");
+                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat, supm),
+           "rt_prepare launch");
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                        (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st),
            "rt_lattice launch");
@@ -644,7 +669,7 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     RtFrameCams zero{};
     zero.c[0][3] = 1.0f;
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, 1, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, c->stream, nullptr, nullptr, nullptr), "prepare");
+                                (RtShade *)c->shade.p, c->stream, nullptr, nullptr, nullptr, nullptr), "prepare");
     CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
     CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec3) + 16), "alloc");
     CG_TRY(c, hipMemcpyAsync(c->probe_c.p, isects, (size_t)n * sizeof(cg_isect), hipMemcpyHostToDevice, c->stream), "h2d");
