@@ -50,9 +50,10 @@ class RtCamera(C.Structure):
 
 
 class RtShard(C.Structure):
-    """Stripes (rows == 0): RtShard(rank, nranks, stripe_h).  Band: RtShard(row0=a, rows=n)."""
+    """Stripes (rows == 0): RtShard(rank, nranks, stripe_h).  Band: RtShard(row0=a, rows=n).
+    RGB24 window: col0=, cols= (see cg_render.h)."""
     _fields_ = [("rank", C.c_int), ("nranks", C.c_int), ("stripe_h", C.c_int), ("row0", C.c_int),
-                ("rows", C.c_int)]
+                ("rows", C.c_int), ("col0", C.c_int), ("cols", C.c_int)]
 
 
 PIX_ARGB8888, PIX_RGB24 = 0, 1   # cg_render.h CG_PIX_*
@@ -98,7 +99,9 @@ _SIGS = {
     "cg_rt_render_frames_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int,
                                              C.POINTER(RtShard), P, C.c_size_t, C.c_int, P]),
     "cg_rt_assemble_device": (C.c_int, [P, P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
-                                        C.c_int, C.c_int, P, C.c_size_t, P]),
+                                        C.c_int, C.c_int, P, C.c_size_t, C.c_int, C.c_int, P]),
+    "cg_rt_frame_columns": (C.c_int, [C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int, C.POINTER(RtCamera),
+                                      C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "cg_rt_shard_rows": (C.c_int, [C.c_int, C.POINTER(RtShard)]),
     "cg_rt_unstripe_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
     "cg_rt_unstripe_batch_device": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P]),
@@ -237,6 +240,16 @@ def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
     return p
 
 
+def frame_columns(tris, n, sph, n_sph, cam):
+    """cg_rt_frame_columns: the columns [c0, c1) an unrotated camera can see anything in."""
+    lib = load()
+    c0, c1 = C.c_int(), C.c_int()
+    rc = lib.cg_rt_frame_columns(tris, n, sph, n_sph, C.byref(cam), C.byref(c0), C.byref(c1))
+    if rc != CG_OK:
+        raise RuntimeError(f"cg_rt_frame_columns failed with {rc}")
+    return c0.value, c1.value
+
+
 def rt_scene():
     lib = load()
     tris = (Tri * 64)()
@@ -337,12 +350,13 @@ class Context:
                     "cg_rt_render_frames_device")
 
     def rt_assemble_device(self, d_src, pix_format, row0, rows, width, height, nframes, d_frames, frame_stride=0,
-                           stream=None):
+                           stream=None, col0=0, cols=0):
         """cg_rt_assemble_device: row blocks (row0[b], rows[b]) of nframes frames -> frames."""
         n = len(rows)
         r0, rs = (C.c_int * n)(*row0), (C.c_int * n)(*rows)
         self._check(self.lib.cg_rt_assemble_device(self.h, P(d_src), pix_format, r0, rs, n, width, height, nframes,
-                                                   P(d_frames), frame_stride, P(stream) if stream else None),
+                                                   P(d_frames), frame_stride, col0, cols,
+                                                   P(stream) if stream else None),
                     "cg_rt_assemble_device")
 
     def rt_unstripe_device(self, d_gathered, width, height, nranks, stripe_h, d_frame, stream=None):

@@ -107,19 +107,30 @@ def pack_rgb24_np(argb: np.ndarray) -> np.ndarray:
     return argb.astype("<u4").view(np.uint8).reshape(-1, 4)[:, :3].reshape(-1).copy()
 
 
-def assemble_np(src: np.ndarray, bpp: int, bands, width: int, height: int, nframes: int, frames: np.ndarray):
+def window_np(rows_px: np.ndarray, width: int, col0: int, cols: int) -> np.ndarray:
+    """The window columns col0 .. col0 + cols - 1 of rows of `width` pixels (flattened)."""
+    return rows_px.reshape(-1, width)[:, col0:col0 + cols].reshape(-1)
+
+
+def assemble_np(src: np.ndarray, bpp: int, bands, width: int, height: int, nframes: int, frames: np.ndarray,
+                col0: int = 0, cols: int = 0):
     """Mirror of rt_assemble_kernel: src = blocks in order, block b = nframes x
-    rows_b rows; frames [nframes, height*width] uint32 updated in place."""
+    rows_b rows (of the window's `cols` pixels when cols > 0, the rest black);
+    frames [nframes, height*width] uint32 updated in place."""
+    pitch = cols if cols else width
+    c0 = col0 if cols else 0
     off = 0
     for r0, n in bands:
         for f in range(nframes):
-            blk = src[off:off + n * width * bpp]
-            off += n * width * bpp
+            blk = src[off:off + n * pitch * bpp]
+            off += n * pitch * bpp
             if bpp == 4:
                 px = blk.view("<u4")
             else:
                 b3 = blk.reshape(-1, 3).astype(np.uint32)
                 px = 0x80000000 | b3[:, 0] | (b3[:, 1] << 8) | (b3[:, 2] << 16)
             rows = min(n, max(0, height - r0))
-            frames[f, r0 * width:(r0 + rows) * width] = px[:rows * width]
+            full = np.full((rows, width), 0x80000000, np.uint32)
+            full[:, c0:c0 + pitch] = px[:rows * pitch].reshape(rows, pitch)
+            frames[f, r0 * width:(r0 + rows) * width] = full.reshape(-1)
     return frames

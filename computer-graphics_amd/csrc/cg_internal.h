@@ -23,6 +23,7 @@ constexpr int kMaxBlocks = 64;       // row blocks of one assembly launch (cg_rt
 // land at frame rows row0[b] ..; cum = prefix sums of rows.
 struct RtBlocks {
     int n, W, H, bpp;
+    int wcol0, wcols;   // source rows hold columns wcol0 .. + wcols - 1 (wcols 0: all); the rest is black
     int row0[kMaxBlocks], rows[kMaxBlocks], cum[kMaxBlocks + 1];
 };
 
@@ -84,6 +85,7 @@ struct RtFrame {
     int rank, nranks, stripe_h, rows_out;
     int row0;      // first global row (band shards; 0 for stripes): v = row0 + stripe map of L
     int out_fmt;   // CG_PIX_ARGB8888 (uint32 per pixel) or CG_PIX_RGB24 (3 bytes: B, G, R)
+    int wcol0, wcols;   // RGB24 output window: columns wcol0 .. wcol0 + wcols - 1 (wcols 0: all)
     int cull_primary, cull_shadow;   // certificates on (CG_RT_CULL env: 0 none, 1 primary, 2 both)
     const RtLight *lights;           // n_lights entries, device memory
     // The light set as the shadow certificate sees it: componentwise min/max

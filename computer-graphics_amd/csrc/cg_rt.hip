@@ -603,6 +603,11 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     unsigned long long stamp_ = __builtin_amdgcn_s_memtime();
     unsigned int stamps_[6] = {0, 0, 0, 0, 0, 0};
 #endif
+    // RGB24 window (a caller's contract: the columns outside are black): tiles
+    // outside it store nothing; windows are 16-pixel aligned
+    const int pitch = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcols : F.W;
+    const int wc0 = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcol0 : 0;
+    if (u0 + nu <= wc0 || u0 >= wc0 + pitch) return;   // whole workgroup
     const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
@@ -617,10 +622,10 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
         if (tx < nu && ty < nv) {
             const uint32_t px = put_pixel(v3(0.0f, 0.0f, 0.0f));
-            const size_t o = (size_t)(L0 + ty) * F.W + u0 + tx;
             if (F.out_fmt == CG_PIX_ARGB8888) {
-                out[o] = px;
+                out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
             } else {
+                const size_t o = (size_t)(L0 + ty) * pitch + (u0 - wc0) + tx;
                 out8[3 * o] = (uint8_t)px;
                 out8[3 * o + 1] = (uint8_t)(px >> 8);
                 out8[3 * o + 2] = (uint8_t)(px >> 16);
@@ -720,7 +725,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         __shared__ uint32_t s_px[kLatTileH * kLatTileW];
         if (have) s_px[ty * kLatTileW + tx] = px;
         __syncthreads();
-        if (nu == kLatTileW && (F.W & 3) == 0 && ((uintptr_t)out8 & 3) == 0) {
+        if (nu == kLatTileW && (pitch & 3) == 0 && ((uintptr_t)out8 & 3) == 0) {
             const int t = threadIdx.x, row = t / 12, j = t - 12 * row;
             if (row < nv) {
                 uint32_t w = 0u;
@@ -729,10 +734,10 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
                     const int byte = 4 * j + b, p = byte / 3, ch = byte - 3 * p;
                     w |= ((s_px[row * kLatTileW + p] >> (8 * ch)) & 0xffu) << (8 * b);
                 }
-                *(uint32_t *)(out8 + ((size_t)(L0 + row) * F.W + u0) * 3 + 4 * j) = w;
+                *(uint32_t *)(out8 + ((size_t)(L0 + row) * pitch + (u0 - wc0)) * 3 + 4 * j) = w;
             }
         } else if (have) {
-            uint8_t *q = out8 + ((size_t)(L0 + ty) * F.W + u0 + tx) * 3;
+            uint8_t *q = out8 + ((size_t)(L0 + ty) * pitch + (u0 - wc0) + tx) * 3;
             q[0] = (uint8_t)px;
             q[1] = (uint8_t)(px >> 8);
             q[2] = (uint8_t)(px >> 16);
@@ -749,25 +754,29 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
 #endif
 }
 
-// ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): four
+// ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): rows
+// of W pixels -> rows of the window's wcols pixels (columns wcol0 ..), four
 // pixels per lane, three dwords out when aligned.
-__global__ void rt_pack_rgb24_kernel(const uint32_t *__restrict__ src, size_t n_px, uint8_t *__restrict__ dst)
+__global__ void rt_pack_rgb24_kernel(const uint32_t *__restrict__ src, int W, int rows, int wcol0, int wcols,
+                                     uint8_t *__restrict__ dst)
 {
-    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x, i = 4 * q;
-    if (i >= n_px) return;
-    if (i + 4 <= n_px && ((uintptr_t)(dst + 3 * i) & 3) == 0) {
-        const uint4 p = *(const uint4 *)(src + i);
-        uint32_t *d = (uint32_t *)(dst + 3 * i);
-        d[0] = (p.x & 0xffffffu) | (p.y << 24);
-        d[1] = ((p.y >> 8) & 0xffffu) | (p.z << 16);
-        d[2] = ((p.z >> 16) & 0xffu) | ((p.w & 0xffffffu) << 8);
+    const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x), y = blockIdx.y;
+    if (x >= wcols || y >= rows) return;
+    const uint32_t *s = src + (size_t)y * W + wcol0 + x;
+    uint8_t *d = dst + ((size_t)y * wcols + x) * 3;
+    if (x + 4 <= wcols && ((uintptr_t)d & 3) == 0 && ((uintptr_t)s & 15) == 0) {
+        const uint4 p = *(const uint4 *)s;
+        uint32_t *dw = (uint32_t *)d;
+        dw[0] = (p.x & 0xffffffu) | (p.y << 24);
+        dw[1] = ((p.y >> 8) & 0xffffu) | (p.z << 16);
+        dw[2] = ((p.z >> 16) & 0xffu) | ((p.w & 0xffffffu) << 8);
         return;
     }
-    for (size_t k = i; k < n_px && k < i + 4; ++k) {
-        const uint32_t p = src[k];
-        dst[3 * k] = (uint8_t)p;
-        dst[3 * k + 1] = (uint8_t)(p >> 8);
-        dst[3 * k + 2] = (uint8_t)(p >> 16);
+    for (int k = 0; k < 4 && x + k < wcols; ++k) {
+        const uint32_t p = s[k];
+        d[3 * k] = (uint8_t)p;
+        d[3 * k + 1] = (uint8_t)(p >> 8);
+        d[3 * k + 2] = (uint8_t)(p >> 16);
     }
 }
 
@@ -786,13 +795,19 @@ __global__ void rt_assemble_kernel(const uint8_t *__restrict__ src, RtBlocks B, 
     const size_t srow = (size_t)nframes * B.cum[b] + (size_t)f * B.rows[b] + l;   // row index in src
     uint32_t *d = frames + (size_t)f * frame_stride + (size_t)g * B.W + x;
     const int n = min(4, B.W - x);
+    const int wc0 = B.wcols ? B.wcol0 : 0, pitch = B.wcols ? B.wcols : B.W;
+    if (x < wc0 || x >= wc0 + pitch) {   // outside the window: PutPixelSDL(0, 0, 0)
+        for (int k = 0; k < n; ++k) d[k] = 0x80000000u;
+        return;
+    }
+    const int xs = x - wc0;              // column in the source row (windows are 4-aligned)
     if (B.bpp == 4) {
-        const uint32_t *s4 = (const uint32_t *)src + srow * B.W + x;
+        const uint32_t *s4 = (const uint32_t *)src + srow * pitch + xs;
         if (n == 4 && ((uintptr_t)s4 & 15) == 0 && ((uintptr_t)d & 15) == 0) *(uint4 *)d = *(const uint4 *)s4;
         else for (int k = 0; k < n; ++k) d[k] = s4[k];
         return;
     }
-    const uint8_t *s3 = src + (srow * B.W + x) * 3;
+    const uint8_t *s3 = src + (srow * pitch + xs) * 3;
     if (n == 4 && ((uintptr_t)s3 & 3) == 0 && ((uintptr_t)d & 15) == 0) {
         const uint32_t a = ((const uint32_t *)s3)[0], bb = ((const uint32_t *)s3)[1], c = ((const uint32_t *)s3)[2];
         *(uint4 *)d = make_uint4(0x80000000u | (a & 0xffffffu), 0x80000000u | (a >> 24) | ((bb & 0xffffu) << 8),
@@ -1011,12 +1026,12 @@ bool rt_lat_stamps(unsigned long long out[8], hipStream_t st)
 #endif
 }
 
-hipError_t launch_rt_pack_rgb24(const uint32_t *d_src, size_t n_px, uint8_t *d_dst, hipStream_t st)
+hipError_t launch_rt_pack_rgb24(const uint32_t *d_src, int W, int rows, int wcol0, int wcols, uint8_t *d_dst,
+                                hipStream_t st)
 {
-    const size_t groups = (n_px + 3) / 4;
-    if (!groups) return hipSuccess;
-    hipLaunchKernelGGL(rt_pack_rgb24_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, d_src, n_px,
-                       d_dst);
+    if (rows <= 0 || wcols <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_pack_rgb24_kernel, dim3(((wcols + 3) / 4 + 255) / 256, rows), dim3(256), 0, st, d_src, W,
+                       rows, wcol0, wcols, d_dst);
     return hipGetLastError();
 }
 

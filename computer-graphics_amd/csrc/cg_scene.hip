@@ -2,6 +2,8 @@
 //   raytracer/Source/TestModelH.h:121-279  (28 triangles + 1 sphere)
 //   rasteriser/Source/TestModelH.h:48-312  (room 10 + boxes 20, setting = settingBoxes = 0)
 // Vertex scaling and normals use the reference's float ops exactly.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "cg_internal.h"
@@ -209,4 +211,70 @@ extern "C" int cg_rt_random_scene(uint64_t seed, int n, cg_tri *out)
         compute_normal(t);
     }
     return n;
+}
+
+// Columns an unrotated camera can see anything in (include/cg_render.h).  A
+// ray of image x-offset X = u - W/2 + i/2 (i = -1, 0, 1) meets the plane
+// z = cz + s at x = cx + s X / f; it can reach a point of the scene's box only
+// if X lies between the extreme projections f (px - cx) / (pz - cz) of the
+// box's corners (all with pz - cz > 0).  FP64, widened by two pixels.
+extern "C" int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int n_spheres,
+                                   const cg_rt_camera *cam, int *col0, int *col1)
+{
+    if (!cam || !col0 || !col1 || n_tris < 0 || n_spheres < 0 || (n_tris && !tris) || (n_spheres && !spheres) ||
+        cam->width <= 0)
+        return CG_E_INVALID;
+    const int W = cam->width;
+    *col0 = 0;
+    *col1 = W;
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            if (cam->R[4 * c + r] != (r == c ? 1.0f : 0.0f)) return CG_OK;   // rotated: whole width
+    if (n_tris == 0 && n_spheres == 0) {   // nothing to see
+        *col1 = 0;
+        return CG_OK;
+    }
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    auto add = [&](double x, double y, double z, double r) {
+        const double p[3] = {x, y, z};
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], p[k] - r);
+            hi[k] = std::max(hi[k], p[k] + r);
+        }
+    };
+    for (int i = 0; i < n_tris; ++i) {
+        const cg_vec4 *v[3] = {&tris[i].v0, &tris[i].v1, &tris[i].v2};
+        for (const cg_vec4 *q : v) add(q->x, q->y, q->z, 0.0);
+    }
+    for (int i = 0; i < n_spheres; ++i)
+        add(spheres[i].centre.x, spheres[i].centre.y, spheres[i].centre.z,
+            std::sqrt((double)spheres[i].radiusSquared) * (1.0 + 1e-6));
+    const double m = 0.02 * (1.0 + std::max({std::fabs(lo[0]), std::fabs(lo[1]), std::fabs(lo[2]), std::fabs(hi[0]),
+                                               std::fabs(hi[1]), std::fabs(hi[2])}));
+    for (int k = 0; k < 3; ++k) {
+        lo[k] -= m;
+        hi[k] += m;
+    }
+    const double cx = cam->camera.x, cz = cam->camera.z, f = cam->focal;
+    if (!(lo[2] - cz > 1e-6) || !(f > 0) || !std::isfinite(f)) return CG_OK;   // box reaches behind the camera
+    double xmin = 1e300, xmax = -1e300;
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            const double X = f * ((a ? hi[0] : lo[0]) - cx) / ((b ? hi[2] : lo[2]) - cz);
+            xmin = std::min(xmin, X);
+            xmax = std::max(xmax, X);
+        }
+    if (!(std::isfinite(xmin) && std::isfinite(xmax))) return CG_OK;
+    // pixel u's sub-rays have X in [u - W/2 - 0.5, u - W/2 + 0.5]
+    const double u0 = std::floor(xmin + W / 2 - 0.5) - 2.0, u1 = std::ceil(xmax + W / 2 + 0.5) + 3.0;
+    int a = (int)std::max(0.0, std::min((double)W, u0)), b = (int)std::max(0.0, std::min((double)W, u1));
+    a = (a / 16) * 16;
+    b = std::min(W, ((b + 15) / 16) * 16);
+    if (a >= b) {
+        *col0 = *col1 = 0;
+        return CG_OK;
+    }
+    *col0 = a;
+    *col1 = b;
+    return CG_OK;
 }

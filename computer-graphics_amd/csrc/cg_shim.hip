@@ -31,7 +31,7 @@ bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vecto
 size_t rt_big_scratch_bytes(const RtFrame &);
 void rt_big_diag(const RtFrame &, void *, hipStream_t);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
-hipError_t launch_rt_pack_rgb24(const uint32_t *, size_t, uint8_t *, hipStream_t);
+hipError_t launch_rt_pack_rgb24(const uint32_t *, int, int, int, int, uint8_t *, hipStream_t);
 hipError_t launch_rt_assemble(const uint8_t *, const RtBlocks &, int, uint32_t *, size_t, hipStream_t);
 hipError_t launch_rt_probe_closest(const RtFrame &, const cg_tri *, const RtSphere *,
                                    const cg_vec4 *, const cg_vec4 *, int, cg_isect *, int *,
@@ -304,7 +304,7 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     F.n_tris = c->n_tris;
     F.n_sph = c->n_sph;
     F.nbound = c->nbound;
-    cg_rt_shard one{0, 1, kRtTileH, 0, 0};
+    cg_rt_shard one{0, 1, kRtTileH, 0, 0, 0, 0};
     const cg_rt_shard *s = shard ? shard : &one;
     if (s->rows > 0) {   // band: rows row0 .. row0 + rows - 1
         if (s->row0 < 0) return CG_E_INVALID;
@@ -322,6 +322,13 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
         F.rows_out = cg_rt_shard_rows(F.H, s);
     }
     F.out_fmt = CG_PIX_ARGB8888;
+    if (s->cols < 0 || s->col0 < 0) return CG_E_INVALID;
+    if (s->cols > 0) {   // RGB24 window (checked against the format by the caller)
+        if (s->col0 % 16 || s->col0 + s->cols > F.W || (s->cols % 16 && s->col0 + s->cols != F.W))
+            return CG_E_INVALID;
+        F.wcol0 = s->col0;
+        F.wcols = s->cols;
+    }
     static int cull = [] {
         const char *e = getenv("CG_RT_CULL");
         return e ? atoi(e) : 2;
@@ -334,7 +341,7 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
 
 extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
 {
-    cg_rt_shard one{0, 1, kRtTileH, 0, 0};
+    cg_rt_shard one{0, 1, kRtTileH, 0, 0, 0, 0};
     const cg_rt_shard *s = shard ? shard : &one;
     if (height <= 0) return CG_E_INVALID;
     if (s->rows > 0) return s->rows;
@@ -371,7 +378,8 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t 
     }
     int rc = rt_enqueue_kernels(c, F, d_out, st);
     if (rc || !pack) return rc;
-    CG_TRY(c, launch_rt_pack_rgb24(d_out, (size_t)F.rows_out * F.W, (uint8_t *)d_out_v, st), "pack launch");
+    CG_TRY(c, launch_rt_pack_rgb24(d_out, F.W, F.rows_out, Fin.wcols ? Fin.wcol0 : 0, Fin.wcols ? Fin.wcols : F.W,
+                                   (uint8_t *)d_out_v, st), "pack launch");
     return CG_OK;
 }
 
@@ -414,6 +422,7 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     int rc = fill_frame(c, lights, n_lights, cam, shard, st, F);
     if (rc) return rc;
+    if (F.wcols) return CG_E_INVALID;   // windows are for the RGB24 wire format
     return rt_enqueue(c, F, d_out, st);
 }
 
@@ -511,7 +520,8 @@ extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int
     int rc = fill_frame(c, lights, n_lights, &cams[0], shard, st, F);
     if (rc) return rc;
     F.out_fmt = pix_format;
-    const size_t px = (size_t)F.rows_out * F.W;
+    if (F.wcols && pix_format != CG_PIX_RGB24) return CG_E_INVALID;
+    const size_t px = (size_t)F.rows_out * (F.wcols ? F.wcols : F.W);
     const size_t stride = frame_stride ? frame_stride : px;   // pixels
     if (stride < px) return CG_E_INVALID;
     uint8_t *out = (uint8_t *)d_out;
@@ -544,8 +554,9 @@ extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int
 
 extern "C" int cg_rt_assemble_device(cg_ctx *c, const void *d_src, int pix_format, const int *row0,
                                      const int *rows, int n_blocks, int width, int height, int n_frames,
-                                     uint32_t *d_frames, size_t frame_stride, void *stream)
+                                     uint32_t *d_frames, size_t frame_stride, int col0, int cols, void *stream)
 {
+    if (cols < 0 || col0 < 0 || (cols > 0 && (col0 % 4 || cols % 4 || col0 + cols > width))) return CG_E_INVALID;
     if (!c || !d_src || !d_frames || !row0 || !rows || n_blocks < 1 || n_blocks > kMaxBlocks || width <= 0 ||
         height <= 0 || n_frames < 1 || n_frames > 65535)
         return CG_E_INVALID;
@@ -557,6 +568,8 @@ extern "C" int cg_rt_assemble_device(cg_ctx *c, const void *d_src, int pix_forma
     B.W = width;
     B.H = height;
     B.bpp = (int)pix_bytes(pix_format);
+    B.wcol0 = col0;
+    B.wcols = cols;
     B.cum[0] = 0;
     for (int b = 0; b < n_blocks; ++b) {
         if (rows[b] < 0 || row0[b] < 0) return CG_E_INVALID;
@@ -605,7 +618,7 @@ extern "C" int cg_rt_unstripe_batch_device(cg_ctx *c, const uint32_t *d_gathered
     if (!c || !d_gathered || !d_frames || width <= 0 || height <= 0 || nranks < 1 || stripe_h <= 0 ||
         nframes < 1 || nframes > 65535)
         return CG_E_INVALID;
-    cg_rt_shard s{0, nranks, stripe_h, 0, 0};
+    cg_rt_shard s{0, nranks, stripe_h, 0, 0, 0, 0};
     int rows = cg_rt_shard_rows(height, &s);
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     CG_TRY(c, launch_rt_unstripe(d_gathered, width, height, nranks, stripe_h, rows, nframes, d_frames,

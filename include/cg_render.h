@@ -64,8 +64,12 @@ typedef struct {
  * stripe_h >= 1 is exact; for speed use a multiple of 15 for the unrotated
  * one-light camera (the lattice kernel's tile height) and of 8 otherwise.
  * Band (rows > 0): this shard renders frame rows row0 .. row0 + rows - 1
- * (rows past the frame are padding); rank / nranks / stripe_h are ignored. */
-typedef struct { int rank, nranks, stripe_h; int row0, rows; } cg_rt_shard;
+ * (rows past the frame are padding); rank / nranks / stripe_h are ignored.
+ * Window (cols > 0, CG_PIX_RGB24 output only): only columns col0 .. col0 +
+ * cols - 1 are stored, rows `cols` pixels apart -- the caller asserts the other
+ * columns are black (cg_rt_frame_columns); col0 and cols are multiples of 16
+ * (cols may end at the frame's right edge). */
+typedef struct { int rank, nranks, stripe_h; int row0, rows; int col0, cols; } cg_rt_shard;
 
 /* Pixel formats of device outputs.  ARGB8888 is PutPixelSDL's uint32
  * (SDLauxiliary.h:149-161).  RGB24 is its wire form for transfers between
@@ -160,10 +164,24 @@ int cg_rt_render_frames_device(cg_ctx *ctx, const cg_light *lights, int n_lights
  * blocks in order, block b = n_frames x rows[b] rows of `width` pixels in
  * pix_format, landing at frame rows row0[b] .. row0[b] + rows[b] - 1 (rows
  * outside the frame are skipped) of frame f = d_frames + f * frame_stride
- * pixels (ARGB8888).  row0 / rows are host arrays, n_blocks <= 64. */
+ * pixels (ARGB8888).  With cols > 0 the source rows hold only the window
+ * columns col0 .. col0 + cols - 1 (4-aligned) and the rest of each row is set
+ * to 0x80000000.  row0 / rows are host arrays, n_blocks <= 64. */
 int cg_rt_assemble_device(cg_ctx *ctx, const void *d_src, int pix_format, const int *row0, const int *rows,
                           int n_blocks, int width, int height, int n_frames, uint32_t *d_frames,
-                          size_t frame_stride, void *stream);
+                          size_t frame_stride, int col0, int cols, void *stream);
+/* The columns an unrotated camera can see anything in: every sub-ray of the
+ * pixels outside [*col0, *col1) certainly misses all triangles and spheres,
+ * so those pixels are PutPixelSDL(0, 0, 0) = 0x80000000 (skeleton.cpp:160-166).
+ * From the scene's bounding box widened by 0.02 (every accepted float hit
+ * lies within ~1e-6 relative of its triangle and within 4e-3 |cameraPos -
+ * centre| of its sphere), projected through the pinhole (the projection of a
+ * box in front of the camera lies in the hull of its corners' projections),
+ * plus 2 pixels, rounded out to 16-pixel boundaries.  Returns the full width
+ * for rotated cameras or when the box reaches behind the camera.  Host-only
+ * (no device work), usable to crop CG_PIX_RGB24 transfers (cg_rt_shard). */
+int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int n_spheres,
+                        const cg_rt_camera *cam, int *col0, int *col1);
 /* Rows a shard renders (including padding rows of its last stripe). */
 int cg_rt_shard_rows(int height, const cg_rt_shard *shard);
 /* Reassemble a frame from gathered shards: d_gathered holds nranks blocks of

@@ -91,23 +91,29 @@ def _band_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        full = oracle.rt_draw(oracle.rt_params(W, H, F)).reshape(H, W)
+        Fb = 40.0   # a focal length at which the scene leaves black columns to crop
+        full = oracle.rt_draw(oracle.rt_params(W, H, Fb)).reshape(H, W)
         bands = cgdist.rebalance(cgdist.equal_bands(H, world), [1.0 + 0.7 * r for r in range(world)],
                                  [0.3] + [0.0] * (world - 1), H)
         r0, nr = bands[rank]
         mine = full[r0:r0 + nr].reshape(-1)
+        # the RGB24 window: columns the camera can see anything in
+        import cgamd
+        t_, n_, s_ = cgamd.rt_scene()
+        c0, c1 = cgamd.frame_columns(t_, n_, s_, 1, cgamd.rt_camera(W, H, Fb))
+        cols = c1 - c0
         if rank == 0:
             frames = np.zeros((1, H * W), np.uint32)
             frames[0, r0 * W:(r0 + nr) * W] = mine
             parts = []
             for p in range(1, world):
-                buf = torch.empty(bands[p][1] * W * 3, dtype=torch.uint8)
+                buf = torch.empty(bands[p][1] * cols * 3, dtype=torch.uint8)
                 dist.recv(buf, src=p)
                 parts.append(buf.numpy())
-            cgdist.assemble_np(np.concatenate(parts), 3, bands[1:], W, H, 1, frames)
-            q.put(bool(np.array_equal(frames[0], full.reshape(-1))))
+            cgdist.assemble_np(np.concatenate(parts), 3, bands[1:], W, H, 1, frames, col0=c0, cols=cols)
+            q.put(bool(np.array_equal(frames[0], full.reshape(-1))) and 0 < cols < W)
         else:
-            dist.send(torch.from_numpy(cgdist.pack_rgb24_np(mine)), dst=0)
+            dist.send(torch.from_numpy(cgdist.pack_rgb24_np(cgdist.window_np(mine, W, c0, cols))), dst=0)
     finally:
         dist.destroy_process_group()
 

@@ -169,8 +169,9 @@ def test_rt_render_frames_batched(rt, golden):
             assert np.array_equal(frame, singles[k]), (S, n, k)
 
 
+@pytest.mark.parametrize("window", [False, True])
 @pytest.mark.parametrize("kind", ["lattice", "yaw", "c4"])
-def test_rt_bands_rgb24_assemble(rt, kind):
+def test_rt_bands_rgb24_assemble(rt, kind, window):
     """bench.py's N > 1 layout on one GPU: uneven bands, rank 0's band rendered
     ARGB straight into the frames, the others in the RGB24 wire format into
     one buffer, cg_rt_assemble_device expands them: == each frame whole."""
@@ -192,25 +193,51 @@ def test_rt_bands_rgb24_assemble(rt, kind):
     st = torch.cuda.Stream()
     frames = torch.zeros(K * H * W, dtype=torch.int32, device="cuda")
     r0, nr = bands[0]
+    # RGB24 window: the columns the camera can see anything in (cg_rt_frame_columns)
+    c0, cols = 0, 0
+    if window:
+        t_, n_, s_ = cgamd.rt_scene()
+        c0, c1 = cgamd.frame_columns(t_, n_, s_, 1, cams[0])
+        cols = c1 - c0 if c1 - c0 < W else 0
+        if kind != "yaw":
+            assert 0 < cols < W
+    pitch = cols or W
+    frames.fill_(-1)                                  # the assembly must write every pixel
     rt.rt_render_frames_device(cams, frames.data_ptr() + 4 * r0 * W, cgamd.RtShard(row0=r0, rows=nr),
                                st.cuda_stream, lights, frame_stride=H * W)
     rbuf = torch.zeros(K * H * W * 3 + 64, dtype=torch.uint8, device="cuda")
     off = 0
     for a, n in bands[1:]:
-        rt.rt_render_frames_device(cams, rbuf.data_ptr() + off, cgamd.RtShard(row0=a, rows=n), st.cuda_stream,
-                                   lights, pix_format=cgamd.PIX_RGB24)
-        off += K * n * W * 3
+        rt.rt_render_frames_device(cams, rbuf.data_ptr() + off, cgamd.RtShard(row0=a, rows=n, col0=c0, cols=cols),
+                                   st.cuda_stream, lights, pix_format=cgamd.PIX_RGB24)
+        off += K * n * pitch * 3
     rt.rt_assemble_device(rbuf.data_ptr(), cgamd.PIX_RGB24, [a for a, _ in bands[1:]], [n for _, n in bands[1:]],
-                          W, H, K, frames.data_ptr(), 0, st.cuda_stream)
+                          W, H, K, frames.data_ptr(), 0, st.cuda_stream, col0=c0, cols=cols)
     st.synchronize()
     got = frames.cpu().numpy().view(np.uint32).reshape(K, -1)
     for k in range(K):
-        assert np.array_equal(got[k], singles[k]), (kind, k)
-    # the wire bytes are exactly the low three bytes of each pixel
+        assert np.array_equal(got[k], singles[k]), (kind, window, k)
+    # the wire bytes are exactly the low three bytes of each pixel (of the window)
     a, n = bands[1]
-    wire = rbuf[:K * n * W * 3].cpu().numpy()
-    want = np.concatenate([cgdist.pack_rgb24_np(s_[a * W:(a + n) * W]) for s_ in singles])
+    wire = rbuf[:K * n * pitch * 3].cpu().numpy()
+    want = np.concatenate([cgdist.pack_rgb24_np(cgdist.window_np(s_[a * W:(a + n) * W], W, c0, pitch))
+                           for s_ in singles])
     assert np.array_equal(wire, want)
+
+
+def test_rt_window_validation(rt):
+    """Windows only for RGB24, 16-aligned, inside the frame."""
+    torch = pytest.importorskip("torch")
+    cam = cgamd.rt_camera(320, 256, 256.0)
+    buf = torch.zeros(320 * 256, dtype=torch.int32, device="cuda")
+    for sh, fmt in ((cgamd.RtShard(row0=0, rows=8, col0=16, cols=64), cgamd.PIX_ARGB8888),
+                    (cgamd.RtShard(row0=0, rows=8, col0=8, cols=64), cgamd.PIX_RGB24),
+                    (cgamd.RtShard(row0=0, rows=8, col0=16, cols=20), cgamd.PIX_RGB24),
+                    (cgamd.RtShard(row0=0, rows=8, col0=304, cols=32), cgamd.PIX_RGB24)):
+        with pytest.raises(RuntimeError):
+            rt.rt_render_frames_device([cam], buf.data_ptr(), sh, None, pix_format=fmt)
+    with pytest.raises(RuntimeError):
+        rt.rt_render_device(cam, buf.data_ptr(), cgamd.RtShard(row0=0, rows=8, col0=16, cols=64))
 
 
 def test_rt_assemble_argb_and_ragged(rt):

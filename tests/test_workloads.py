@@ -61,3 +61,31 @@ def test_starfield_init_and_update_match_oracle():
         cgamd.starfield_update(a, dt)
         oracle.starfield_update(b, dt)
         assert a.tobytes() == b.tobytes(), dt
+
+
+def test_frame_columns_only_black_outside():
+    """cg_rt_frame_columns (host-only): every pixel outside the returned columns
+    of the oracle's frame is PutPixelSDL(0,0,0) = 0x80000000 -- the contract the
+    multi-GPU RGB24 window relies on -- at several cameras, focal lengths and a
+    random scene; rotated cameras get the whole width."""
+    import os
+    tris, n, sph = cgamd.rt_scene()
+    threads = min(8, os.cpu_count() or 1)
+    cases = [(320, 256, 256.0, (0.0, 0.0, -3.0, 1.0)), (480, 270, 270.0, (0.0, 0.0, -3.0, 1.0)),
+             (320, 256, 400.0, (0.2, -0.1, -2.5, 1.0)), (256, 144, 144.0, (0.0, 0.0, -3.0, 1.0))]
+    for W, H, f, c in cases:
+        c0, c1 = cgamd.frame_columns(tris, n, sph, 1, cgamd.rt_camera(W, H, f, c))
+        assert 0 <= c0 < c1 <= W and c0 % 16 == 0 and (c1 % 16 == 0 or c1 == W)
+        frame = oracle.rt_draw(oracle.rt_params(W, H, f, c), threads=threads).reshape(H, W)
+        outside = np.concatenate([frame[:, :c0].ravel(), frame[:, c1:].ravel()])
+        assert np.all(outside == 0x80000000), (W, H, f, c)
+        assert c0 > 0 or c1 < W or f >= 400.0      # it does crop the default framings
+    rs = cgamd.random_scene(2000, 0x5EED)
+    c0, c1 = cgamd.frame_columns(rs, 2000, None, 0, cgamd.rt_camera(256, 144, 144.0))
+    ors = oracle.rt_random_scene(0x5EED, 2000)
+    frame = oracle.rt_draw(oracle.rt_params(256, 144, 144.0), scene=(ors, 2000, None, 0), threads=threads)
+    frame = frame.reshape(144, 256)
+    assert np.all(frame[:, :c0] == 0x80000000) and np.all(frame[:, c1:] == 0x80000000)
+    assert cgamd.frame_columns(tris, n, sph, 1, cgamd.rt_camera(320, 256, 256.0, R=cgamd.yaw_matrix(0.1))) == (0, 320)
+    # camera inside the box: no crop
+    assert cgamd.frame_columns(tris, n, sph, 1, cgamd.rt_camera(320, 256, 256.0, (0.0, 0.0, 0.0, 1.0))) == (0, 320)
