@@ -337,7 +337,10 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
                     sphere = true;
                     sphere_hit_box(sph[q], camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi);
                 }
-        const unsigned long long m = seg_or((keep ? (1ull << k) : 0ull) | (sphere ? (1ull << 63) : 0ull), cp);
+        unsigned long long m = seg_or((keep ? (1ull << k) : 0ull) | (sphere ? (1ull << 63) : 0ull), cp);
+        // bit 62: the tile's only candidate is one triangle that every ray
+        // certainly hits -- the lattice kernel then skips the u, v tests
+        const unsigned long long cov = seg_or((keep && primary_covers(c, pd)) ? (1ull << k) : 0ull, cp);
         float blo[3], bhi[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
@@ -357,7 +360,8 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
         const unsigned long long ownm = seg_or(own ? (1ull << k) : 0ull, cp);
         if (tl < kT && ci == 0) {
             const bool live = tile_of(tl, t, G);
-            s_pm[tl] = live ? m : 0ull;
+            const bool single = m != 0ull && (m & (m - 1ull)) == 0ull && !(m >> 63);
+            s_pm[tl] = live ? (m | ((single && (cov & m)) ? (1ull << 62) : 0ull)) : 0ull;
             s_own[tl] = ownm;
             for (int q = 0; q < 3; ++q) {
                 s_box[tl][q] = blo[q];
@@ -611,7 +615,8 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
-    const unsigned long long mask = m0 & ~(1ull << 63), smask = s0 & ~(1ull << 63);
+    const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
+    const bool covered = (m0 >> 62) & 1ull;   // one triangle, hit by every ray of the tile (certified)
     RtFrame Fp = F;                        // pass 1: spheres only where one may be hit
     if (!(m0 >> 63)) Fp.n_sph = 0;
     RtFrame Fs = F;                        // pass 2: spheres only where one may block a shadow ray
@@ -654,7 +659,26 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         }
         int bi[NP];
         float t[NP];
-        closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t);                       // :140
+        if (covered) {
+            // the tile's one candidate triangle k is certainly accepted by every
+            // ray (rt_tile_cert_kernel: t > 0, u, v inside, nothing else can be
+            // hit): the reference's closest hit is k with t = detT / det (:306),
+            // formed with closest_primary_n's float ops; the u, v tests and the
+            // distance are not needed
+            const int k = __builtin_ctzll(mask);
+            const RtTri c = tc[k];
+#pragma unroll
+            for (int n = 0; n < NP; ++n) {
+                const vec3 nd = -v3(X[n], Y[n], F.focal);
+                const float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+                const float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+                const float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;   // :289
+                t[n] = c.detT / det;                                         // :306
+                bi[n] = k;
+            }
+        } else {
+            closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t);                   // :140
+        }
 #pragma unroll
         for (int n = 0; n < NP; ++n) {
             if (!live[n]) continue;
@@ -969,7 +993,7 @@ bool rt_use_lattice(const RtFrame &F)
         const char *e = getenv("CG_RT_LATTICE");
         return !e || atoi(e) != 0;
     }();
-    return lattice_on && F.n_tris > 0 && F.n_tris <= 63 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
+    return lattice_on && F.n_tris > 0 && F.n_tris <= 62 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
 }
 
 size_t rt_lattice_tiles(const RtFrame &F)
