@@ -83,6 +83,13 @@ struct cg_ctx {
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
     DevBuf latmask;                     // lattice tiles' certificates (two masks per tile)
     DevBuf supmask;                     // their super-tiles' certificates (two-level path)
+    // Batched lattice launches pipeline their certificate kernels on `aux`:
+    // call j+1's certificates run beside call j's lattice kernel, each call
+    // with its own slot of buffers (rt_enqueue_lattice_batch).
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_cert[2] = {nullptr, nullptr}, ev_lat[2] = {nullptr, nullptr};
+    int slot = 0;
+    DevBuf ptc[2], pshade[2], plat[2], psup[2];
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
@@ -182,6 +189,13 @@ extern "C" void cg_destroy(cg_ctx *c)
                       &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights, &c->big,
                       &c->gstart, &c->gtris};
     for (DevBuf *b : bufs) b->release();
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
+    for (int k = 0; k < 2; ++k) {
+        c->ptc[k].release(); c->pshade[k].release(); c->plat[k].release(); c->psup[k].release();
+        if (c->ev_cert[k]) (void)hipEventDestroy(c->ev_cert[k]);
+        if (c->ev_lat[k]) (void)hipEventDestroy(c->ev_lat[k]);
+    }
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     rast_release(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -431,27 +445,56 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
                                     void *d_out, size_t stride, hipStream_t st)
 {
+    static const bool pipe = [] {
+        const char *e = getenv("CG_RT_PIPE");
+        return !e || atoi(e) != 0;
+    }();
+    if (pipe && !c->aux) {
+        CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
+        for (int k = 0; k < 2; ++k) {
+            CG_TRY(c, hipEventCreateWithFlags(&c->ev_cert[k], hipEventDisableTiming), "aux event");
+            CG_TRY(c, hipEventCreateWithFlags(&c->ev_lat[k], hipEventDisableTiming), "aux event");
+            CG_TRY(c, hipEventRecord(c->ev_lat[k], c->aux), "aux event");
+        }
+    }
+    // pipelined: this call's slot (its buffers were last read by the lattice
+    // launch two calls ago, ev_lat[k]); otherwise the context's own buffers
+    const int k = c->slot;
+    if (pipe) c->slot ^= 1;
+    DevBuf &btc = pipe ? c->ptc[k] : c->tc, &bsh = pipe ? c->pshade[k] : c->shade;
+    DevBuf &blat = pipe ? c->plat[k] : c->latmask, &bsup = pipe ? c->psup[k] : c->supmask;
     const size_t tiles = rt_lattice_tiles(F);
-    CG_TRY(c, c->latmask.ensure((size_t)nf * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
-    CG_TRY(c, c->tc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
+    CG_TRY(c, blat.ensure((size_t)nf * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
+    CG_TRY(c, btc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
+    CG_TRY(c, bsh.ensure((size_t)std::max(F.n_tris, 1) * sizeof(RtShade)), "alloc tri shading");
     RtFrameCams fc{};
     for (int f = 0; f < nf; ++f) {
         fc.c[f][0] = cams[f].camera.x; fc.c[f][1] = cams[f].camera.y;
         fc.c[f][2] = cams[f].camera.z; fc.c[f][3] = cams[f].camera.w;
     }
-    unsigned long long *lat = (unsigned long long *)c->latmask.p;
+    unsigned long long *lat = (unsigned long long *)blat.p;
     unsigned long long *supm = nullptr;
     if (rt_two_level()) {
-        CG_TRY(c, c->supmask.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)),
+        CG_TRY(c, bsup.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)),
                "alloc super-tile masks");
-        supm = (unsigned long long *)c->supmask.p;
+        supm = (unsigned long long *)bsup.p;
     }
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat, supm),
+    hipStream_t cst = st;
+    if (pipe) {   // certificates on aux, after the slot's previous reader
+        cst = c->aux;
+        CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
+    }
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)btc.p,
+                                (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm),
            "rt_prepare launch");
-    CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
+    if (pipe) {
+        CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
+        CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
+    }
+    CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
                                        (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st),
            "rt_lattice launch");
+    if (pipe) CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
     static const bool diag = getenv("CG_RT_LAT_DIAG") != nullptr;
     if (diag) {   // certificate statistics of frame 0's tiles (diagnostics only: synchronises)
         std::vector<unsigned long long> m(2 * tiles);

@@ -1,5 +1,6 @@
 """A/B timing of libcgamd.so variants on the C2 workload as bench.py runs it
-(16 frames per cg_rt_render_frames_device call).  Each variant runs in its own
+(16 frames per cg_rt_render_frames_device call; us_per_frame synchronises
+after every call, stream_us_per_frame times 8 calls back to back).  Each variant runs in its own
 process (CGAMD_LIB), rounds interleaved; prints the median us per frame and
 whether frame 0 equals the golden C2 frame.
 usage: python scripts/rt_ab16.py [lib.so ...]   (default: the in-tree build)"""
@@ -24,9 +25,16 @@ for _ in range({reps}):
     a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
     a.record(st); ctx.rt_render_frames_device(cams, buf.data_ptr(), None, st.cuda_stream); b.record(st)
     b.synchronize(); ts.append(a.elapsed_time(b))
+bs = []   # back-to-back calls (what bench.py times): certificates overlap
+for _ in range(5):
+    a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(8): ctx.rt_render_frames_device(cams, buf.data_ptr(), None, st.cuda_stream)
+    b.record(st); b.synchronize(); bs.append(a.elapsed_time(b))
 f0 = buf[:1920 * 1080].cpu().numpy().view(np.uint32)
 want = json.load(open({golden!r}))["rt"]["rt_1920x1080_f1080"]["argb_sha256"]
 print(json.dumps(dict(us_per_frame=float(np.median(ts)) * 1e3 / K, min=float(np.min(ts)) * 1e3 / K,
+                      stream_us_per_frame=float(np.median(bs)) * 1e3 / (8 * K),
                       exact=hashlib.sha256(f0.tobytes()).hexdigest() == want)))
 """
 
