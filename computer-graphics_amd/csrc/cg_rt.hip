@@ -567,8 +567,76 @@ __device__ unsigned int cg_lat_stamps[kStampWaves][6];
     do {              \
     } while (0)
 #endif
+#ifdef CG_RT_SHADOW_STATS
+// Diagnostic builds: pass-2 wave steps by shadow class (all lit / all shadowed
+// / mixed) and shadow-loop iterations now vs. with the best single blocker first.
+__device__ unsigned long long cg_shadow_stats[8];
+#endif
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
+
+#ifndef CG_RT_LAT_PAIR2
+#define CG_RT_LAT_PAIR2 0   // 1: pass 2 takes two lattice points per lane per step (measured 12% slower: 69 VGPRs)
+#endif
+// Pass 2 of rt_lattice_kernel for lattice points p and p + 64: DirectLight
+// (skeleton.cpp:366-415, as direct_light<true> with light 0) of each point
+// that hit, written over its LDS slot.  The shadow loop walks the tile's
+// candidates once for both points; each point stops at its first blocker.
+__device__ __forceinline__ void direct_light_pair(const RtFrame &F, const RtTri *__restrict__ tc,
+                                                  const RtShade *__restrict__ shade,
+                                                  const RtSphere *__restrict__ sph, float4 *s_pt,
+                                                  unsigned long long smask, int p, int p_hi, int cols, int ax0,
+                                                  int ay0)
+{
+    const RtLight Lt = F.lights[0];
+    const vec3 lp = v3(Lt.x, Lt.y, Lt.z);
+    bool hit[2], done[2];
+    int bi[2], pp[2];
+    vec3 pos[2], r[2], normal[2], origin[2];
+    float rmag[2], len[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        pp[n] = p + 64 * n;
+        const int cy = pp[n] / kLatW, cx = pp[n] - cy * kLatW;
+        float4 q = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(INT_MIN));
+        if (pp[n] < p_hi && cx < cols) q = s_pt[pp[n]];
+        bi[n] = __float_as_int(q.w);
+        hit[n] = bi[n] != INT_MIN;
+        const int b = hit[n] ? bi[n] : 0;
+        const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy), t = q.x;
+        pos[n] = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
+        r[n] = lp - pos[n];                                               // :370
+        rmag[n] = light_rmag(r[n]);                                       // :371
+        normal[n] = hit_normal(shade, sph, b, pos[n]);                    // :377-387
+        origin[n] = pos[n] + normal[n] * 0.00001f;                        // :394
+        len[n] = length(r[n]);
+        done[n] = !hit[n];
+    }
+    bool shadow[2] = {false, false};
+    unsigned long long m = smask;
+    while (m != 0ull && !(done[0] && done[1])) {                         // :394-398
+        const int k = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const RtTri c = tc[k];
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+            if (!done[n] && tri_shadow_hit(c, origin[n], -r[n], len[n], rmag[n])) shadow[n] = done[n] = true;
+    }
+    for (int k = 0; k < F.n_sph; ++k) {
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            float ts;
+            if (!done[n] && sphere_intersect(sph[k], origin[n], r[n], ts) && ts < rmag[n]) shadow[n] = done[n] = true;
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        if (!hit[n]) continue;
+        const vec3 dl = shadow[n] ? v3(0.0f, 0.0f, 0.0f)
+                                  : direct_light_lit(Lt, r[n], rmag[n], normal[n], object_colour(shade, sph, bi[n]));
+        s_pt[pp[n]] = make_float4(dl.x, dl.y, dl.z, __int_as_float(bi[n]));
+    }
+}
 
 // blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
 // tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
@@ -700,12 +768,22 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     LAT_STAMP(0);   // pass 1
     // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
     // attributes from the LDS copy
+#if CG_RT_LAT_PAIR2
+    // two points per lane per step (p, p + 64): two independent chains for the
+    // issue slots, one scalar load of each shadow candidate for both
+    for (int p0 = p_lo; p0 < p_hi; p0 += 128)
+        direct_light_pair(Fs, tc, s_shade, sph, s_pt, smask, p0 + lane, p_hi, cols, ax0, ay0);
+#else
 #ifdef CG_ABLATE_SHADE
     if (smask == 12345ull)
 #endif
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
         const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
+#ifdef CG_RT_SHADOW_STATS
+        bool st_act = false;
+        unsigned long long st_blk = 0ull;   // bit j: the j-th candidate (ctz order, spheres last) blocks
+#endif
         if (p < p_hi && cx < cols) {
             const float4 q = s_pt[idx];
             const int bi = __float_as_int(q.w);
@@ -713,11 +791,56 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
                 const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
                 const float t = q.x;
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
+#ifdef CG_RT_SHADOW_STATS
+                {
+                    st_act = true;
+                    const RtLight Lt = Fs.lights[0];
+                    const vec3 r = v3(Lt.x, Lt.y, Lt.z) - pos;
+                    const float rmag = light_rmag(r);
+                    const vec3 o = pos + hit_normal(s_shade, sph, bi, pos) * 0.00001f;
+                    const vec3 nd = -r;
+                    const float len = length(r);
+                    unsigned long long m = smask;
+                    int j = 0;
+                    for (; m; ++j) {
+                        const int k = __builtin_ctzll(m);
+                        m &= m - 1ull;
+                        if (tri_shadow_hit(tc[k], o, nd, len, rmag)) st_blk |= 1ull << j;
+                    }
+                    for (int k = 0; k < Fs.n_sph; ++k, ++j) {
+                        float ts;
+                        if (sphere_intersect(sph[k], o, r, ts) && ts < rmag) st_blk |= 1ull << j;
+                    }
+                }
+#endif
                 const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
                 s_pt[idx] = make_float4(dl.x, dl.y, dl.z, q.w);
             }
         }
+#ifdef CG_RT_SHADOW_STATS
+        {
+            const int ncand = __builtin_popcountll(smask) + Fs.n_sph;
+            const unsigned long long act = __ballot(st_act), shd = __ballot(st_act && st_blk != 0ull);
+            // iterations now: all candidates if any lane is lit, else the latest first blocker
+            int it = st_act && st_blk ? __builtin_ctzll(st_blk) + 1 : 0;
+            for (int o = 32; o; o >>= 1) it = max(it, __shfl_xor(it, o));
+            unsigned long long common = st_act ? st_blk : ~0ull;
+            for (int o = 32; o; o >>= 1) {
+                const unsigned lo = __shfl_xor((unsigned)common, o), hi = __shfl_xor((unsigned)(common >> 32), o);
+                common &= ((unsigned long long)hi << 32) | lo;
+            }
+            if (lane == 0 && act) {
+                const int cls = shd == 0ull ? 0 : (shd == act ? 1 : 2);
+                const int cur = cls == 1 ? it : ncand;
+                atomicAdd(&cg_shadow_stats[cls], 1ull);
+                atomicAdd(&cg_shadow_stats[3 + cls], (unsigned long long)cur);
+                if (cls == 1) atomicAdd(&cg_shadow_stats[6], (unsigned long long)(common ? 1 : cur));
+                atomicAdd(&cg_shadow_stats[7], (unsigned long long)__popcll(act));
+            }
+        }
+#endif
     }
+#endif
     LAT_STAMP(3);   // pass 2
     __syncthreads();
     LAT_STAMP(4);   // pass-2 barrier
@@ -1030,6 +1153,21 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         hipLaunchKernelGGL(rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     return hipGetLastError();
+}
+
+// Diagnostic builds: read and clear the pass-2 shadow statistics.
+bool rt_shadow_stats(unsigned long long out[8], hipStream_t st)
+{
+#ifdef CG_RT_SHADOW_STATS
+    if (hipStreamSynchronize(st) != hipSuccess) return false;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cg_shadow_stats), 64) != hipSuccess) return false;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(cg_shadow_stats), z, 64) == hipSuccess;
+#else
+    (void)out;
+    (void)st;
+    return false;
+#endif
 }
 
 // Diagnostic builds: read and clear the lattice phase stamps (cycles summed over waves).

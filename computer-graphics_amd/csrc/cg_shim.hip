@@ -24,6 +24,7 @@ hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, con
                             const unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
 bool rt_lat_stamps(unsigned long long out[8], hipStream_t st);
+bool rt_shadow_stats(unsigned long long out[8], hipStream_t st);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t);
@@ -537,6 +538,12 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                     }
             }
         }
+        unsigned long long ss[8];
+        if (rt_shadow_stats(ss, st))
+            fprintf(stderr,
+                    "[cg_rt_lattice] pass-2 wave steps lit %llu shadowed %llu mixed %llu; shadow iterations "
+                    "lit %llu shadowed %llu (best-first %llu) mixed %llu; lanes %llu\n",
+                    ss[0], ss[1], ss[2], ss[3], ss[4], ss[6], ss[5], ss[7]);
         unsigned long long ph[8];
         if (rt_lat_stamps(ph, st)) {
             const double waves = (double)nf * tiles * (kRtThreads / 64);
