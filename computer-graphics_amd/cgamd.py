@@ -67,7 +67,7 @@ class RTri(C.Structure):       # rasteriser Triangle, 84 B
 class RastParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", Vec4),
                 ("R", C.c_float * 16), ("light_scene", Vec4), ("light_power", Vec3),
-                ("indirect_first", C.c_float), ("colour_mode", C.c_int), ("pad_", C.c_int),
+                ("indirect_first", C.c_float), ("colour_mode", C.c_int), ("yaw", C.c_float),
                 ("rand_offset", C.c_uint64)]
 
 
@@ -80,6 +80,15 @@ assert C.sizeof(Tri) == 76 and C.sizeof(Sphere) == 44 and C.sizeof(Light) == 28
 assert C.sizeof(Isect) == 28 and C.sizeof(RTri) == 84
 
 P = C.c_void_p
+TEXTURE_MAPS = ("marble", "woven", "woven_ao", "woven_opacity", "woven_normal",
+                "grill", "grill_opacity", "grill_normal")
+TEXTURE_SHAPES = {"marble": (2000, 2000, 3)}   # the rest 1024 x 1024 x 3 (BGR)
+
+
+class RastTextures(C.Structure):   # cg_rast_textures
+    _fields_ = [(n, C.c_void_p) for n in TEXTURE_MAPS]
+
+
 _SIGS = {
     "cg_create": (C.c_int, [C.c_int, C.POINTER(P)]),
     "cg_destroy": (None, [P]),
@@ -117,6 +126,8 @@ _SIGS = {
                                  C.POINTER(Stats)]),
     "cg_rast_render_device": (C.c_int, [P, P, C.c_int, C.POINTER(RastParams), Vec4, P, P, P, P]),
     "cg_rast_set_scene": (C.c_int, [P, C.POINTER(RTri), C.c_int, C.POINTER(RTri), C.c_int]),
+    "cg_rast_set_textures": (C.c_int, [P, C.POINTER(RastTextures)]),
+    "cg_rast_opacity_map": (C.c_int, [P, C.c_int, P]),
     "cg_rast_draw": (C.c_int, [P, C.POINTER(RastParams), P, P, P, C.POINTER(Stats)]),
     "cg_rast_draw_device": (C.c_int, [P, C.POINTER(RastParams), P, P, P, P]),
 }
@@ -226,7 +237,7 @@ def random_scene(n, seed=0x5EED):
 
 
 def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
-                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2, colour_mode=0, rand_offset=0):
+                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2, colour_mode=0, rand_offset=0, yaw=0.0):
     p = RastParams()
     p.width, p.height, p.focal = width, height, focal
     p.camera = Vec4(*cam)
@@ -237,7 +248,18 @@ def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
     p.indirect_first = indirect_first
     p.colour_mode = colour_mode
     p.rand_offset = rand_offset
+    p.yaw = yaw
     return p
+
+
+def opacity_map(bgr):
+    """cg_rast_opacity_map (host-only): BGR texels -> 0/255 bytes."""
+    a = np.ascontiguousarray(bgr, dtype=np.uint8)
+    out = np.zeros(a.size // 3, np.uint8)
+    rc = load().cg_rast_opacity_map(a.ctypes.data_as(P), out.size, out.ctypes.data_as(P))
+    if rc != CG_OK:
+        raise RuntimeError(f"cg_rast_opacity_map failed with {rc}")
+    return out
 
 
 def frame_columns(tris, n, sph, n_sph, cam):
@@ -260,13 +282,19 @@ def rt_scene():
     return tris, n, sph
 
 
-def rast_scene():
+def rast_scene(setting=0, setting_boxes=0):
+    """LoadTestModel; setting / setting_boxes are the texture selectors of the
+    room and the boxes (TestModelH.h:9-10: 0 none, 1 marble, 2 grill, 3 woven)."""
     lib = load()
     room, boxes = (RTri * 16)(), (RTri * 32)()
     nr, nb = C.c_int(), C.c_int()
     rc = lib.cg_rast_load_test_model(room, 16, C.byref(nr), boxes, 32, C.byref(nb))
     if rc < 0:
         raise RuntimeError(f"cg_rast_load_test_model failed: {rc}")
+    for i in range(nr.value):
+        room[i].texture = setting
+    for i in range(nb.value):
+        boxes[i].texture = setting_boxes
     return room, nr.value, boxes, nb.value
 
 
@@ -408,6 +436,21 @@ class Context:
         if room is None:
             room, nr, boxes, nb = rast_scene()
         self._check(self.lib.cg_rast_set_scene(self.h, room, nr, boxes, nb), "cg_rast_set_scene")
+
+    def rast_set_textures(self, maps):
+        """maps: {name: uint8 (H, W, 3) BGR array} over TEXTURE_MAPS (absent = not
+        loaded), as cv::imread returns them; None unloads."""
+        if maps is None:
+            self._check(self.lib.cg_rast_set_textures(self.h, None), "cg_rast_set_textures")
+            return
+        arrs = {}
+        for k, v in maps.items():
+            a = np.ascontiguousarray(v, dtype=np.uint8)
+            if a.shape != TEXTURE_SHAPES.get(k, (1024, 1024, 3)):
+                raise ValueError(f"texture {k}: shape {a.shape}")
+            arrs[k] = a
+        t = RastTextures(**{k: a.ctypes.data for k, a in arrs.items()})
+        self._check(self.lib.cg_rast_set_textures(self.h, C.byref(t)), "cg_rast_set_textures")
 
     def rast_draw(self, params, want_depth=True, want_shadow=True):
         """Whole Draw on the device (geometry + fill + post)."""

@@ -32,6 +32,7 @@ namespace cg {
 
 void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e);
 int ctx_fail(cg_ctx *c, hipError_t e, const char *what);
+int ctx_invalid(cg_ctx *c, const char *what);
 void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b);
 
 constexpr int kSetupThreads = 256;
@@ -233,7 +234,11 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
                         if (x >= A.W) break;
                         if (x < 0) continue;
                         float zi = s.lz + (s.sz * (float)i);
-                        if (zi >= 0.0f) {
+                        // on an empty z-buffer a fragment shades unless it is a
+                        // transparent texel of texture 2/3 (:602, :624)
+                        if (zi >= 0.0f && (!A.textured || rast_opaque(A, T.texture, T.index, zi,
+                                                                     s.lX + (s.sX * (float)i),
+                                                                     s.lY + (s.sY * (float)i)))) {
                             atomicMin(&fkey, ((unsigned long long)(unsigned)y << 32) | (unsigned)x);
                             break;
                         }
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
             r.first_x = (t == ft && h.fy == y) ? h.fx : -1;
             r.shadow = T.color.x >= 0 ? 0 : 1;
             r.nx = T.normal.x; r.ny = T.normal.y; r.nz = T.normal.z;
-            r.pad0 = r.pad1 = 0.f;
+            r.tex = T.texture; r.index = T.index;
             recs[(size_t)y * A.n + c + __popcll(below)] = r;
         }
         c += __popcll(m);
@@ -308,11 +313,17 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
 constexpr int kFillPx = 64;
 constexpr int kFillPerLane = kFillPx / 64;
 
+// TEX: texture modes 1-3 possible (A.textured): a fragment of texture 2/3
+// that passes the depth test but hits a transparent texel sets the depth to 0
+// and shades nothing (:619, :643, :665) -- decided in the ordered walk; the
+// winner's texel word goes to texel_out for the post-pass.
+template <bool TEX>
 __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRec *__restrict__ recs,
                                                        const int *__restrict__ count,
                                                        float4 *__restrict__ state,
                                                        float *__restrict__ depth_out,
-                                                       int32_t *__restrict__ shadow_out)
+                                                       int32_t *__restrict__ shadow_out,
+                                                       uint32_t *__restrict__ texel_out)
 {
     RastArgs A = A0;
     if (A.d_light) {                                      // light from the device geometry (:223)
@@ -327,11 +338,12 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
     const int y = seg / segs;
     if (y >= A.H) return;
     const int x0 = (seg - y * segs) * kFillPx;
-    float depth[kFillPerLane];
+    float depth[kFillPerLane], win_z[kFillPerLane];
     int shadow[kFillPerLane], win[kFillPerLane];
 #pragma unroll
     for (int p = 0; p < kFillPerLane; ++p) {
         depth[p] = 0.0f;                                  // :247
+        win_z[p] = 0.0f;                                  // zinv of the last shading fragment
         shadow[p] = 0;                                    // :259
         win[p] = -1;                                      // record of the last shading fragment
     }
@@ -346,12 +358,16 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
     // ordered loop.
     for (int base = 0; base < cnt; base += 64) {
         const int q = base + lane;
-        int mlx = 0, mrx = 0, msh = 0;
-        float mlz = 0.f, msz = 0.f;
+        int mlx = 0, mrx = 0, msh = 0, mtex = 0, midx = 0;
+        float mlz = 0.f, msz = 0.f, mlX = 0.f, msX = 0.f, mlY = 0.f, msY = 0.f;
         bool ov = false;
         if (q < cnt) {
             const RowRec &mr = rr[q];
             mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = mr.shadow;
+            if (TEX) {
+                mtex = mr.tex; midx = mr.index;
+                mlX = mr.lX; msX = mr.sX; mlY = mr.lY; msY = mr.sY;
+            }
             ov = !(mrx - 1 < x0 || mlx > x0 + kFillPx - 1);
         }
         unsigned long long m = __ballot(ov);
@@ -363,6 +379,18 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
             const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlz), b));
             const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msz), b));
             const int shd = __builtin_amdgcn_readlane(msh, b);
+            int tex = 0, idx = 0;
+            float lX = 0.f, sX = 0.f, lY = 0.f, sY = 0.f;
+            if (TEX) {
+                tex = __builtin_amdgcn_readlane(mtex, b);
+                if (tex >= 2) {                                        // opacity-tested textures
+                    idx = __builtin_amdgcn_readlane(midx, b);
+                    lX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlX), b));
+                    sX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msX), b));
+                    lY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlY), b));
+                    sY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msY), b));
+                }
+            }
 #pragma unroll
             for (int p = 0; p < kFillPerLane; ++p) {
                 const int x = x0 + lane + 64 * p;
@@ -371,8 +399,14 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
                 const float zinv = lz + (sz * (float)i);               // :543
                 if (!shd) {
                     if (zinv >= depth[p]) {                            // :574
-                        depth[p] = zinv;                               // :665
-                        win[p] = base + b;
+                        if (TEX && tex >= 2 &&
+                            !rast_opaque(A, tex, idx, zinv, lX + (sX * (float)i), lY + (sY * (float)i))) {
+                            depth[p] = 0.0f;                           // p.zinv = 0 (:619, :643), :665
+                        } else {
+                            depth[p] = zinv;                           // :665
+                            win_z[p] = zinv;
+                            win[p] = base + b;
+                        }
                     }
                 } else if (zinv > depth[p]) {                          // :668-669
                     shadow[p] = 1;
@@ -386,15 +420,19 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
         if (x < A.W) {
             int tri = -1;
             vec3 D = v3(0.f, 0.f, 0.f);
+            uint32_t texel = 0u;
             if (win[p] >= 0) {
                 const RowRec r = rr[win[p]];
                 const int i = x - r.lx;
                 const float X = r.lX + (r.sX * (float)i);              // :547-548 numerators
                 const float Y = r.lY + (r.sY * (float)i);
-                D = illum_D(A, depth[p], X, Y, v3(r.nx, r.ny, r.nz));  // :580-585
+                vec3 N = v3(r.nx, r.ny, r.nz);
+                if (TEX && r.tex != 0) N = rast_tex_normal(A, r.tex, r.index, win_z[p], X, Y, x, y, N, texel);
+                D = illum_D(A, win_z[p], X, Y, N);                     // :580-585 (:590-645)
                 tri = r.t | (x == r.first_x ? (1 << 30) : 0);
             }
             size_t o = (size_t)y * A.W + x;
+            if (TEX) texel_out[o] = texel;
             state[o] = make_float4(__int_as_float(tri), D.x, D.y, D.z);
             if (depth_out) depth_out[o] = depth[p];
             shadow_out[o] = shadow[p];
@@ -404,7 +442,8 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
 
 // shade buffers of one pixel as they stand after the fill (:580-585), from its
 // state and its triangle's colour
-__device__ __forceinline__ void shade3c(const RastArgs &A, float4 st, cg_vec3 col, vec3 &sc, vec3 &lo, vec3 &hi)
+__device__ __forceinline__ void shade3c(const RastArgs &A, float4 st, cg_vec3 col, vec3 &sc, vec3 &lo, vec3 &hi,
+                                        int tex = 0, uint32_t texel = 0u)
 {
     const int tb = __float_as_int(st.x);
     if (tb < 0) {
@@ -417,8 +456,25 @@ __device__ __forceinline__ void shade3c(const RastArgs &A, float4 st, cg_vec3 co
         return;
     }
     const float ind = (tb & (1 << 30)) ? A.ind_first : 0.2f * 1;
-    const vec3 c = v3(col.x, col.y, col.z);
     const vec3 D = v3(st.y, st.z, st.w);
+    if (tex != 0) {
+        // textureColour (:590, :611, :636) and, texture 3, the occlusion (:626-627)
+        const vec3 c = v3((float)((texel >> 16) & 255u) / 255.0f, (float)((texel >> 8) & 255u) / 255.0f,
+                          (float)(texel & 255u) / 255.0f);
+        if (tex == 3) {
+            float occ = (float)(texel >> 24);
+            occ /= 255.0f;
+            sc = c * ((D + v3(ind, ind, ind)) * occ);                                // :638
+            lo = c * ((D + v3(0.0f * 1, 0.0f * 1, 0.0f * 1)) * occ);                 // :640
+            hi = c * ((D + v3(0.4f * 1, 0.4f * 1, 0.4f * 1)) * occ);                 // :642
+        } else {
+            sc = c * (D + v3(ind, ind, ind));
+            lo = c * (D + v3(0.0f * 1, 0.0f * 1, 0.0f * 1));
+            hi = c * (D + v3(0.4f * 1, 0.4f * 1, 0.4f * 1));
+        }
+        return;
+    }
+    const vec3 c = v3(col.x, col.y, col.z);
     sc = c * (D + v3(ind, ind, ind));                      // :580
     lo = c * (D + v3(0.0f * 1, 0.0f * 1, 0.0f * 1));       // :582
     hi = c * (D + v3(0.4f * 1, 0.4f * 1, 0.4f * 1));       // :584
@@ -450,10 +506,12 @@ constexpr int kPostTW = 64, kPostTH = 8;
 constexpr int kPostHW = kPostTW + 2, kPostHH = kPostTH + 2;      // shade halo 1
 constexpr int kPostSW = kPostTW + 4, kPostSH = kPostTH + 4;      // shadow halo 2
 
+template <bool TEX>
 __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
                                                        const float4 *__restrict__ state,
                                                        const int32_t *__restrict__ sh,
-                                                       uint32_t *__restrict__ argb)
+                                                       uint32_t *__restrict__ argb,
+                                                       const uint32_t *__restrict__ texels)
 {
     __shared__ int s_sh[kPostSH][kPostSW];
     __shared__ float s_c[9][kPostHH][kPostHW];      // sc.xyz, lo.xyz, hi.xyz
@@ -482,10 +540,23 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         stv[r] = inb[r] ? state[(size_t)gy * W + gx] : make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
     }
     cg_vec3 col[kStR];
+    int texm[kStR];
+    uint32_t txl[kStR];
 #pragma unroll
     for (int r = 0; r < kStR; ++r) {
         const int tb = __float_as_int(stv[r].x);
-        col[r] = (tb >= 0 && !(tb & kStateDirect)) ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f};
+        const bool tri = tb >= 0 && !(tb & kStateDirect);
+        col[r] = tri ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f};
+        texm[r] = 0;
+        txl[r] = 0u;
+        if (TEX && tri) {
+            texm[r] = tris[tb & ~(1 << 30)].texture;
+            if (texm[r] != 0) {
+                const int i = threadIdx.x + 256 * r;
+                const int cy = i / kPostHW, cx = i - cy * kPostHW;
+                txl[r] = texels[(size_t)(gy0 - 1 + cy) * W + (gx0 - 1 + cx)];
+            }
+        }
     }
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
@@ -502,7 +573,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
         float d = 0.0f;
         if (inb[r]) {
-            shade3c(A, stv[r], col[r], sc, lo, hi);
+            shade3c(A, stv[r], col[r], sc, lo, hi, texm[r], txl[r]);
             if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
         }
         s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
@@ -557,20 +628,58 @@ hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room
 // light read from d_light).
 static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_dev, const cg_rast_params *p,
                          cg_vec4 light, const cg_vec4 *d_light, uint32_t *d_argb, float *d_depth,
-                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open);
+                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open, int tex_mask);
+int rast_tex_maps(cg_ctx *c, RastTexMaps *m);
+
+// glm::inverse for mat4 (glm/detail/type_mat4x4.inl:37-90), column-major
+// m[4c + r] = m[c][r]: findU / findV's inverse(R) (skeleton.cpp:1762).
+static void mat4_inverse_glm(const float *m, float *out)
+{
+    auto M = [m](int c, int r) { return m[4 * c + r]; };
+    const float c00 = M(2, 2) * M(3, 3) - M(3, 2) * M(2, 3), c02 = M(1, 2) * M(3, 3) - M(3, 2) * M(1, 3);
+    const float c03 = M(1, 2) * M(2, 3) - M(2, 2) * M(1, 3);
+    const float c04 = M(2, 1) * M(3, 3) - M(3, 1) * M(2, 3), c06 = M(1, 1) * M(3, 3) - M(3, 1) * M(1, 3);
+    const float c07 = M(1, 1) * M(2, 3) - M(2, 1) * M(1, 3);
+    const float c08 = M(2, 1) * M(3, 2) - M(3, 1) * M(2, 2), c10 = M(1, 1) * M(3, 2) - M(3, 1) * M(1, 2);
+    const float c11 = M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2);
+    const float c12 = M(2, 0) * M(3, 3) - M(3, 0) * M(2, 3), c14 = M(1, 0) * M(3, 3) - M(3, 0) * M(1, 3);
+    const float c15 = M(1, 0) * M(2, 3) - M(2, 0) * M(1, 3);
+    const float c16 = M(2, 0) * M(3, 2) - M(3, 0) * M(2, 2), c18 = M(1, 0) * M(3, 2) - M(3, 0) * M(1, 2);
+    const float c19 = M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2);
+    const float c20 = M(2, 0) * M(3, 1) - M(3, 0) * M(2, 1), c22 = M(1, 0) * M(3, 1) - M(3, 0) * M(1, 1);
+    const float c23 = M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1);
+    const float fac[6][4] = {{c00, c00, c02, c03}, {c04, c04, c06, c07}, {c08, c08, c10, c11},
+                             {c12, c12, c14, c15}, {c16, c16, c18, c19}, {c20, c20, c22, c23}};
+    const float vec[4][4] = {{M(1, 0), M(0, 0), M(0, 0), M(0, 0)}, {M(1, 1), M(0, 1), M(0, 1), M(0, 1)},
+                             {M(1, 2), M(0, 2), M(0, 2), M(0, 2)}, {M(1, 3), M(0, 3), M(0, 3), M(0, 3)}};
+    float inv[4][4];
+    for (int k = 0; k < 4; ++k) {
+        const float sa = (k & 1) ? -1.0f : 1.0f, sb = -sa;   // SignA (+,-,+,-), SignB (-,+,-,+)
+        inv[0][k] = ((vec[1][k] * fac[0][k] - vec[2][k] * fac[1][k]) + vec[3][k] * fac[2][k]) * sa;
+        inv[1][k] = ((vec[0][k] * fac[0][k] - vec[2][k] * fac[3][k]) + vec[3][k] * fac[4][k]) * sb;
+        inv[2][k] = ((vec[0][k] * fac[1][k] - vec[1][k] * fac[3][k]) + vec[3][k] * fac[5][k]) * sa;
+        inv[3][k] = ((vec[0][k] * fac[2][k] - vec[1][k] * fac[4][k]) + vec[2][k] * fac[5][k]) * sb;
+    }
+    const float d0 = M(0, 0) * inv[0][0], d1 = M(0, 1) * inv[1][0], d2 = M(0, 2) * inv[2][0],
+                d3 = M(0, 3) * inv[3][0];
+    const float one_over = 1.0f / ((d0 + d1) + (d2 + d3));
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) out[4 * c + r] = inv[c][r] * one_over;
+}
 
 int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_params *p, cg_vec4 light,
                        uint32_t *d_argb, float *d_depth, int32_t *d_shadow, hipStream_t st,
-                       cg_stats *stats)
+                       cg_stats *stats, int tex_mask)
 {
-    return rast_pipeline(c, d_tris, n, nullptr, p, light, nullptr, d_argb, d_depth, d_shadow, st, stats, false);
+    return rast_pipeline(c, d_tris, n, nullptr, p, light, nullptr, d_argb, d_depth, d_shadow, st, stats, false,
+                         tex_mask);
 }
 
 // Whole rasteriser Draw on the device: geometry (shadow volumes + clip) then
 // fill + post.  room/boxes are device pointers (cg_rast_set_scene).
 int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri *d_boxes, int n_boxes,
                      const cg_rast_params *p, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
-                     hipStream_t st, cg_stats *stats, int **n_out)
+                     hipStream_t st, cg_stats *stats, int **n_out, int tex_mask)
 {
     if (p->width <= 2 || p->height <= 2 || p->height > kRastMaxRows || p->focal == 0.0f) return CG_E_INVALID;
     const int n_in = n_room + 7 * n_boxes;
@@ -591,12 +700,12 @@ int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri
         return ctx_fail(c, e, "rast_geometry launch");
     if (n_out) *n_out = geo;
     return rast_pipeline(c, tris, cap, geo, p, cg_vec4{0, 0, 0, 1}, (const cg_vec4 *)(geo + 4), d_argb, d_depth,
-                         d_shadow, st, stats, true);
+                         d_shadow, st, stats, true, tex_mask);
 }
 
 static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_dev, const cg_rast_params *p,
                          cg_vec4 light, const cg_vec4 *d_light, uint32_t *d_argb, float *d_depth,
-                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open)
+                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open, int tex_mask)
 {
     if (p->width <= 2 || p->height <= 2 || p->height > kRastMaxRows) return CG_E_INVALID;
     const int W = p->width, H = p->height;
@@ -629,6 +738,22 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     A.ind_first = p->indirect_first;
     A.want_first = p->colour_mode == 0 && p->indirect_first != 0.2f * 1;   // the :585 rewrite is mode 0 only
     A.d_light = d_light;
+    // texture modes 1-3: the maps, cameraPos and, when yaw != 0, inverse(R)
+    const int loaded = rast_tex_maps(c, &A.tx);
+    if (tex_mask & 16) return ctx_invalid(c, "texture selector outside 0-3 (TestModelH.h:21)");
+    if (tex_mask & ~loaded & 0xe)
+        return ctx_invalid(c, "a triangle carries a texture whose maps are not loaded (cg_rast_set_textures)");
+    if ((tex_mask & 2) && (size_t)(H - 1) * kMarbleN + (W - 1) >= (size_t)kMarbleN * kMarbleN)
+        return ctx_invalid(c, "marble: normalMap_marble[y * 2000 + x] would index past the map");
+    A.textured = (tex_mask & 0xe) != 0;
+    A.use_inv = p->yaw != 0.0f;
+    A.cam[0] = p->camera.x; A.cam[1] = p->camera.y; A.cam[2] = p->camera.z; A.cam[3] = p->camera.w;
+    mat4_inverse_glm(p->R, A.Rinv);
+    uint32_t *texels = nullptr;
+    if (A.textured) {
+        texels = (uint32_t *)ctx_buf(c, 16, npx * sizeof(uint32_t), &e);
+        if (!texels) return ctx_fail(c, e, "alloc texels");
+    }
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
     if (stats && !events_open && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
@@ -650,13 +775,22 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
         if (stats) stats->n_shaded = ns;
     } else {
         const int fsegs = (W + kFillPx - 1) / kFillPx;
-        hipLaunchKernelGGL(rast_fill_kernel, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
-                           state, d_depth, shadow);
+        if (A.textured)
+            hipLaunchKernelGGL(rast_fill_kernel<true>, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
+                               state, d_depth, shadow, texels);
+        else
+            hipLaunchKernelGGL(rast_fill_kernel<false>, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs,
+                               count, state, d_depth, shadow, (uint32_t *)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
         if (stats) stats->n_shaded = -1;
     }
-    hipLaunchKernelGGL(rast_post_kernel, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH), dim3(256), 0,
-                       st, d_tris, A, state, shadow, d_argb);
+    const bool tex_post = A.textured && p->colour_mode == 0;
+    if (tex_post)
+        hipLaunchKernelGGL(rast_post_kernel<true>, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH),
+                           dim3(256), 0, st, d_tris, A, state, shadow, d_argb, (const uint32_t *)texels);
+    else
+        hipLaunchKernelGGL(rast_post_kernel<false>, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH),
+                           dim3(256), 0, st, d_tris, A, state, shadow, d_argb, (const uint32_t *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");
     if (stats && (e = hipEventRecord(e1, st)) != hipSuccess) return ctx_fail(c, e, "event");
     if (stats) {

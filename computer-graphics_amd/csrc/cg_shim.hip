@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "cg_internal.h"
+#include "cg_rast_dev.h"
 
 namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTri *, RtShade *, hipStream_t,
@@ -42,10 +43,10 @@ hipError_t launch_rt_probe_direct_light(const RtFrame &, const RtTri *, const Rt
                                         hipStream_t);
 int rast_render_device(cg_ctx *ctx, const cg_rtri *d_tris, int n, const cg_rast_params *p,
                        cg_vec4 light, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
-                       hipStream_t st, cg_stats *stats);
+                       hipStream_t st, cg_stats *stats, int tex_mask);
 int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri *d_boxes, int n_boxes,
                      const cg_rast_params *p, uint32_t *d_argb, float *d_depth, int32_t *d_shadow,
-                     hipStream_t st, cg_stats *stats, int **n_out);
+                     hipStream_t st, cg_stats *stats, int **n_out, int tex_mask);
 void rast_release(cg_ctx *ctx);
 }  // namespace cg
 
@@ -98,6 +99,10 @@ struct cg_ctx {
     DevBuf rpc, rtl, rrnd, rjt;          // colour modes 1-2 (cg_rast_colour.hip)
     DevBuf sstars, sframe;               // starfield (cg_starfield.hip)
     int n_room = -1, n_boxes = 0;
+    int scene_tex = 0;                   // bit k: the uploaded room/boxes carry texture k
+    // texture modes 1-3 (cg_rast_set_textures): device copies of the maps
+    DevBuf tmarble, tnoise, twoven, twoven_ao, twoven_op, twoven_nrm, tgrill, tgrill_op, tgrill_nrm, rtexel;
+    int tex_loaded = 0;                  // bit k: texture k renderable
 };
 
 namespace cg {
@@ -122,12 +127,18 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
     case 13: b = &c->rjt; break;
     case 14: b = &c->sstars; break;
     case 15: b = &c->sframe; break;
+    case 16: b = &c->rtexel; break;
     default: *e = hipErrorInvalidValue; return nullptr;
     }
     *e = b->ensure(bytes);
     return *e == hipSuccess ? b->p : nullptr;
 }
 hipStream_t ctx_stream(cg_ctx *c) { return c->stream; }
+int ctx_invalid(cg_ctx *c, const char *what)
+{
+    c->err = what;
+    return CG_E_INVALID;
+}
 int ctx_fail(cg_ctx *c, hipError_t e, const char *what)
 {
     c->err = std::string(what) + ": " + hipGetErrorString(e);
@@ -145,6 +156,23 @@ void rast_release(cg_ctx *c)
     c->rrecs.release(); c->rgeo.release(); c->rroom.release(); c->rboxes.release();
     c->rpc.release(); c->rtl.release(); c->rrnd.release(); c->rjt.release();
     c->sstars.release(); c->sframe.release();
+    c->tmarble.release(); c->tnoise.release(); c->twoven.release(); c->twoven_ao.release();
+    c->twoven_op.release(); c->twoven_nrm.release(); c->tgrill.release(); c->tgrill_op.release();
+    c->tgrill_nrm.release(); c->rtexel.release();
+}
+// the device texture maps and which textures are renderable (bit k: texture k)
+int rast_tex_maps(cg_ctx *c, RastTexMaps *m)
+{
+    m->marble = (const uint8_t *)c->tmarble.p;
+    m->marble_noise = (const float *)c->tnoise.p;
+    m->woven = (const uint8_t *)c->twoven.p;
+    m->woven_ao = (const uint8_t *)c->twoven_ao.p;
+    m->woven_op = (const uint8_t *)c->twoven_op.p;
+    m->woven_nrm = (const uint8_t *)c->twoven_nrm.p;
+    m->grill = (const uint8_t *)c->tgrill.p;
+    m->grill_op = (const uint8_t *)c->tgrill_op.p;
+    m->grill_nrm = (const uint8_t *)c->tgrill_nrm.p;
+    return c->tex_loaded;
 }
 }  // namespace cg
 
@@ -747,14 +775,27 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
 // ---------------------------------------------------------------------------
 // RAST entry points (kernels in cg_rast.hip)
 
+extern "C" int cg_glibc_rand(uint64_t offset, int n, int32_t *out);
+
+// bit k set: some triangle of the list carries texture k (1-3)
+static int rast_tex_mask(const cg_rtri *t, int n)
+{
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        if (t[i].color.x >= 0 && t[i].texture != 0)
+            m |= (t[i].texture >= 1 && t[i].texture <= 3) ? 1 << t[i].texture : 1 << 4;   // 16: no such texture
+    return m;
+}
+
 extern "C" int cg_rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n,
                                      const cg_rast_params *p, cg_vec4 light, uint32_t *d_argb,
                                      float *d_depth, int32_t *d_shadow, void *stream)
 {
     if (!c || !p || !d_argb || n < 0 || (n && !d_tris)) return CG_E_INVALID;
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    // device lists are not inspected: textures run if any maps are loaded
     return rast_render_device(c, d_tris, n, p, light, d_argb, d_depth, d_shadow,
-                              stream ? (hipStream_t)stream : c->stream, nullptr);
+                              stream ? (hipStream_t)stream : c->stream, nullptr, c->tex_loaded);
 }
 
 extern "C" int cg_rast_render(cg_ctx *c, const cg_rtri *tris, int n, const cg_rast_params *p,
@@ -777,7 +818,8 @@ extern "C" int cg_rast_render(cg_ctx *c, const cg_rtri *tris, int n, const cg_ra
     int32_t *d_shadow = (int32_t *)ctx_buf(c, 6, npx * 4, &e);
     if (!d_shadow) return ctx_fail(c, e, "alloc shadow");
     if (n) CG_TRY(c, hipMemcpyAsync(d_tris, tris, (size_t)n * sizeof(cg_rtri), hipMemcpyHostToDevice, c->stream), "upload tris");
-    int rc = rast_render_device(c, d_tris, n, p, light, d_argb, d_depth, d_shadow, c->stream, stats);
+    int rc = rast_render_device(c, d_tris, n, p, light, d_argb, d_depth, d_shadow, c->stream, stats,
+                                rast_tex_mask(tris, n));
     if (rc) return rc;
     CG_TRY(c, hipMemcpyAsync(argb, d_argb, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h argb");
     if (depth) CG_TRY(c, hipMemcpyAsync(depth, d_depth, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h depth");
@@ -807,6 +849,64 @@ extern "C" int cg_rast_set_scene(cg_ctx *c, const cg_rtri *room, int n_room, con
     CG_TRY(c, hipStreamSynchronize(c->stream), "scene upload");
     c->n_room = n_room;
     c->n_boxes = n_boxes;
+    c->scene_tex = rast_tex_mask(room, n_room) | rast_tex_mask(boxes, n_boxes);
+    return CG_OK;
+}
+
+extern "C" int cg_rast_opacity_map(const uint8_t *bgr, int n, uint8_t *out)
+{
+    if (n < 0 || (n && (!bgr || !out))) return CG_E_INVALID;
+    for (int i = 0; i < n; ++i) {   // RGB2Gray<uchar> (blueIdx 0), then threshold(100, 255, BINARY)
+        const int y = (bgr[3 * i] * 1868 + bgr[3 * i + 1] * 9617 + bgr[3 * i + 2] * 4899 + (1 << 13)) >> 14;
+        out[i] = y > 100 ? 255 : 0;
+    }
+    return CG_OK;
+}
+
+extern "C" int cg_rast_set_textures(cg_ctx *c, const cg_rast_textures *t)
+{
+    if (!c) return CG_E_INVALID;
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "sync");
+    DevBuf *all[] = {&c->tmarble, &c->tnoise, &c->twoven, &c->twoven_ao, &c->twoven_op, &c->twoven_nrm,
+                     &c->tgrill, &c->tgrill_op, &c->tgrill_nrm};
+    for (DevBuf *b : all) b->release();
+    c->tex_loaded = 0;
+    if (!t) return CG_OK;
+    const size_t tn = (size_t)kTexN * kTexN, mn = (size_t)kMarbleN * kMarbleN;
+    auto up = [&](DevBuf &b, const void *src, size_t bytes) -> int {
+        CG_TRY(c, b.ensure(bytes), "alloc texture");
+        CG_TRY(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice), "upload texture");
+        return CG_OK;
+    };
+    auto up_op = [&](DevBuf &b, const uint8_t *bgr) -> int {   // skeleton.cpp:149-155
+        std::vector<uint8_t> op(tn);
+        cg_rast_opacity_map(bgr, (int)tn, op.data());
+        return up(b, op.data(), tn);
+    };
+    int rc = 0;
+    if (t->grill && t->grill_opacity && t->grill_normal) {
+        if ((rc = up(c->tgrill, t->grill, 3 * tn)) || (rc = up_op(c->tgrill_op, t->grill_opacity)) ||
+            (rc = up(c->tgrill_nrm, t->grill_normal, 3 * tn)))
+            return rc;
+        c->tex_loaded |= 1 << 2;
+    }
+    if (t->woven && t->woven_ao && t->woven_opacity && t->woven_normal) {
+        if ((rc = up(c->twoven, t->woven, 3 * tn)) || (rc = up(c->twoven_ao, t->woven_ao, 3 * tn)) ||
+            (rc = up_op(c->twoven_op, t->woven_opacity)) || (rc = up(c->twoven_nrm, t->woven_normal, 3 * tn)))
+            return rc;
+        c->tex_loaded |= 1 << 3;
+    }
+    if (t->marble) {
+        // normalMap_marble (:158-170): the process's first 3 * 2000 * 2000 rand() calls
+        std::vector<int32_t> r(3 * mn);
+        if ((rc = cg_glibc_rand(0, (int)r.size(), r.data()))) return rc;
+        std::vector<float> noise(3 * mn);
+        const float LO = -0.000002f, HI = 0.000002f;
+        for (size_t i = 0; i < r.size(); ++i) noise[i] = LO + (float)r[i] / ((float)((float)RAND_MAX / HI - LO));
+        if ((rc = up(c->tmarble, t->marble, 3 * mn)) || (rc = up(c->tnoise, noise.data(), noise.size() * 4))) return rc;
+        c->tex_loaded |= 1 << 1;
+    }
     return CG_OK;
 }
 
@@ -820,7 +920,8 @@ extern "C" int cg_rast_draw_device(cg_ctx *c, const cg_rast_params *p, uint32_t 
     }
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     return rast_draw_device(c, (const cg_rtri *)c->rroom.p, c->n_room, (const cg_rtri *)c->rboxes.p, c->n_boxes, p,
-                            d_argb, d_depth, d_shadow, stream ? (hipStream_t)stream : c->stream, nullptr, nullptr);
+                            d_argb, d_depth, d_shadow, stream ? (hipStream_t)stream : c->stream, nullptr, nullptr,
+                            c->scene_tex);
 }
 
 extern "C" int cg_rast_draw(cg_ctx *c, const cg_rast_params *p, uint32_t *argb, float *depth, int32_t *shadow,
@@ -843,7 +944,7 @@ extern "C" int cg_rast_draw(cg_ctx *c, const cg_rast_params *p, uint32_t *argb, 
     if (!d_shadow) return ctx_fail(c, e, "alloc shadow");
     int *d_n = nullptr;
     int rc = rast_draw_device(c, (const cg_rtri *)c->rroom.p, c->n_room, (const cg_rtri *)c->rboxes.p, c->n_boxes, p,
-                              d_argb, d_depth, d_shadow, c->stream, stats, &d_n);
+                              d_argb, d_depth, d_shadow, c->stream, stats, &d_n, c->scene_tex);
     if (rc) return rc;
     int n = 0;
     CG_TRY(c, hipMemcpyAsync(&n, d_n, sizeof(int), hipMemcpyDeviceToHost, c->stream), "d2h count");

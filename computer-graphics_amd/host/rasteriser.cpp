@@ -63,7 +63,7 @@ void Draw(screen *screen)
     p.light_power = cg_vec3{lightPower.x, lightPower.y, lightPower.z};
     p.indirect_first = indirectLightPowerPerArea.x;
     p.colour_mode = randColourSelect;
-    p.pad_ = 0;
+    p.yaw = yaw;
     p.rand_offset = randCalls;
     // geometry (shadow volumes + clip), fill and post-pass all on the GPU
     cg_stats st;

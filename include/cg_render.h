@@ -95,7 +95,8 @@ typedef struct {
                                  colour-mode-0 fragment was shaded */
     int colour_mode;          /* randColourSelect (:81, SPACE key :408): 0 lit triangle colour,
                                  1 random colour, 2 night vision (:647-662) */
-    int pad_;
+    float yaw;                /* yaw (:34): findU/findV (:1756-1825) map through inverse(R)
+                                 when it is non-zero (texture modes 1-3 only) */
     uint64_t rand_offset;     /* modes 1-2: glibc rand() calls made before this frame (the
                                  reference never seeds: srand(1)); each shaded fragment
                                  consumes 3 (cg_stats.n_shaded) */
@@ -243,6 +244,35 @@ int cg_rast_draw(cg_ctx *ctx, const cg_rast_params *p, uint32_t *argb, float *de
                  cg_stats *stats);
 int cg_rast_draw_device(cg_ctx *ctx, const cg_rast_params *p, uint32_t *d_argb, float *d_depth,
                         int32_t *d_shadow, void *stream);
+
+/* Texture modes 1-3 (skeleton.cpp:588-645; a triangle's `texture` field,
+ * TestModelH.h:21: 1 marble, 2 metal grill, 3 woven wood -- set it on the
+ * room/boxes lists, as `setting` / `settingBoxes` do, TestModelH.h:9-10).
+ * The maps as cv::imread(..., CV_LOAD_IMAGE_UNCHANGED) returns them
+ * (:135-146): row-major BGR, 3 bytes per texel; marble 2000 x 2000, the rest
+ * 1024 x 1024.  NULL = not loaded; a texture is renderable when all its maps
+ * are (marble: marble; grill: grill, grill_opacity, grill_normal; woven: all
+ * four woven maps), and rendering a triangle with a texture that is not
+ * fails with CG_E_INVALID (the reference reads an empty cv::Mat). */
+typedef struct {
+    const uint8_t *marble;                                   /* Marble2000x2000.jpg */
+    const uint8_t *woven;                                    /* woven1024x1024.jpg */
+    const uint8_t *woven_ao;                                 /* Wood_wicker_003_ambientOcclusion.jpg */
+    const uint8_t *woven_opacity;                            /* Wood_wicker_003_opacity.jpg */
+    const uint8_t *woven_normal;                             /* Wood_wicker_003_normal.jpg */
+    const uint8_t *grill;                                    /* Metal_Grill_002_basecolor.jpg */
+    const uint8_t *grill_opacity;                            /* Metal_Grill_002_opacity.jpg */
+    const uint8_t *grill_normal;                             /* Metal_Grill_002_normal.jpg */
+} cg_rast_textures;
+/* Upload the maps and build what main() derives from them at start-up
+ * (:148-170): the opacity maps (cg_rast_opacity_map) and, with marble, the
+ * normal-noise map from the process's first 3 * 2000 * 2000 rand() calls --
+ * colour modes 1-2 then start at rand_offset 12,000,000.  NULL unloads. */
+int cg_rast_set_textures(cg_ctx *ctx, const cg_rast_textures *tex);
+/* Host-only: OpenCV 3.4 cvtColor(CV_BGR2GRAY) on 8-bit BGR (fixed point,
+ * 14-bit coefficients) then threshold(100, 255, THRESH_BINARY) (:149-155):
+ * n texels in, n bytes (0 or 255) out. */
+int cg_rast_opacity_map(const uint8_t *bgr, int n, uint8_t *out);
 
 /* ---- starfield (starfield/Source/skeleton.cpp) -------------------------- */
 /* n stars as (x, y, z) float triples from glibc rand() (:41-46, seed 1). */

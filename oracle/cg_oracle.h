@@ -103,9 +103,31 @@ typedef struct {
     cgo_v3 light_power;       /* skeleton.cpp:53 */
     float indirect_first;     /* value of indirectLightPowerPerArea at frame start (0.15 first frame, 0.2 after) */
     int colour_mode;          /* randColourSelect (skeleton.cpp:81, :408): 0 lit colour, 1 random, 2 night vision */
-    int pad_;
+    float yaw;                /* skeleton.cpp:34; findU/findV (:1756-1825) take inverse(R) when yaw != 0 */
     uint64_t rand_offset;     /* glibc rand() calls made before this frame (srand never called: seed 1) */
+    int setting, setting_boxes; /* TestModelH.h:9-10: texture of the room / the boxes (0 none, 1 marble,
+                                 2 metal grill, 3 woven wood); maps from cgo_rast_set_textures */
 } cgo_rast_params;
+
+/* The texture maps as the reference's cv::imread(..., CV_LOAD_IMAGE_UNCHANGED)
+ * returns them (skeleton.cpp:135-146): row-major BGR, 3 bytes per texel.
+ * marble 2000x2000, the rest 1024x1024; NULL = not loaded (a triangle with
+ * that texture is then not renderable: the reference reads an empty Mat). */
+typedef struct {
+    const uint8_t *marble;
+    const uint8_t *woven, *woven_ao, *woven_opacity, *woven_normal;
+    const uint8_t *grill, *grill_opacity, *grill_normal;
+} cgo_rast_textures;
+/* Keeps the pointers (caller-owned) and builds what main() derives at start-up
+ * (skeleton.cpp:148-172): the two opacity maps (cvtColor BGR2GRAY, threshold
+ * 100 -> 0/255) and, with marble, the normal-noise map from the first
+ * 3 * 2000 * 2000 rand() calls.  NULL clears. */
+void cgo_rast_set_textures(const cgo_rast_textures *t);
+/* OpenCV 3.4 cvtColor(CV_BGR2GRAY) for 8-bit BGR (fixed point, 14-bit
+ * coefficients) followed by threshold(100, 255, THRESH_BINARY). */
+void cgo_rast_opacity_map(const uint8_t *bgr, int n, uint8_t *out);
+/* glm::inverse (glm/detail/type_mat4x4.inl:37-90), column-major m[4c + r]. */
+void cgo_mat4_inverse(const float *m, float *out);
 
 typedef struct {
     uint64_t n_tris, n_spans, n_frags, n_shaded, n_shadow;

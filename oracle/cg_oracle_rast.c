@@ -1,8 +1,8 @@
 /*
  * cg_oracle_rast.c -- TEST INFRASTRUCTURE ONLY (checker + CPU baseline).
  *
- * Plain-C restatement of the reference rasteriser's Draw (texture mode 0,
- * colour mode 0): host geometry (camera space, shadow volumes, rotation,
+ * Plain-C restatement of the reference rasteriser's Draw (texture modes
+ * 0-3, colour modes 0-2): host geometry (camera space, shadow volumes, rotation,
  * clip space, six clip planes), VertexShader, ComputePolygonRows,
  * Interpolate, DrawPolygonRows, PixelShader, calculateIllumination and the
  * soft-shadow + anti-alias post-pass.  Each function cites the reference
@@ -299,6 +299,8 @@ int cgo_rast_geometry(const cgo_rast_params *p, cgo_rast_tri *out, int cap, cgo_
     cgo_rast_tri room[16], boxes[32];
     int nr, nb;
     cgo_rast_load_scene(room, &nr, boxes, &nb);
+    for (int i = 0; i < nr; ++i) room[i].texture = p->setting;          /* TestModelH.h:85-129 */
+    for (int i = 0; i < nb; ++i) boxes[i].texture = p->setting_boxes;   /* TestModelH.h:148-260 */
     enum { MAXT = 8192 };
     cgo_rast_tri *A = (cgo_rast_tri *)malloc(sizeof(cgo_rast_tri) * MAXT);
     cgo_rast_tri *B = (cgo_rast_tri *)malloc(sizeof(cgo_rast_tri) * MAXT);
@@ -450,13 +452,128 @@ int cgo_rast_polygon_rows(const cgo_pixel *vp, cgo_pixel *left, cgo_pixel *right
     return rows;
 }
 
+/* ---------------------------- textures --------------------------------- */
+
+static const cgo_rast_textures *g_tex;
+static uint8_t *g_grill_op, *g_woven_op;    /* thresholded gray maps (skeleton.cpp:149-155) */
+static float *g_noise;                       /* normalMap_marble xyz (:158-170) */
+enum { TEX_N = 1024, MARBLE_N = 2000 };
+
+/* OpenCV 3.4 RGB2Gray<uchar> (imgproc/src/color.cpp) with blueIdx 0:
+ * Y = (B*1868 + G*9617 + R*4899 + (1 << 13)) >> 14, then threshold (:154-155):
+ * 255 where Y > 100, else 0. */
+void cgo_rast_opacity_map(const uint8_t *bgr, int n, uint8_t *out)
+{
+    for (int i = 0; i < n; ++i) {
+        const int y = (bgr[3 * i] * 1868 + bgr[3 * i + 1] * 9617 + bgr[3 * i + 2] * 4899 + (1 << 13)) >> 14;
+        out[i] = y > 100 ? 255 : 0;
+    }
+}
+
+void cgo_rast_set_textures(const cgo_rast_textures *t)
+{
+    free(g_grill_op); free(g_woven_op); free(g_noise);
+    g_grill_op = g_woven_op = 0;
+    g_noise = 0;
+    g_tex = t;
+    if (!t) return;
+    if (t->grill_opacity) {
+        g_grill_op = (uint8_t *)malloc(TEX_N * TEX_N);
+        cgo_rast_opacity_map(t->grill_opacity, TEX_N * TEX_N, g_grill_op);
+    }
+    if (t->woven_opacity) {
+        g_woven_op = (uint8_t *)malloc(TEX_N * TEX_N);
+        cgo_rast_opacity_map(t->woven_opacity, TEX_N * TEX_N, g_woven_op);
+    }
+    if (t->marble) {   /* :158-170, the process's first rand() calls (seed 1) */
+        const float LO = -0.000002f, HI = 0.000002f;
+        g_noise = (float *)malloc(sizeof(float) * 3 * MARBLE_N * MARBLE_N);
+        srand(1);
+        for (int i = 0; i < 3 * MARBLE_N * MARBLE_N; ++i)
+            g_noise[i] = LO + (float)rand() / ((float)(RAND_MAX / HI - LO));
+    }
+}
+
+/* glm/detail/type_mat4x4.inl:37-90 (compute_inverse), m[4c + r] = m[c][r] */
+void cgo_mat4_inverse(const float *m, float *out)
+{
+#define M(c, r) m[4 * (c) + (r)]
+    float c00 = M(2,2) * M(3,3) - M(3,2) * M(2,3), c02 = M(1,2) * M(3,3) - M(3,2) * M(1,3);
+    float c03 = M(1,2) * M(2,3) - M(2,2) * M(1,3);
+    float c04 = M(2,1) * M(3,3) - M(3,1) * M(2,3), c06 = M(1,1) * M(3,3) - M(3,1) * M(1,3);
+    float c07 = M(1,1) * M(2,3) - M(2,1) * M(1,3);
+    float c08 = M(2,1) * M(3,2) - M(3,1) * M(2,2), c10 = M(1,1) * M(3,2) - M(3,1) * M(1,2);
+    float c11 = M(1,1) * M(2,2) - M(2,1) * M(1,2);
+    float c12 = M(2,0) * M(3,3) - M(3,0) * M(2,3), c14 = M(1,0) * M(3,3) - M(3,0) * M(1,3);
+    float c15 = M(1,0) * M(2,3) - M(2,0) * M(1,3);
+    float c16 = M(2,0) * M(3,2) - M(3,0) * M(2,2), c18 = M(1,0) * M(3,2) - M(3,0) * M(1,2);
+    float c19 = M(1,0) * M(2,2) - M(2,0) * M(1,2);
+    float c20 = M(2,0) * M(3,1) - M(3,0) * M(2,1), c22 = M(1,0) * M(3,1) - M(3,0) * M(1,1);
+    float c23 = M(1,0) * M(2,1) - M(2,0) * M(1,1);
+    const float F0[4] = {c00, c00, c02, c03}, F1[4] = {c04, c04, c06, c07}, F2[4] = {c08, c08, c10, c11};
+    const float F3[4] = {c12, c12, c14, c15}, F4[4] = {c16, c16, c18, c19}, F5[4] = {c20, c20, c22, c23};
+    const float V0[4] = {M(1,0), M(0,0), M(0,0), M(0,0)}, V1[4] = {M(1,1), M(0,1), M(0,1), M(0,1)};
+    const float V2[4] = {M(1,2), M(0,2), M(0,2), M(0,2)}, V3[4] = {M(1,3), M(0,3), M(0,3), M(0,3)};
+    float inv[4][4];
+    for (int k = 0; k < 4; ++k) {
+        const float sa = (k & 1) ? -1.0f : 1.0f;   /* SignA (+ - + -) */
+        inv[0][k] = ((V1[k] * F0[k] - V2[k] * F1[k]) + V3[k] * F2[k]) * sa;
+        inv[1][k] = ((V0[k] * F0[k] - V2[k] * F3[k]) + V3[k] * F4[k]) * -sa;   /* SignB */
+        inv[2][k] = ((V0[k] * F1[k] - V1[k] * F3[k]) + V3[k] * F5[k]) * sa;
+        inv[3][k] = ((V0[k] * F2[k] - V1[k] * F4[k]) + V2[k] * F5[k]) * -sa;
+    }
+    const float d0 = M(0,0) * inv[0][0], d1 = M(0,1) * inv[1][0], d2 = M(0,2) * inv[2][0], d3 = M(0,3) * inv[3][0];
+    const float one_over = 1.0f / ((d0 + d1) + (d2 + d3));
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) out[4 * c + r] = inv[c][r] * one_over;
+#undef M
+}
+
 typedef struct {
     const cgo_rast_params *p;
     cgo_v4 lightPos;
     float *depth; int32_t *shadow; float *screen, *low, *high;
     float indirect;          /* the global indirectLightPowerPerArea (x component) */
     cgo_rast_counters *cnt;
+    float Rinv[16];          /* glm::inverse(R) (findU/findV with yaw != 0) */
 } rast_state;
+
+/* findU / findV (skeleton.cpp:1756-1825): texel row u and column v of the
+ * fragment's world position for object `index`.  A negative remainder (the
+ * reference indexes the Mat out of bounds there) wraps to [0, size). */
+static void find_uv(const rast_state *s, const cgo_pixel *px, int size, int index, int *u, int *v)
+{
+    cgo_v4 os;
+    if (s->p->yaw != 0) {
+        os = v4_add(mat4_mul(s->Rinv, px->pos3d), s->p->camera);
+    } else {
+        os = v4_add(px->pos3d, s->p->camera);
+    }
+    const float nh = (float)(-size / 2), h = (float)(size / 2);
+    float fu = 0.0f, fv = 0.0f;
+    int iu = 0, iv = 0;
+    switch (index) {
+    case 3: fu = (nh * os.y) + h; fv = (h * os.z) + h; break;
+    case 1: fu = (nh * os.x) + h; fv = (nh * os.z) + h; break;
+    case 4: fu = (nh * os.y) + h; fv = (nh * os.z) + h; break;
+    case 2: fu = (nh * os.x) + h; fv = (nh * os.z) + h; break;
+    case 0: fu = (nh * os.x) + h; fv = (nh * os.y) + h; break;
+    default: break;
+    }
+    if (index >= 0 && index <= 4) { iu = f2i(fu); iv = f2i(fv); }
+    iu %= size; iv %= size;
+    if (iu < 0) iu += size;
+    if (iv < 0) iv += size;
+    *u = iu; *v = iv;
+}
+
+/* glm::normalize(vec4) = v * (1 / sqrt(dot(v, v))), dot = (x*x + y*y) + (z*z + w*w) */
+static cgo_v4 normalize4(cgo_v4 v)
+{
+    float px = v.x * v.x, py = v.y * v.y, pz = v.z * v.z, pw = v.w * v.w;
+    float inv = 1.0f / sqrtf((px + py) + (pz + pw));
+    return v4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
+}
 
 /* skeleton.cpp:674-688 */
 static cgo_v3 illum(const rast_state *s, const cgo_pixel *px, cgo_v4 N, float ind)
@@ -506,9 +623,42 @@ static void pixel_shader(rast_state *s, const cgo_pixel *px, const cgo_rast_tri 
         if (s->cnt) s->cnt->n_shaded++;
     } else if (px->zinv >= s->depth[o] && t->color.x >= 0) {
         cgo_v3 c = t->color;
-        cgo_v3 sc = v3_mul(c, illum(s, px, t->normal, s->indirect));
-        cgo_v3 lo = v3_mul(c, illum(s, px, t->normal, 0.0f * 1));
-        cgo_v3 hi = v3_mul(c, illum(s, px, t->normal, 0.4f * 1));
+        cgo_v4 N = t->normal;
+        float occ = 1.0f;
+        const int tex = t->texture;
+        if (tex == 1) {                                               /* marble :588-599 */
+            int u, v;
+            find_uv(s, px, MARBLE_N, t->index, &u, &v);
+            const uint8_t *m = g_tex->marble + 3 * ((size_t)u * MARBLE_N + v);
+            c = v3((float)m[2] / 255.0f, (float)m[1] / 255.0f, (float)m[0] / 255.0f);
+            const float *nz = g_noise + 3 * ((size_t)y * MARBLE_N + x);
+            N = v4_add(N, v4(nz[0], nz[1], nz[2], 0.0f));
+        } else if (tex == 2 || tex == 3) {                            /* grill :600-621, woven :622-645 */
+            int u, v;
+            find_uv(s, px, TEX_N, t->index, &u, &v);
+            const size_t k = (size_t)u * TEX_N + v;
+            if ((tex == 2 ? g_grill_op : g_woven_op)[k] != 255) {
+                s->depth[o] = 0.0f;                                   /* p.zinv = 0 (:619, :643), :665 */
+                return;
+            }
+            if (tex == 3) {
+                occ = (float)g_tex->woven_ao[(size_t)u * 3 * TEX_N + v];   /* at<uchar> on the BGR Mat */
+                occ /= 255.0f;
+            }
+            const uint8_t *nm = (tex == 2 ? g_tex->grill_normal : g_tex->woven_normal) + 3 * k;
+            N = normalize4(v4((float)nm[0] / 255.0f, (float)nm[1] / 255.0f, (float)nm[2] / 255.0f, 1.0f));
+            const uint8_t *cm = (tex == 2 ? g_tex->grill : g_tex->woven) + 3 * k;
+            c = v3((float)cm[2] / 255.0f, (float)cm[1] / 255.0f, (float)cm[0] / 255.0f);
+        }
+        cgo_v3 il = illum(s, px, N, s->indirect), il0 = illum(s, px, N, 0.0f * 1), il4 = illum(s, px, N, 0.4f * 1);
+        if (tex == 3) {
+            il = v3(il.x * occ, il.y * occ, il.z * occ);
+            il0 = v3(il0.x * occ, il0.y * occ, il0.z * occ);
+            il4 = v3(il4.x * occ, il4.y * occ, il4.z * occ);
+        }
+        cgo_v3 sc = v3_mul(c, il);
+        cgo_v3 lo = v3_mul(c, il0);
+        cgo_v3 hi = v3_mul(c, il4);
         s->indirect = 0.2f * 1;
         s->screen[3 * o + 0] = sc.x; s->screen[3 * o + 1] = sc.y; s->screen[3 * o + 2] = sc.z;
         s->low[3 * o + 0] = lo.x;    s->low[3 * o + 1] = lo.y;    s->low[3 * o + 2] = lo.z;
@@ -535,6 +685,7 @@ void cgo_rast_draw(const cgo_rast_params *p, uint32_t *argb, float *depth, int32
     memset(&s, 0, sizeof(s));
     s.p = p;
     s.cnt = cnt;
+    cgo_mat4_inverse(p->R, s.Rinv);
     int n = cgo_rast_geometry(p, tris, CAP, &s.lightPos);
     if (n > CAP) n = CAP;
     s.depth = depth ? depth : (float *)malloc(sizeof(float) * npx);

@@ -64,8 +64,16 @@ class Pixel(C.Structure):
 class RastParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", V4),
                 ("R", C.c_float * 16), ("light_scene", V4), ("light_power", V3),
-                ("indirect_first", C.c_float), ("colour_mode", C.c_int), ("pad_", C.c_int),
-                ("rand_offset", C.c_uint64)]
+                ("indirect_first", C.c_float), ("colour_mode", C.c_int), ("yaw", C.c_float),
+                ("rand_offset", C.c_uint64), ("setting", C.c_int), ("setting_boxes", C.c_int)]
+
+
+TEXTURE_MAPS = ("marble", "woven", "woven_ao", "woven_opacity", "woven_normal",
+                "grill", "grill_opacity", "grill_normal")
+
+
+class RastTextures(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in TEXTURE_MAPS]
 
 
 class RastCounters(C.Structure):
@@ -121,6 +129,9 @@ def load():
         "cgo_rast_draw": (None, [C.POINTER(RastParams), P, P, P, P, P, P,
                                  C.POINTER(RastCounters)]),
         "cgo_glibc_rand": (None, [C.c_uint64, C.c_int, P]),
+        "cgo_rast_set_textures": (None, [C.POINTER(RastTextures)]),
+        "cgo_rast_opacity_map": (None, [P, C.c_int, P]),
+        "cgo_mat4_inverse": (None, [P, P]),
         "cgo_starfield_init": (None, [P, C.c_int]),
         "cgo_starfield_update": (None, [P, C.c_int, C.c_float]),
         "cgo_starfield_draw": (None, [P, C.c_int, C.c_int, C.c_int, P]),
@@ -237,7 +248,8 @@ def starfield_draw(stars, W=320, H=256):
 
 
 def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
-                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2, colour_mode=0, rand_offset=0):
+                light=(0.0, -0.5, 0.0, 1.0), indirect_first=0.2, colour_mode=0, rand_offset=0,
+                setting=0, setting_boxes=0, yaw=0.0):
     lib = load()
     p = RastParams()
     lib.cgo_rast_default_params(C.byref(p), width, height)
@@ -249,7 +261,42 @@ def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
     p.indirect_first = indirect_first
     p.colour_mode = colour_mode
     p.rand_offset = rand_offset
+    p.setting = setting
+    p.setting_boxes = setting_boxes
+    p.yaw = yaw
     return p
+
+
+_textures_keepalive = None
+
+
+def rast_set_textures(maps):
+    """maps: {name: uint8 array (H, W, 3) BGR} for names in TEXTURE_MAPS (missing = not
+    loaded); None clears.  The arrays must stay alive while frames are drawn."""
+    global _textures_keepalive
+    lib = load()
+    if maps is None:
+        lib.cgo_rast_set_textures(None)
+        _textures_keepalive = None
+        return
+    arrs = {k: np.ascontiguousarray(v, dtype=np.uint8) for k, v in maps.items()}
+    t = RastTextures(**{k: a.ctypes.data for k, a in arrs.items()})
+    _textures_keepalive = (arrs, t)
+    lib.cgo_rast_set_textures(C.byref(t))
+
+
+def opacity_map(bgr):
+    a = np.ascontiguousarray(bgr, dtype=np.uint8)
+    out = np.zeros(a.size // 3, np.uint8)
+    load().cgo_rast_opacity_map(a.ctypes.data_as(C.c_void_p), out.size, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def mat4_inverse(R):
+    m = np.ascontiguousarray(R, dtype=np.float32).reshape(16)
+    out = np.zeros(16, np.float32)
+    load().cgo_mat4_inverse(m.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p))
+    return out
 
 
 def rast_geometry(p):

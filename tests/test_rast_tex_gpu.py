@@ -1,0 +1,122 @@
+"""GPU: rasteriser texture modes 1-3 (skeleton.cpp:588-645) against the oracle,
+bit-exact in colour, depth and shadow.  The maps are synthetic (seeded): the
+reference's own JPEGs need OpenCV's decoder and Marble2000x2000.jpg is missing,
+so no reference-rendered textured frame exists ("parity unpinned" against the
+reference; pinned against the CPU restatement, which follows the reference
+line by line)."""
+import numpy as np
+import pytest
+
+import cgamd
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+W, H, F = 320, 240, 256.0
+
+
+def _maps(seed=7, marble=False):
+    rng = np.random.default_rng(seed)
+    u = np.arange(1024)
+    block = (((u[:, None] // 48) + (u[None, :] // 48)) % 2 == 0)   # big opaque / transparent blocks
+    speck = rng.random((1024, 1024)) < 0.1                           # and isolated flipped texels
+    op = np.where(block ^ speck, 230, 40).astype(np.uint8)
+    op3 = np.repeat(op[:, :, None], 3, axis=2)
+    m = {"grill": rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8),
+         "grill_opacity": op3,
+         "grill_normal": rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8),
+         "woven": rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8),
+         "woven_ao": rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8),
+         "woven_opacity": op3[::-1].copy(),
+         "woven_normal": rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8)}
+    if marble:
+        m["marble"] = rng.integers(0, 256, (2000, 2000, 3), dtype=np.uint8)
+    return m
+
+
+@pytest.fixture(scope="module")
+def tex_ctx(ctx):
+    maps = _maps(marble=True)
+    ctx.rast_set_textures(maps)
+    oracle.rast_set_textures(maps)
+    yield ctx, maps
+    ctx.rast_set_textures(None)
+    oracle.rast_set_textures(None)
+    ctx.rast_set_scene()
+
+
+def _check(got, ref, what):
+    for nm, a, b in zip(("argb", "depth", "shadow"), got, ref):
+        a = a.view(np.uint32) if a.dtype == np.float32 else a
+        b = b.view(np.uint32) if b.dtype == np.float32 else b
+        bad = np.flatnonzero(a != b)
+        assert bad.size == 0, f"{what} {nm}: {bad.size} differ, first {bad[:5]} gpu {a[bad[:3]]} ref {b[bad[:3]]}"
+
+
+CASES = [(2, 0, 0.2, 0.0), (3, 0, 0.2, 0.0), (0, 2, 0.2, 0.0), (0, 3, 0.2, 0.0), (2, 3, 0.2, 0.0),
+         (3, 2, 0.15, 0.0), (2, 0, 0.15, 0.0), (1, 0, 0.2, 0.0), (1, 3, 0.15, 0.0), (2, 3, 0.2, 0.35),
+         (3, 1, 0.2, -0.35)]
+
+
+@pytest.mark.parametrize("setting,boxes,ind,yaw", CASES)
+def test_textured_draw_matches_oracle(tex_ctx, setting, boxes, ind, yaw):
+    ctx, _ = tex_ctx
+    R = cgamd.yaw_matrix(yaw) if yaw else None
+    p = cgamd.rast_params(W, H, F, R=R, indirect_first=ind, yaw=yaw)
+    po = oracle.rast_params(W, H, F, R=list(R) if R is not None else None, indirect_first=ind,
+                            setting=setting, setting_boxes=boxes, yaw=yaw)
+    ref = oracle.rast_draw(po)
+    ctx.rast_set_scene(*cgamd.rast_scene(setting, boxes))
+    a, d, s, _ = ctx.rast_draw(p)                       # device geometry
+    _check((a, d, s), ref, f"draw {setting}/{boxes}")
+    room, nr, bx, nb = cgamd.rast_scene(setting, boxes)
+    tris, n, light = cgamd.rast_prepare(p, room, nr, bx, nb)
+    a, d, s, _ = ctx.rast_render(tris, n, p, light)     # host geometry, caller's list
+    _check((a, d, s), ref, f"render {setting}/{boxes}")
+
+
+def test_textures_change_the_frame(tex_ctx):
+    """The textured path is exercised: frames differ from texture 0, and some
+    pixels of a grill room are see-through (depth 0 inside the box)."""
+    ctx, _ = tex_ctx
+    p = cgamd.rast_params(W, H, F)
+    ctx.rast_set_scene(*cgamd.rast_scene(0, 0))
+    a0, d0, _, _ = ctx.rast_draw(p)
+    ctx.rast_set_scene(*cgamd.rast_scene(2, 0))
+    a2, d2, _, _ = ctx.rast_draw(p)
+    assert (a0 != a2).mean() > 0.3
+    assert (d2 == 0).sum() > (d0 == 0).sum() + 1000
+
+
+def test_colour_modes_ignore_textures(tex_ctx):
+    """randColourSelect 1-2 switch before the texture branches (:575-662)."""
+    ctx, _ = tex_ctx
+    for mode in (1, 2):
+        p = cgamd.rast_params(W, H, F, colour_mode=mode, rand_offset=12_000_000)
+        po = oracle.rast_params(W, H, F, colour_mode=mode, rand_offset=12_000_000, setting=3, setting_boxes=2)
+        ref = oracle.rast_draw(po)
+        ctx.rast_set_scene(*cgamd.rast_scene(3, 2))
+        a, d, s, _ = ctx.rast_draw(p)
+        _check((a, d, s), ref, f"colour mode {mode}")
+
+
+def test_missing_maps_and_bad_selector_fail_loudly(ctx):
+    ctx.rast_set_textures(None)
+    try:
+        p = cgamd.rast_params(64, 48, 64.0)
+        ctx.rast_set_scene(*cgamd.rast_scene(3, 0))
+        with pytest.raises(RuntimeError):
+            ctx.rast_draw(p)
+        maps = _maps(seed=3)
+        ctx.rast_set_textures({k: v for k, v in maps.items() if k.startswith("grill")})
+        ctx.rast_set_scene(*cgamd.rast_scene(2, 0))
+        ctx.rast_draw(p)                                 # grill loaded: fine
+        ctx.rast_set_scene(*cgamd.rast_scene(3, 0))
+        with pytest.raises(RuntimeError):                # woven still missing
+            ctx.rast_draw(p)
+        ctx.rast_set_scene(*cgamd.rast_scene(5, 0))
+        with pytest.raises(RuntimeError):                # no texture 5
+            ctx.rast_draw(p)
+    finally:
+        ctx.rast_set_textures(None)
+        ctx.rast_set_scene()
