@@ -10,8 +10,13 @@
 // in Update() (:311-417): w s a d q e =
 // light, 1 2 = indirect, U D L R z x = camera, n m = yaw, f g = focal,
 // ' ' (SPACE) = colour mode, ESC = 'X'.
+// Texture modes (TestModelH.h:9-10 setting / settingBoxes, skeleton.cpp:135-170):
+// --setting / --setting-boxes pick the room's / boxes' texture, --textures DIR
+// holds the decoded maps as raw BGR files NAME.bgr (scripts/decode_textures.py;
+// names as cg_rast_textures: marble, woven, woven_ao, ...).
 //
 //   rasteriser [--width W] [--height H] [--focal F] [--keys KEYS] [--out FILE]
+//              [--setting S] [--setting-boxes B] [--textures DIR]
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -114,9 +119,22 @@ bool Update()
     return true;
 }
 
+// DIR/NAME.bgr of exactly `bytes` bytes, or empty if absent
+static vector<uint8_t> read_map(const string &dir, const char *name, size_t bytes)
+{
+    vector<uint8_t> v;
+    FILE *f = fopen((dir + "/" + name + ".bgr").c_str(), "rb");
+    if (!f) return v;
+    v.resize(bytes);
+    if (fread(v.data(), 1, bytes, f) != bytes) v.clear();
+    fclose(f);
+    return v;
+}
+
 int main(int argc, char *argv[])
 {
-    string out = "screenshot.bmp";
+    string out = "screenshot.bmp", tex_dir;
+    int setting = 0, setting_boxes = 0;
     for (int i = 1; i + 1 < argc; i += 2) {
         string a = argv[i];
         if (a == "--width") SCREEN_WIDTH = atoi(argv[i + 1]);
@@ -124,11 +142,27 @@ int main(int argc, char *argv[])
         else if (a == "--focal") focalLength = (float)atof(argv[i + 1]);
         else if (a == "--keys") g_keys = argv[i + 1];
         else if (a == "--out") out = argv[i + 1];
+        else if (a == "--setting") setting = atoi(argv[i + 1]);
+        else if (a == "--setting-boxes") setting_boxes = atoi(argv[i + 1]);
+        else if (a == "--textures") tex_dir = argv[i + 1];
     }
     int rc = cg_create(0, &g_ctx);
     if (rc) die(rc, "cg_create");
     screen *screen = InitializeSDL(SCREEN_WIDTH, SCREEN_HEIGHT, false);
     rast::LoadTestModel(originalroom, originalbox);          // :131
+    for (auto &t : originalroom) t.texture = setting;         // TestModelH.h:85-129
+    for (auto &t : originalbox) t.texture = setting_boxes;    // TestModelH.h:148-260
+    vector<uint8_t> maps[8];
+    if (!tex_dir.empty()) {                                   // :135-170
+        const char *names[8] = {"marble", "woven", "woven_ao", "woven_opacity", "woven_normal",
+                                "grill", "grill_opacity", "grill_normal"};
+        for (int k = 0; k < 8; ++k) maps[k] = read_map(tex_dir, names[k], k ? 1024u * 1024 * 3 : 2000u * 2000 * 3);
+        auto ptr = [&](int k) { return maps[k].empty() ? nullptr : maps[k].data(); };
+        cg_rast_textures tx = {ptr(0), ptr(1), ptr(2), ptr(3), ptr(4), ptr(5), ptr(6), ptr(7)};
+        rc = cg_rast_set_textures(g_ctx, &tx);
+        if (rc) die(rc, "cg_rast_set_textures");
+        if (tx.marble) randCalls = 3ull * 2000 * 2000;       // normalMap_marble's rand() calls (:158-170)
+    }
     rc = cg_rast_set_scene(g_ctx, reinterpret_cast<const cg_rtri *>(originalroom.data()), (int)originalroom.size(),
                            reinterpret_cast<const cg_rtri *>(originalbox.data()), (int)originalbox.size());
     if (rc) die(rc, "cg_rast_set_scene");

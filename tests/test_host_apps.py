@@ -70,3 +70,40 @@ def test_rasteriser_app_colour_modes(tmp_path):
         ref, _, _, cnt = oracle.rast_draw(p, counters=True)
         off += 3 * cnt.n_shaded
     assert np.array_equal(mg.screenshot_argb(out), ref)
+
+
+def _write_maps(d, seed=11):
+    rng = np.random.default_rng(seed)
+    u = np.arange(1024)
+    op = np.where((((u[:, None] // 40) + (u[None, :] // 40)) % 2) == 0, 200, 30).astype(np.uint8)
+    maps = {k: rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8)
+            for k in ("woven", "woven_ao", "woven_normal", "grill", "grill_normal")}
+    maps["grill_opacity"] = np.repeat(op[:, :, None], 3, axis=2)
+    maps["woven_opacity"] = np.repeat(op.T[:, :, None], 3, axis=2).copy()
+    maps["marble"] = rng.integers(0, 256, (2000, 2000, 3), dtype=np.uint8)
+    for k, v in maps.items():
+        v.tofile(os.path.join(d, k + ".bgr"))
+    return maps
+
+
+def test_rasteriser_app_textures(tmp_path):
+    """--setting 2 --setting-boxes 3 over maps from DIR/NAME.bgr: frame 1 (the
+    0.15 first-fragment quirk, found among opaque texels) then UP; and a
+    colour-mode-1 frame, whose rand() stream starts after the marble noise
+    map's 12,000,000 calls (skeleton.cpp:158-170)."""
+    maps = _write_maps(str(tmp_path))
+    oracle.rast_set_textures(maps)
+    try:
+        f32 = lambda x: float(np.float32(x))
+        args = ["--width", "320", "--height", "240", "--focal", "180", "--textures", str(tmp_path)]
+        out = _run("rasteriser", args + ["--setting", "2", "--setting-boxes", "3", "--keys", "U"], tmp_path)
+        cam_z = f32(np.float32(-3.001) + np.float32(0.1))
+        ref = oracle.rast_draw(oracle.rast_params(320, 240, 180.0, (0.0, 0.0, cam_z, 1.0), indirect_first=f32(0.2),
+                                                  setting=2, setting_boxes=3))[0]
+        assert np.array_equal(mg.screenshot_argb(out), ref)
+        out = _run("rasteriser", args + ["--setting", "1", "--keys", " "], tmp_path)
+        ref = oracle.rast_draw(oracle.rast_params(320, 240, 180.0, indirect_first=f32(0.15), colour_mode=1,
+                                                  rand_offset=12_000_000, setting=1))[0]
+        assert np.array_equal(mg.screenshot_argb(out), ref)
+    finally:
+        oracle.rast_set_textures(None)
