@@ -130,6 +130,7 @@ _SIGS = {
     "cg_rast_opacity_map": (C.c_int, [P, C.c_int, P]),
     "cg_rast_draw": (C.c_int, [P, C.POINTER(RastParams), P, P, P, C.POINTER(Stats)]),
     "cg_rast_draw_device": (C.c_int, [P, C.POINTER(RastParams), P, P, P, P]),
+    "cg_rast_draw_frames_device": (C.c_int, [P, C.POINTER(RastParams), C.c_int, P, P, P, C.c_size_t, P]),
 }
 EXPORTS = tuple(_SIGS)
 
@@ -469,6 +470,16 @@ class Context:
         self._check(self.lib.cg_rast_draw_device(self.h, C.byref(params), P(d_argb), P(d_depth) if d_depth else None,
                                                  P(d_shadow) if d_shadow else None, P(stream) if stream else None),
                     "cg_rast_draw_device")
+
+    def rast_draw_frames_device(self, params_list, d_argb, d_depth=None, d_shadow=None, frame_stride=0,
+                                stream=None):
+        """len(params_list) colour-mode-0 Draws, frame f at d_argb + f * stride pixels,
+        overlapped on the context's internal streams; `stream` waits for them."""
+        arr = (RastParams * len(params_list))(*params_list)
+        self._check(self.lib.cg_rast_draw_frames_device(
+            self.h, arr, len(params_list), P(d_argb), P(d_depth) if d_depth else None,
+            P(d_shadow) if d_shadow else None, frame_stride, P(stream) if stream else None),
+            "cg_rast_draw_frames_device")
 
     def rast_render_device(self, d_tris, n, params, light, d_argb, d_depth=None, d_shadow=None,
                            stream=None):

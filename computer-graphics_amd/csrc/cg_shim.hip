@@ -103,6 +103,14 @@ struct cg_ctx {
     // texture modes 1-3 (cg_rast_set_textures): device copies of the maps
     DevBuf tmarble, tnoise, twoven, twoven_ao, twoven_op, twoven_nrm, tgrill, tgrill_op, tgrill_nrm, rtexel;
     int tex_loaded = 0;                  // bit k: texture k renderable
+    cg_ctx *tex_owner = nullptr;         // a lane reads its parent's maps
+    // cg_rast_draw_frames_device: frames overlap on `lanes` (child contexts,
+    // each with its own stream and scratch; scene copied device to device)
+    static constexpr int kRastLanes = 8;
+    cg_ctx *lanes[kRastLanes] = {};
+    hipEvent_t lane_ev[kRastLanes] = {};
+    hipEvent_t start_ev = nullptr;
+    unsigned scene_gen = 0, lane_gen[kRastLanes] = {};
 };
 
 namespace cg {
@@ -163,6 +171,7 @@ void rast_release(cg_ctx *c)
 // the device texture maps and which textures are renderable (bit k: texture k)
 int rast_tex_maps(cg_ctx *c, RastTexMaps *m)
 {
+    if (c->tex_owner) c = c->tex_owner;
     m->marble = (const uint8_t *)c->tmarble.p;
     m->marble_noise = (const float *)c->tnoise.p;
     m->woven = (const uint8_t *)c->twoven.p;
@@ -219,6 +228,11 @@ extern "C" void cg_destroy(cg_ctx *c)
                       &c->gstart, &c->gtris};
     for (DevBuf *b : bufs) b->release();
     if (c->aux) (void)hipStreamSynchronize(c->aux);
+    for (int k = 0; k < cg_ctx::kRastLanes; ++k) {
+        if (c->lanes[k]) cg_destroy(c->lanes[k]);
+        if (c->lane_ev[k]) (void)hipEventDestroy(c->lane_ev[k]);
+    }
+    if (c->start_ev) (void)hipEventDestroy(c->start_ev);
     for (int k = 0; k < 2; ++k) {
         c->ptc[k].release(); c->pshade[k].release(); c->plat[k].release(); c->psup[k].release();
         if (c->ev_cert[k]) (void)hipEventDestroy(c->ev_cert[k]);
@@ -850,6 +864,72 @@ extern "C" int cg_rast_set_scene(cg_ctx *c, const cg_rtri *room, int n_room, con
     c->n_room = n_room;
     c->n_boxes = n_boxes;
     c->scene_tex = rast_tex_mask(room, n_room) | rast_tex_mask(boxes, n_boxes);
+    ++c->scene_gen;
+    return CG_OK;
+}
+
+extern "C" int cg_rast_draw_frames_device(cg_ctx *c, const cg_rast_params *ps, int n_frames, uint32_t *d_argb,
+                                          float *d_depth, int32_t *d_shadow, size_t frame_stride, void *stream)
+{
+    if (!c || n_frames < 0 || (n_frames && (!ps || !d_argb))) return CG_E_INVALID;
+    if (c->n_room < 0) {
+        c->err = "draw before cg_rast_set_scene";
+        return CG_E_NOSCENE;
+    }
+    if (n_frames == 0) return CG_OK;
+    const size_t px = (size_t)ps[0].width * ps[0].height;
+    const size_t stride = frame_stride ? frame_stride : px;
+    for (int f = 0; f < n_frames; ++f)
+        if (ps[f].colour_mode != 0 || ps[f].width != ps[0].width || ps[f].height != ps[0].height || stride < px)
+            return ctx_invalid(c, "draw_frames: colour mode 0 frames of one size (modes 1-2 chain rand offsets)");
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    static const int env_lanes = [] {
+        const char *e = getenv("CG_RAST_LANES");
+        return e ? std::max(1, std::min(cg_ctx::kRastLanes, atoi(e))) : 2;   // measured: 2 > 4 > 3 (C3)
+    }();
+    const int L = std::min(env_lanes, n_frames);
+    if (!c->start_ev) CG_TRY(c, hipEventCreateWithFlags(&c->start_ev, hipEventDisableTiming), "event");
+    for (int k = 0; k < L; ++k) {
+        if (!c->lanes[k]) {
+            int rc = cg_create(c->device, &c->lanes[k]);
+            if (rc) return ctx_invalid(c, "lane context");
+            c->lanes[k]->tex_owner = c;
+            CG_TRY(c, hipEventCreateWithFlags(&c->lane_ev[k], hipEventDisableTiming), "event");
+            c->lane_gen[k] = c->scene_gen - 1;
+        }
+        cg_ctx *l = c->lanes[k];
+        if (c->lane_gen[k] != c->scene_gen) {   // the parent's scene, device to device
+            CG_TRY(c, l->rroom.ensure(c->rroom.bytes), "alloc lane room");
+            CG_TRY(c, l->rboxes.ensure(c->rboxes.bytes), "alloc lane boxes");
+            CG_TRY(c, hipMemcpyAsync(l->rroom.p, c->rroom.p, c->rroom.bytes, hipMemcpyDeviceToDevice, c->stream),
+                   "lane scene");
+            CG_TRY(c, hipMemcpyAsync(l->rboxes.p, c->rboxes.p, c->rboxes.bytes, hipMemcpyDeviceToDevice, c->stream),
+                   "lane scene");
+            CG_TRY(c, hipStreamSynchronize(c->stream), "lane scene");
+            l->n_room = c->n_room;
+            l->n_boxes = c->n_boxes;
+            l->scene_tex = c->scene_tex;
+            c->lane_gen[k] = c->scene_gen;
+        }
+    }
+    CG_TRY(c, hipEventRecord(c->start_ev, st), "event");
+    for (int k = 0; k < L; ++k) CG_TRY(c, hipStreamWaitEvent(c->lanes[k]->stream, c->start_ev, 0), "lane wait");
+    for (int f = 0; f < n_frames; ++f) {
+        cg_ctx *l = c->lanes[f % L];
+        const size_t o = (size_t)f * stride;
+        int rc = rast_draw_device(l, (const cg_rtri *)l->rroom.p, l->n_room, (const cg_rtri *)l->rboxes.p, l->n_boxes,
+                                  &ps[f], d_argb + o, d_depth ? d_depth + o : nullptr, d_shadow ? d_shadow + o : nullptr,
+                                  l->stream, nullptr, nullptr, l->scene_tex);
+        if (rc) {
+            c->err = std::string("lane: ") + l->err;
+            return rc;
+        }
+    }
+    for (int k = 0; k < L; ++k) {
+        CG_TRY(c, hipEventRecord(c->lane_ev[k], c->lanes[k]->stream), "event");
+        CG_TRY(c, hipStreamWaitEvent(st, c->lane_ev[k], 0), "lane join");
+    }
     return CG_OK;
 }
 

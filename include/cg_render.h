@@ -244,6 +244,15 @@ int cg_rast_draw(cg_ctx *ctx, const cg_rast_params *p, uint32_t *argb, float *de
                  cg_stats *stats);
 int cg_rast_draw_device(cg_ctx *ctx, const cg_rast_params *p, uint32_t *d_argb, float *d_depth,
                         int32_t *d_shadow, void *stream);
+/* n_frames whole Draws (colour mode 0, one size; each frame its own params --
+ * camera, light, R, first-frame indirect) into frame f at d_argb + f *
+ * frame_stride pixels (0: W*H), likewise d_depth / d_shadow (may be NULL).
+ * The frames overlap on internal streams (the reference's main loop draws
+ * them one after another; frames are independent given their params);
+ * `stream` waits for all of them.  Colour modes 1-2 chain the rand() offset
+ * from frame to frame: use cg_rast_draw_device per frame for those. */
+int cg_rast_draw_frames_device(cg_ctx *ctx, const cg_rast_params *ps, int n_frames, uint32_t *d_argb,
+                               float *d_depth, int32_t *d_shadow, size_t frame_stride, void *stream);
 
 /* Texture modes 1-3 (skeleton.cpp:588-645; a triangle's `texture` field,
  * TestModelH.h:21: 1 marble, 2 metal grill, 3 woven wood -- set it on the
