@@ -26,8 +26,8 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench_rt 600 python bench.py --steps 200 --warmup 20
-  step bench_rast 300 python bench.py --workload rast --steps 200 --warmup 20
+  step bench_rt 600 python bench.py
+  step bench_rast 300 python bench.py --workload rast
   step bench_c4 300 python bench.py --workload c4 --steps 30 --warmup 3
   step bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 2
 fi
