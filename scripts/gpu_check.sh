@@ -34,9 +34,9 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
   step rocprof_rt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rt" -o rt -- \
-      python3 "$ROOT/bench.py" --steps 64 --warmup 16 --no-cpu-baseline
+      python3 "$ROOT/bench.py" --no-cpu-baseline
   step rocprof_rast 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rast" -o rast -- \
-      python3 "$ROOT/bench.py" --workload rast --steps 64 --warmup 16 --no-cpu-baseline
+      python3 "$ROOT/bench.py" --workload rast --no-cpu-baseline
   step rocprof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o c4 -- \
       python3 "$ROOT/bench.py" --workload c4 --steps 10 --warmup 2 --no-cpu-baseline
   step rocprof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o c5 -- \
