@@ -6,10 +6,17 @@
 // The per-wave culling certificates of cg_rt_dev.h are exact for any ray
 // bundle, so they are applied hierarchically:
 //   K0 rt_bin_primary    per (bin of 128x32 pixels, triangle): camera-ray
-//                        certificate of the bin's bundle -> bin list;
-//   K1 rt_big_primary    per 8x8 wave: certificate of the wave's bundle over
-//                        its bin list (64 candidates per pass, one per lane),
-//                        then the closest-hit walk for the 9 sub-rays; hits
+//                        certificate of the bin's bundle -> bin list, each
+//                        entry with a certified lower bound ("key") on the
+//                        float distance any ray of the bin can compute for it;
+//      rt_bin_count / rt_bin_scan / rt_bin_scatter
+//                        bucket each bin list by key (kDepthBuckets);
+//   K1 rt_big_primary    per 8x8 wave: the bin's buckets nearest first; a
+//                        candidate whose key exceeds every lane's current best
+//                        distance cannot win and is skipped (exact: ties need
+//                        distance == best <= key); certificate of the wave's
+//                        bundle (64 candidates per pass, one per lane), then
+//                        the closest-hit walk for the 9 sub-rays; hits
 //                        (index, t) to HBM, the wave's shadow-ray box too;
 //   K2 rt_bin_boxes      union of the wave boxes of each bin;
 //   K3 rt_bin_shadow     per (bin, triangle): shadow-ray certificate of the
@@ -36,6 +43,7 @@ constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
 static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
 constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
 constexpr int kMaxPend = 65536;               // pending shadow rays searched exhaustively in K5
+constexpr int kDepthBuckets = 32;             // per bin: 0 = no key (det's sign uncertain), 1.. by key
 
 // A shadow ray K4 could not resolve (skeleton.cpp:394 arguments, reference
 // float values) and where its verdict goes.
@@ -46,6 +54,12 @@ struct PendRay {
 
 struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
+    // primary bin lists with keys: key bits << 32 | triangle, unsorted and by bucket
+    unsigned long long *bin_ent, *bin_sorted;          // [n_bins][cap]
+    int *bkt_cnt;                 // [n_bins][kDepthBuckets]: counts, then scatter cursors
+    int *bkt_off;                 // [n_bins][kDepthBuckets + 1]
+    unsigned *bkt_min_inv;        // [n_bins][kDepthBuckets]: ~(smallest key bits) (0 = empty)
+    unsigned *key_lo_inv, *key_hi;                     // [n_bins]: ~min / max bits of the positive keys
     int *sbin_list, *sbin_n;
     int *hit_bi;                  // [9][rows_out * W]
     float *hit_t;
@@ -168,20 +182,178 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
     }
 }
 
-// K0: camera-ray certificate per (bin, triangle).
+// K0: camera-ray certificate per (bin, triangle), with the key: every float
+// distance fl(t |nd|) a ray of the bin computes for the triangle is >= key
+// (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23) since nd.z = f, :137).
 __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
     const int bin = blockIdx.y;
     float x0, x1, y0, y1;
     if (!bin_bundle(F, bin % B.bins_x, bin / B.bins_x, x0, x1, y0, y1)) return;
     const int base = blockIdx.x * kBinTris;
+    __shared__ int s_w[4][4];
+    __shared__ int s_base;
+    __shared__ unsigned s_lo, s_hi;
+    if (threadIdx.x == 0) {
+        s_lo = 0u;
+        s_hi = 0u;
+    }
     bool kept[4];
+    unsigned kbits[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = base + r * 256 + (int)threadIdx.x;
-        kept[r] = i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal);
+        kept[r] = false;
+        kbits[r] = 0u;
+        if (i < F.n_tris) {
+            PrimDet pd;
+            kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
+            double tlo, thi;
+            if (kept[r] && primary_t_range(tc[i], pd, tlo, thi)) {
+                const double kd = tlo * (double)F.focal * (1.0 - 0x1p-20);
+                float k = (float)kd;
+                if ((double)k > kd) k = nextafterf(k, 0.0f);
+                kbits[r] = __float_as_uint(k);
+            }
+        }
     }
-    bin_append(kept, base, B.bin_list + (size_t)bin * B.cap, B.bin_n + bin);
+    __syncthreads();
+    // append (one atomic per workgroup), and the bin's positive key range
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long m[4];
+    unsigned lo_inv = 0u, hi = 0u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = __ballot(kept[r]);
+        if (lane == 0) s_w[r][w] = __popcll(m[r]);
+        if (kept[r] && kbits[r]) {
+            lo_inv = max(lo_inv, ~kbits[r]);
+            hi = max(hi, kbits[r]);
+        }
+    }
+    for (int o = 32; o; o >>= 1) {
+        lo_inv = max(lo_inv, (unsigned)__shfl_xor((int)lo_inv, o));
+        hi = max(hi, (unsigned)__shfl_xor((int)hi, o));
+    }
+    if (lane == 0) {
+        atomicMax(&s_lo, lo_inv);
+        atomicMax(&s_hi, hi);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < 4; ++q) tot += s_w[r][q];
+        s_base = tot ? atomicAdd(B.bin_n + bin, tot) : 0;
+        if (tot) {
+            atomicMax(B.key_lo_inv + bin, s_lo);
+            atomicMax(B.key_hi + bin, s_hi);
+        }
+    }
+    __syncthreads();
+    unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
+    int off = s_base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        int before = 0;
+        for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
+        if (kept[r])
+            list[off + before + __popcll(m[r] & lt)] =
+                ((unsigned long long)kbits[r] << 32) | (unsigned)(base + r * 256 + (int)threadIdx.x);
+        for (int q = 0; q < 4; ++q) off += s_w[r][q];
+    }
+}
+
+// Bucket of a key within its bin: 0 without a key, else 1 + its place in the
+// bin's positive key range (the same float ops in count and scatter).
+__device__ __forceinline__ int depth_bucket(unsigned kbits, const BigBufs &B, int bin)
+{
+    if (kbits == 0u) return 0;
+    const float lo = __uint_as_float(~B.key_lo_inv[bin]), hi = __uint_as_float(B.key_hi[bin]);
+    const float k = __uint_as_float(kbits);
+    int b = hi > lo ? 1 + (int)((k - lo) / (hi - lo) * (float)(kDepthBuckets - 1)) : 1;
+    return min(max(b, 1), kDepthBuckets - 1);
+}
+
+// Per bin: bucket sizes and each bucket's smallest key (workgroups stride
+// over the list 1024 entries at a time).
+__global__ __launch_bounds__(256) void rt_bin_count_kernel(BigBufs B)
+{
+    const int bin = blockIdx.y, n = B.bin_n[bin];
+    if ((int)blockIdx.x * 1024 >= n) return;
+    __shared__ int s_cnt[kDepthBuckets];
+    __shared__ unsigned s_min[kDepthBuckets];
+    if (threadIdx.x < kDepthBuckets) {
+        s_cnt[threadIdx.x] = 0;
+        s_min[threadIdx.x] = 0u;
+    }
+    __syncthreads();
+    const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
+    for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024)
+        for (int e = e0 + (int)threadIdx.x; e < min(n, e0 + 1024); e += 256) {
+            const unsigned kb = (unsigned)(list[e] >> 32);
+            const int b = depth_bucket(kb, B, bin);
+            atomicAdd(&s_cnt[b], 1);
+            atomicMax(&s_min[b], ~kb);
+        }
+    __syncthreads();
+    if (threadIdx.x < kDepthBuckets && s_cnt[threadIdx.x]) {
+        atomicAdd(&B.bkt_cnt[bin * kDepthBuckets + threadIdx.x], s_cnt[threadIdx.x]);
+        atomicMax(&B.bkt_min_inv[bin * kDepthBuckets + threadIdx.x], s_min[threadIdx.x]);
+    }
+}
+
+// Per bin: bucket offsets; the counts become the scatter cursors.
+__global__ void rt_bin_scan_kernel(BigBufs B, int bins)
+{
+    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bin >= bins) return;
+    int *cnt = B.bkt_cnt + bin * kDepthBuckets, *off = B.bkt_off + bin * (kDepthBuckets + 1);
+    int acc = 0;
+    for (int b = 0; b < kDepthBuckets; ++b) {
+        off[b] = acc;
+        const int c = cnt[b];
+        cnt[b] = acc;
+        acc += c;
+    }
+    off[kDepthBuckets] = acc;
+}
+
+// Per bin: entries into their buckets (one global reservation per bucket and
+// 1024-entry chunk; workgroups stride over the list).
+__global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
+{
+    const int bin = blockIdx.y, n = B.bin_n[bin];
+    __shared__ int s_cnt[kDepthBuckets], s_base[kDepthBuckets];
+    const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
+    unsigned long long *dst = B.bin_sorted + (size_t)bin * B.cap;
+    for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024) {
+        if (threadIdx.x < kDepthBuckets) s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        unsigned long long ent[4];
+        int bk[4], loc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = e0 + r * 256 + (int)threadIdx.x;
+            bk[r] = -1;
+            loc[r] = 0;
+            ent[r] = 0ull;
+            if (e < n) {
+                ent[r] = list[e];
+                bk[r] = depth_bucket((unsigned)(ent[r] >> 32), B, bin);
+                loc[r] = atomicAdd(&s_cnt[bk[r]], 1);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < kDepthBuckets && s_cnt[threadIdx.x])
+            s_base[threadIdx.x] = atomicAdd(&B.bkt_cnt[bin * kDepthBuckets + threadIdx.x], s_cnt[threadIdx.x]);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (bk[r] >= 0) dst[s_base[bk[r]] + loc[r]] = ent[r];
+        __syncthreads();                                    // s_cnt / s_base reused by the next chunk
+    }
 }
 
 // K1: closest hits of the 9 sub-rays of every pixel.
@@ -203,8 +375,9 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
     const bool any = x0 <= x1;
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
-    const int n = any ? B.bin_n[bin] : 0;
-    const int *list = B.bin_list + (size_t)bin * B.cap;
+    const unsigned long long *list = B.bin_sorted + (size_t)bin * B.cap;
+    const int *boff = B.bkt_off + bin * (kDepthBuckets + 1);
+    const unsigned *bmin_inv = B.bkt_min_inv + bin * kDepthBuckets;
     const float m = 0.5f;
     float best[9], bt[9], len[9];
     int bi[9];
@@ -217,24 +390,49 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
         bt[s] = 0.0f;
         bi[s] = INT_MIN;
     }
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int cand = c0 + lane < n ? list[c0 + lane] : -1;
-        const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
-        unsigned long long mask = __ballot(keep);
-
-        while (mask) {
-            const int b = __builtin_ctzll(mask);
-            mask &= mask - 1ull;
-            const int k = __builtin_amdgcn_readlane(cand, b);
-            const RtTri T = tc[k];                                                    // scalar loads
-            if (active) {
-#pragma unroll
-                for (int s = 0; s < 9; ++s) {
-                    const int i = s / 3 - 1, j = s % 3 - 1;
-                    vec3 nd = -v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
-                    tri_closest(T, k, nd, len[s], best[s], bt[s], bi[s]);
+    // buckets nearest first; tb = the largest best distance of any active
+    // lane's sub-ray (FLT_MAX while one has no hit): a candidate whose key
+    // exceeds it cannot win or tie for any of them
+    float tb = FLT_MAX;
+    for (int q = 0; any && q < kDepthBuckets; ++q) {
+        const int b0 = boff[q], b1 = boff[q + 1];
+        if (b0 == b1 || __uint_as_float(~bmin_inv[q]) > tb) continue;
+        for (int c0 = b0; c0 < b1; c0 += 64) {
+            const unsigned long long ent = c0 + lane < b1 ? list[c0 + lane] : 0ull;
+            const int cand = (int)(unsigned)(ent & 0xffffffffull);
+            const bool keep = c0 + lane < b1 && !(__uint_as_float((unsigned)(ent >> 32)) > tb) &&
+                              !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
+            unsigned long long mask = __ballot(keep);
+            if (B.diag) {
+                const unsigned long long ex =
+                    __ballot(c0 + lane < b1 && !(__uint_as_float((unsigned)(ent >> 32)) > tb));
+                if (lane == 0) {
+                    atomicAdd(&B.diag[4], (unsigned long long)__popcll(ex));
+                    atomicAdd(&B.diag[5], (unsigned long long)__popcll(mask));
+                    atomicAdd(&B.diag[2], tb < FLT_MAX ? 1ull : 0ull);      // chunks walked with a finite bound
                 }
             }
+            if (!mask) continue;
+            while (mask) {
+                const int b = __builtin_ctzll(mask);
+                mask &= mask - 1ull;
+                const int k = __builtin_amdgcn_readlane(cand, b);
+                const RtTri T = tc[k];                                                // scalar loads
+                if (active) {
+#pragma unroll
+                    for (int s = 0; s < 9; ++s) {
+                        const int i = s / 3 - 1, j = s % 3 - 1;
+                        vec3 nd = -v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+                        tri_closest(T, k, nd, len[s], best[s], bt[s], bi[s]);
+                    }
+                }
+            }
+            float lm = -FLT_MAX;
+            if (active) {
+#pragma unroll
+                for (int s = 0; s < 9; ++s) lm = fmaxf(lm, best[s]);
+            }
+            tb = wave_max(lm);
         }
     }
     LaneShadowBox sb;
@@ -607,13 +805,21 @@ BigBufs big_layout(const RtFrame &F, int cap)
     return B;
 }
 
+// The per-frame counters (cleared by one memset at the start of the scratch).
+size_t big_counter_bytes(const BigBufs &B)
+{
+    const size_t bins = (size_t)B.bins_x * B.bins_y;
+    return 2 * bins * 4 + 16 + 2 * bins * kDepthBuckets * 4 + 2 * bins * 4;
+}
+
 // Bytes of device scratch for big_layout(F, cap), and its carving.
 size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return 2 * bins * B.cap * 4 + 2 * bins * 4 + 16 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
-           2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 512;
+    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 2 * bins * (size_t)B.cap * 8 +
+           bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
+           2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
 {
@@ -623,6 +829,11 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears them
     B.sbin_n = (int *)p; p += bins * 4;
     B.pend_n = (int *)p; p += 16;
+    B.bkt_cnt = (int *)p;           p += bins * kDepthBuckets * 4;
+    B.bkt_min_inv = (unsigned *)p;  p += bins * kDepthBuckets * 4;
+    B.key_lo_inv = (unsigned *)p;   p += bins * 4;
+    B.key_hi = (unsigned *)p;       p += bins * 4;
+    B.bkt_off = (int *)p;           p += bins * (kDepthBuckets + 1) * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
@@ -634,7 +845,10 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.pend_bits = (unsigned long long *)p; p += npix * 8;
     B.pend_ray = (PendRay *)p;             p += (size_t)kMaxPend * sizeof(PendRay);
     B.bin_list = (int *)p; p += bins * B.cap * 4;
-    B.sbin_list = (int *)p;
+    B.sbin_list = (int *)p; p += bins * B.cap * 4;
+    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    B.bin_ent = (unsigned long long *)p;    p += bins * (size_t)B.cap * 8;
+    B.bin_sorted = (unsigned long long *)p;
 }
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
@@ -650,12 +864,16 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         if (e != hipSuccess) return e;
     }
     const int bins = B.bins_x * B.bins_y;
-    hipError_t e = hipMemsetAsync(B.bin_n, 0, 2 * (size_t)bins * 4 + 16, st);
+    hipError_t e = hipMemsetAsync(B.bin_n, 0, big_counter_bytes(B), st);
     if (e != hipSuccess) return e;
     const bool flags_fit = 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+    const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
+    hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, B);
+    hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((bins + 255) / 256), dim3(256), 0, st, B, bins);
+    hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, B);
     hipLaunchKernelGGL(rt_big_primary_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     if (!flags_fit) {
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
@@ -692,7 +910,8 @@ void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
     unsigned long long d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpy(d, (char *)scratch + big_scratch_bytes(B, F) - 64, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess)
         fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays; "
-                "pending waves %llu with %llu certified candidates in total\n", d[0], d[7], d[3], d[6], d[1]);
+                "pending waves %llu with %llu certified candidates in total; primary candidates examined %llu, "
+                "tested %llu, chunks with a finite bound %llu\n", d[0], d[7], d[3], d[6], d[1], d[4], d[5], d[2]);
 }
 
 // Host build of the scene grid: cubic cells sized for ~2 triangle centroids
