@@ -427,7 +427,8 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
                 const float X = r.lX + (r.sX * (float)i);              // :547-548 numerators
                 const float Y = r.lY + (r.sY * (float)i);
                 vec3 N = v3(r.nx, r.ny, r.nz);
-                if (TEX && r.tex != 0) N = rast_tex_normal(A, r.tex, r.index, win_z[p], X, Y, x, y, N, texel);
+                if (TEX && r.tex != 0 && rast_tex_present(A, r.tex))
+                    N = rast_tex_normal(A, r.tex, r.index, win_z[p], X, Y, x, y, N, texel);
                 D = illum_D(A, win_z[p], X, Y, N);                     // :580-585 (:590-645)
                 tri = r.t | (x == r.first_x ? (1 << 30) : 0);
             }
@@ -551,6 +552,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         txl[r] = 0u;
         if (TEX && tri) {
             texm[r] = tris[tb & ~(1 << 30)].texture;
+            if (!rast_tex_present(A, texm[r])) texm[r] = 0;           // as the fill shaded it
             if (texm[r] != 0) {
                 const int i = threadIdx.x + 256 * r;
                 const int cy = i / kPostHW, cx = i - cy * kPostHW;

@@ -120,9 +120,21 @@ __device__ __forceinline__ void rast_find_uv(const RastArgs &A, int index, int s
 }
 
 // Opacity test of textures 2 and 3 (:602, :624); textures 0-1 always shade.
+// Whether texture tex's maps are on the device.  The host entries refuse a
+// list with a texture whose maps are missing; a device list is not inspected
+// (cg_rast_render_device), so the kernels never read a missing map: such a
+// fragment shades as texture 0.
+__device__ __forceinline__ bool rast_tex_present(const RastArgs &A, int tex)
+{
+    if (tex == 1) return A.tx.marble && A.tx.marble_noise;
+    if (tex == 2) return A.tx.grill && A.tx.grill_op && A.tx.grill_nrm;
+    if (tex == 3) return A.tx.woven && A.tx.woven_ao && A.tx.woven_op && A.tx.woven_nrm;
+    return false;
+}
+
 __device__ __forceinline__ bool rast_opaque(const RastArgs &A, int tex, int index, float zinv, float Xn, float Yn)
 {
-    if (tex != 2 && tex != 3) return true;
+    if ((tex != 2 && tex != 3) || !rast_tex_present(A, tex)) return true;
     int u, v;
     rast_find_uv(A, index, kTexN, zinv, Xn, Yn, u, v);
     return (tex == 2 ? A.tx.grill_op : A.tx.woven_op)[(size_t)u * kTexN + v] == 255;

@@ -4,6 +4,8 @@ reference's own JPEGs need OpenCV's decoder and Marble2000x2000.jpg is missing,
 so no reference-rendered textured frame exists ("parity unpinned" against the
 reference; pinned against the CPU restatement, which follows the reference
 line by line)."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -120,3 +122,27 @@ def test_missing_maps_and_bad_selector_fail_loudly(ctx):
     finally:
         ctx.rast_set_textures(None)
         ctx.rast_set_scene()
+
+
+def test_device_list_with_unloaded_texture_shades_as_texture_0(ctx):
+    """cg_rast_render_device does not inspect a device list: a triangle whose
+    texture maps are not loaded must not be read from (no fault) and shades as
+    texture 0."""
+    import torch
+    W2, H2, F2 = 160, 120, 96.0
+    maps = _maps(seed=5)
+    ctx.rast_set_textures({k: v for k, v in maps.items() if k.startswith("grill")})
+    try:
+        p = cgamd.rast_params(W2, H2, F2)
+        room, nr, bx, nb = cgamd.rast_scene(3, 0)                 # woven room, woven not loaded
+        tris, n, light = cgamd.rast_prepare(p, room, nr, bx, nb)
+        d_tris = torch.frombuffer(bytearray(tris), dtype=torch.uint8)[:n * C.sizeof(cgamd.RTri)].cuda()
+        a = torch.zeros(W2 * H2, dtype=torch.int32, device="cuda")
+        d = torch.zeros(W2 * H2, dtype=torch.float32, device="cuda")
+        s = torch.zeros(W2 * H2, dtype=torch.int32, device="cuda")
+        ctx.rast_render_device(d_tris.data_ptr(), n, p, light, a.data_ptr(), d.data_ptr(), s.data_ptr())
+        torch.cuda.synchronize()
+        ra, rd, rs = oracle.rast_draw(oracle.rast_params(W2, H2, F2))
+        _check((a.cpu().numpy().view(np.uint32), d.cpu().numpy(), s.cpu().numpy()), (ra, rd, rs), "device list")
+    finally:
+        ctx.rast_set_textures(None)
