@@ -56,6 +56,7 @@ struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
     // primary bin lists with keys: key bits << 32 | triangle, unsorted and by bucket
     unsigned long long *bin_ent, *bin_sorted;          // [n_bins][cap]
+    unsigned long long *bin_pbox, *bin_spbox;          // [n_bins][cap]: projected boxes (proj_box16), same order
     int *bkt_cnt;                 // [n_bins][kDepthBuckets]: counts, then scatter cursors
     int *bkt_off;                 // [n_bins][kDepthBuckets + 1]
     unsigned *bkt_min_inv;        // [n_bins][kDepthBuckets]: ~(smallest key bits) (0 = empty)
@@ -182,10 +183,70 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
     }
 }
 
+// Box (in the bundle's (x, y) units, 4 x int16: x0 | x1 << 16 | y0 << 32 |
+// y1 << 48) holding the direction (x, y) of every camera ray of the bin that
+// the reference's test can accept for this triangle.  With det's sign certain
+// (pd: the bin's PrimDet), an accepted hit's exact plane point X lies in the
+// triangle (v0, v0 + e1, v0 + e2) widened by sig (|e1| + |e2|), sig = 2 (Ed +
+// Eu + Ev) / dmin + 2^-21 (the barycentric slack of primary_hit_box), and the
+// ray through X has x = f (X - cam).x / (X - cam).z (nd.z = f, :137).  Without
+// a certain sign, or with the widened box reaching the camera plane, the box
+// is everything.
+constexpr unsigned long long kProjAll = 0x7fff8000ull | (0x7fff8000ull << 32);
+__device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, const cg_tri &T, const float cam[4],
+                                         float f)
+{
+    double dmin;
+    if (pd.dlo - pd.Ed > 0) dmin = pd.dlo - pd.Ed;
+    else if (pd.dhi + pd.Ed < 0) dmin = -(pd.dhi + pd.Ed);
+    else return kProjAll;
+    // the slack is used doubled below; far from the camera it is ~|s| / |e|
+    // times the rounding of the dets (1e-3 .. 1e-2 for C5's small triangles)
+    const double sig = 2.0 * (pd.Ed + pd.Eu + pd.Ev) / dmin + 0x1p-21;
+    if (!(isfinite(sig) && sig < 0.05)) return kProjAll;
+    const double v0[3] = {(double)T.v0.x, (double)T.v0.y, (double)T.v0.z};
+    const double a1[3] = {(double)c.e1x, (double)c.e1y, (double)c.e1z}, a2[3] = {(double)c.e2x, (double)c.e2y, (double)c.e2z};
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        const double p1 = v0[k] + a1[k], p2 = v0[k] + a2[k];
+        const double m = 2.0 * sig * (fabs(a1[k]) + fabs(a2[k])) + 1e-12 * (fabs(v0[k]) + fabs(a1[k]) + fabs(a2[k]) +
+                                                                      fabs((double)cam[k]));
+        lo[k] = fmin(v0[k], fmin(p1, p2)) - m - (double)cam[k];
+        hi[k] = fmax(v0[k], fmax(p1, p2)) + m - (double)cam[k];
+    }
+    if (!(lo[2] > 0.0) || !isfinite(hi[2])) return kProjAll;
+    const double fd = f;
+    auto range = [&](double l, double h, double &rl, double &rh) {
+        rl = fd * (l >= 0.0 ? l / hi[2] : l / lo[2]);
+        rh = fd * (h >= 0.0 ? h / lo[2] : h / hi[2]);
+        rl -= 1e-9 * fabs(rl) + 1e-3;
+        rh += 1e-9 * fabs(rh) + 1e-3;
+    };
+    double xl, xh, yl, yh;
+    range(lo[0], hi[0], xl, xh);
+    range(lo[1], hi[1], yl, yh);
+    auto q = [](double v, bool up) -> unsigned long long {
+        double r = up ? ceil(v) : floor(v);
+        r = fmin(fmax(r, -32768.0), 32767.0);
+        return (unsigned long long)(unsigned short)(short)(int)r;
+    };
+    if (!(isfinite(xl) && isfinite(xh) && isfinite(yl) && isfinite(yh))) return kProjAll;
+    return q(xl, false) | (q(xh, true) << 16) | (q(yl, false) << 32) | (q(yh, true) << 48);
+}
+
+// Does the box of proj_box16 meet the bundle [x0, x1] x [y0, y1]?
+__device__ __forceinline__ bool proj_meets(unsigned long long b, float x0, float x1, float y0, float y1)
+{
+    const float bx0 = (float)(short)(b & 0xffff), bx1 = (float)(short)((b >> 16) & 0xffff);
+    const float by0 = (float)(short)((b >> 32) & 0xffff), by1 = (float)(short)((b >> 48) & 0xffff);
+    return !(x1 < bx0 || x0 > bx1 || y1 < by0 || y0 > by1);
+}
+
 // K0: camera-ray certificate per (bin, triangle), with the key: every float
 // distance fl(t |nd|) a ray of the bin computes for the triangle is >= key
 // (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23) since nd.z = f, :137).
-__global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+__global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                             const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int bin = blockIdx.y;
     float x0, x1, y0, y1;
@@ -200,11 +261,13 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
     }
     bool kept[4];
     unsigned kbits[4];
+    unsigned long long pbox[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = base + r * 256 + (int)threadIdx.x;
         kept[r] = false;
         kbits[r] = 0u;
+        pbox[r] = kProjAll;
         if (i < F.n_tris) {
             PrimDet pd;
             kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
@@ -214,6 +277,14 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
                 float k = (float)kd;
                 if ((double)k > kd) k = nextafterf(k, 0.0f);
                 kbits[r] = __float_as_uint(k);
+            }
+            if (kept[r]) {
+                pbox[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                if (B.diag) {
+                    atomicAdd(&B.diag[6], pbox[r] == kProjAll ? 1ull : 0ull);
+                    const float w = (float)(short)((pbox[r] >> 16) & 0xffff) - (float)(short)(pbox[r] & 0xffff);
+                    if (pbox[r] != kProjAll) atomicAdd(&B.diag[1], (unsigned long long)w);
+                }
             }
         }
     }
@@ -252,15 +323,16 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
         }
     }
     __syncthreads();
-    unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
     int off = s_base;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         int before = 0;
         for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
-        if (kept[r])
-            list[off + before + __popcll(m[r] & lt)] =
-                ((unsigned long long)kbits[r] << 32) | (unsigned)(base + r * 256 + (int)threadIdx.x);
+        if (kept[r]) {
+            const size_t at = (size_t)bin * B.cap + off + before + __popcll(m[r] & lt);
+            B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)(base + r * 256 + (int)threadIdx.x);
+            B.bin_pbox[at] = pbox[r];
+        }
         for (int q = 0; q < 4; ++q) off += s_w[r][q];
     }
 }
@@ -331,7 +403,7 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
     for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024) {
         if (threadIdx.x < kDepthBuckets) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        unsigned long long ent[4];
+        unsigned long long ent[4], pb[4];
         int bk[4], loc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -339,8 +411,10 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
             bk[r] = -1;
             loc[r] = 0;
             ent[r] = 0ull;
+            pb[r] = kProjAll;
             if (e < n) {
                 ent[r] = list[e];
+                pb[r] = B.bin_pbox[(size_t)bin * B.cap + e];
                 bk[r] = depth_bucket((unsigned)(ent[r] >> 32), B, bin);
                 loc[r] = atomicAdd(&s_cnt[bk[r]], 1);
             }
@@ -351,7 +425,10 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if (bk[r] >= 0) dst[s_base[bk[r]] + loc[r]] = ent[r];
+            if (bk[r] >= 0) {
+                dst[s_base[bk[r]] + loc[r]] = ent[r];
+                B.bin_spbox[(size_t)bin * B.cap + s_base[bk[r]] + loc[r]] = pb[r];
+            }
         __syncthreads();                                    // s_cnt / s_base reused by the next chunk
     }
 }
@@ -398,14 +475,18 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
         const int b0 = boff[q], b1 = boff[q + 1];
         if (b0 == b1 || __uint_as_float(~bmin_inv[q]) > tb) continue;
         for (int c0 = b0; c0 < b1; c0 += 64) {
-            const unsigned long long ent = c0 + lane < b1 ? list[c0 + lane] : 0ull;
+            const bool in = c0 + lane < b1;
+            const unsigned long long ent = in ? list[c0 + lane] : 0ull;
+            const unsigned long long pb = in ? B.bin_spbox[(size_t)bin * B.cap + c0 + lane] : 0ull;
             const int cand = (int)(unsigned)(ent & 0xffffffffull);
-            const bool keep = c0 + lane < b1 && !(__uint_as_float((unsigned)(ent >> 32)) > tb) &&
+            // projected box first (no gather), then the key, then the wave certificate
+            const bool keep = in && proj_meets(pb, x0, x1, y0, y1) &&
+                              !(__uint_as_float((unsigned)(ent >> 32)) > tb) &&
                               !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
             unsigned long long mask = __ballot(keep);
             if (B.diag) {
-                const unsigned long long ex =
-                    __ballot(c0 + lane < b1 && !(__uint_as_float((unsigned)(ent >> 32)) > tb));
+                const unsigned long long ex = __ballot(in && proj_meets(pb, x0, x1, y0, y1) &&
+                                                       !(__uint_as_float((unsigned)(ent >> 32)) > tb));
                 if (lane == 0) {
                     atomicAdd(&B.diag[4], (unsigned long long)__popcll(ex));
                     atomicAdd(&B.diag[5], (unsigned long long)__popcll(mask));
@@ -817,7 +898,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 2 * bins * (size_t)B.cap * 8 +
+    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 4 * bins * (size_t)B.cap * 8 +
            bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
            2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
 }
@@ -848,11 +929,13 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.sbin_list = (int *)p; p += bins * B.cap * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.bin_ent = (unsigned long long *)p;    p += bins * (size_t)B.cap * 8;
-    B.bin_sorted = (unsigned long long *)p;
+    B.bin_sorted = (unsigned long long *)p; p += bins * (size_t)B.cap * 8;
+    B.bin_pbox = (unsigned long long *)p;   p += bins * (size_t)B.cap * 8;
+    B.bin_spbox = (unsigned long long *)p;
 }
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
-                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st)
+                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const cg_tri *d_tris)
 {
     BigBufs B = big_layout(F, F.n_tris);
     big_carve(B, F, scratch);
@@ -869,7 +952,7 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const bool flags_fit = 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+    hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, B);
     hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((bins + 255) / 256), dim3(256), 0, st, B, bins);
@@ -911,7 +994,9 @@ void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
     if (hipMemcpy(d, (char *)scratch + big_scratch_bytes(B, F) - 64, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess)
         fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays; "
                 "pending waves %llu with %llu certified candidates in total; primary candidates examined %llu, "
-                "tested %llu, chunks with a finite bound %llu\n", d[0], d[7], d[3], d[6], d[1], d[4], d[5], d[2]);
+                "tested %llu, chunks with a finite bound %llu (primary-only runs: bin entries without a projected "
+                "box = the pending-wave count, box widths summed = the candidate count)\n",
+                d[0], d[7], d[3], d[6], d[1], d[4], d[5], d[2]);
 }
 
 // Host build of the scene grid: cubic cells sized for ~2 triangle centroids

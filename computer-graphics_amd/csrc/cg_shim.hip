@@ -28,7 +28,7 @@ bool rt_lat_stamps(unsigned long long out[8], hipStream_t st);
 bool rt_shadow_stats(unsigned long long out[8], hipStream_t st);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
-                         uint32_t *, hipStream_t);
+                         uint32_t *, hipStream_t, const cg_tri *);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &);
 void rt_big_diag(const RtFrame &, void *, hipStream_t);
@@ -460,7 +460,7 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
         // large scene: binned certificates (cg_rt_big.hip)
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
         CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
-                                c->grid, c->big.p, d_out, st), "rt_big launch");
+                                c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p), "rt_big launch");
         static const bool diag = getenv("CG_RT_BIG_DIAG") != nullptr;
         if (diag) rt_big_diag(F, c->big.p, st);
         return CG_OK;
