@@ -203,7 +203,7 @@ __device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, cons
     // the slack is used doubled below; far from the camera it is ~|s| / |e|
     // times the rounding of the dets (1e-3 .. 1e-2 for C5's small triangles)
     const double sig = 2.0 * (pd.Ed + pd.Eu + pd.Ev) / dmin + 0x1p-21;
-    if (!(isfinite(sig) && sig < 0.05)) return kProjAll;
+    if (!(isfinite(sig) && sig < 4.0)) return kProjAll;   // exact bound for any slack; a wide box still prunes
     const double v0[3] = {(double)T.v0.x, (double)T.v0.y, (double)T.v0.z};
     const double a1[3] = {(double)c.e1x, (double)c.e1y, (double)c.e1z}, a2[3] = {(double)c.e2x, (double)c.e2y, (double)c.e2z};
     double lo[3], hi[3];
