@@ -707,6 +707,20 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         return;                            // the whole workgroup (m0 is uniform)
     }
     __syncthreads();                       // s_shade
+#ifndef CG_RT_OBJCOL_LDS
+#define CG_RT_OBJCOL_LDS 0   // 1: no flat loads, but measured 5 % slower (C2 52.1 vs 49.3 us)
+#endif
+    // objColor of a hit (:143-149): triangles from the LDS copy, the first
+    // sphere from registers (uniform), any other sphere by a guarded load --
+    // explicit address spaces, so no generic (flat) load per sample
+    const vec3 sph0_col = F.n_sph > 0 ? v3(sph[0].cr, sph[0].cg, sph[0].cb) : v3(0.0f, 0.0f, 0.0f);
+    auto obj_col = [&](int bi) -> vec3 {
+        const RtShade sh = s_shade[bi < 0 ? 0 : bi];
+        vec3 c = v3(sh.cr, sh.cg, sh.cb);
+        if (bi == -1) c = sph0_col;
+        if (bi < -1) c = v3(sph[-1 - bi].cr, sph[-1 - bi].cg, sph[-1 - bi].cb);
+        return c;
+    };
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
 #if CG_RT_LAT_PAIR
     // CG_RT_LAT_PAIR + 1 points per lane per step (p, p + 64, ...): one triangle
@@ -813,7 +827,11 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
                     }
                 }
 #endif
+#if CG_RT_OBJCOL_LDS
+                const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, obj_col(bi), 0, smask);
+#else
                 const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
+#endif
                 s_pt[idx] = make_float4(dl.x, dl.y, dl.z, q.w);
             }
         }
@@ -861,7 +879,11 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             if (bi == INT_MIN) continue;
             valid = true;
             pc = pc + v3(q.x, q.y, q.z);                                                  // :151-153
+#if CG_RT_OBJCOL_LDS
+            pc = pc + (obj_col(bi) * ind);                                                // :156
+#else
             pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
+#endif
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
         if (F.out_fmt == CG_PIX_ARGB8888) out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
