@@ -56,7 +56,8 @@ struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
     // primary bin lists with keys: key bits << 32 | triangle, unsorted and by bucket
     unsigned long long *bin_ent, *bin_sorted;          // [n_bins][cap]
-    unsigned long long *bin_pbox, *bin_spbox;          // [n_bins][cap]: projected boxes (proj_box16), same order
+    unsigned long long *bin_pbox, *bin_spbox;          // [n_bins][cap]: projected boxes (proj_box16), same order,
+    unsigned long long *bin_pbox2, *bin_spbox2;        // for the bin's left half and (2) right half
     int *bkt_cnt;                 // [n_bins][kDepthBuckets]: counts, then scatter cursors
     int *bkt_off;                 // [n_bins][kDepthBuckets + 1]
     unsigned *bkt_min_inv;        // [n_bins][kDepthBuckets]: ~(smallest key bits) (0 = empty)
@@ -151,6 +152,30 @@ __device__ bool bin_bundle(const RtFrame &F, int bx, int by, float &x0, float &x
     return true;
 }
 
+// The same for columns [part * kBinW / 2, (part + 1) * kBinW / 2) of the bin
+// (its left / right half); false when that half has no pixel.
+__device__ bool bin_half_bundle(const RtFrame &F, int bx, int by, int part, float &x0, float &x1, float &y0,
+                                float &y1)
+{
+    const int u0 = bx * kBinW + part * (kBinW / 2), u1 = min(F.W, u0 + kBinW / 2) - 1;
+    if (u0 > u1) return false;
+    const int L0 = by * kBinH, L1 = min(F.rows_out, L0 + kBinH) - 1;
+    const int v0 = shard_row(F, L0);
+    if (v0 >= F.H) return false;
+    const int v1 = min(shard_row(F, L1), F.H - 1);
+    x0 = y0 = FLT_MAX;
+    x1 = y1 = -FLT_MAX;
+    const int us[2] = {u0, u1}, vs[2] = {v0, v1};
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            vec4 d = mat4_mul(F.R, v4((float)(us[a] - F.W / 2), (float)(vs[b] - F.H / 2), F.focal, 1.0f));
+            x0 = fminf(x0, d.x); x1 = fmaxf(x1, d.x);
+            y0 = fminf(y0, d.y); y1 = fmaxf(y1, d.y);
+        }
+    x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    return true;
+}
+
 // Append the kept triangles of this workgroup to a bin list (one atomic per
 // workgroup); kept[r] is this thread's verdict on triangle base + r*256 + tid.
 __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *list, int *count)
@@ -193,6 +218,7 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
 // a certain sign, or with the widened box reaching the camera plane, the box
 // is everything.
 constexpr unsigned long long kProjAll = 0x7fff8000ull | (0x7fff8000ull << 32);
+constexpr unsigned long long kProjNone = 0x80007fffull | (0x80007fffull << 32);   // x0 > x1: meets nothing
 __device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, const cg_tri &T, const float cam[4],
                                          float f)
 {
@@ -261,13 +287,13 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
     }
     bool kept[4];
     unsigned kbits[4];
-    unsigned long long pbox[4];
+    unsigned long long pbox[4], pbox2[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = base + r * 256 + (int)threadIdx.x;
         kept[r] = false;
         kbits[r] = 0u;
-        pbox[r] = kProjAll;
+        pbox[r] = pbox2[r] = kProjAll;
         if (i < F.n_tris) {
             PrimDet pd;
             kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
@@ -279,7 +305,7 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
                 kbits[r] = __float_as_uint(k);
             }
             if (kept[r]) {
-                pbox[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                pbox[r] = pbox2[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
                 if (B.diag) {
                     atomicAdd(&B.diag[6], pbox[r] == kProjAll ? 1ull : 0ull);
                     const float w = (float)(short)((pbox[r] >> 16) & 0xffff) - (float)(short)(pbox[r] & 0xffff);
@@ -332,6 +358,7 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
             const size_t at = (size_t)bin * B.cap + off + before + __popcll(m[r] & lt);
             B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)(base + r * 256 + (int)threadIdx.x);
             B.bin_pbox[at] = pbox[r];
+            B.bin_pbox2[at] = pbox2[r];
         }
         for (int q = 0; q < 4; ++q) off += s_w[r][q];
     }
@@ -350,10 +377,18 @@ __device__ __forceinline__ int depth_bucket(unsigned kbits, const BigBufs &B, in
 
 // Per bin: bucket sizes and each bucket's smallest key (workgroups stride
 // over the list 1024 entries at a time).
-__global__ __launch_bounds__(256) void rt_bin_count_kernel(BigBufs B)
+__global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                           const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int bin = blockIdx.y, n = B.bin_n[bin];
     if ((int)blockIdx.x * 1024 >= n) return;
+    // an entry without a box for the whole bin (det's sign uncertain there)
+    // gets one per half of the bin where the half's own certificate allows,
+    // and none at all where it culls the triangle
+    float hx0[2], hx1[2], hy0[2], hy1[2];
+    bool hv[2];
+    for (int h = 0; h < 2; ++h)
+        hv[h] = bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, h, hx0[h], hx1[h], hy0[h], hy1[h]);
     __shared__ int s_cnt[kDepthBuckets];
     __shared__ unsigned s_min[kDepthBuckets];
     if (threadIdx.x < kDepthBuckets) {
@@ -364,6 +399,17 @@ __global__ __launch_bounds__(256) void rt_bin_count_kernel(BigBufs B)
     const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
     for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024)
         for (int e = e0 + (int)threadIdx.x; e < min(n, e0 + 1024); e += 256) {
+            const size_t at = (size_t)bin * B.cap + e;
+            if (B.bin_pbox[at] == kProjAll) {
+                const int i = (int)(unsigned)(list[e] & 0xffffffffull);
+                for (int h = 0; h < 2; ++h) {
+                    PrimDet ph;
+                    unsigned long long b = kProjNone;
+                    if (hv[h] && !cull_primary(tc[i], hx0[h], hx1[h], hy0[h], hy1[h], F.focal, &ph))
+                        b = proj_box16(tc[i], ph, tris[i], F.cam, F.focal);
+                    (h ? B.bin_pbox2 : B.bin_pbox)[at] = b;
+                }
+            }
             const unsigned kb = (unsigned)(list[e] >> 32);
             const int b = depth_bucket(kb, B, bin);
             atomicAdd(&s_cnt[b], 1);
@@ -403,7 +449,7 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
     for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024) {
         if (threadIdx.x < kDepthBuckets) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        unsigned long long ent[4], pb[4];
+        unsigned long long ent[4], pb[4], pb2[4];
         int bk[4], loc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -411,10 +457,11 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
             bk[r] = -1;
             loc[r] = 0;
             ent[r] = 0ull;
-            pb[r] = kProjAll;
+            pb[r] = pb2[r] = kProjAll;
             if (e < n) {
                 ent[r] = list[e];
                 pb[r] = B.bin_pbox[(size_t)bin * B.cap + e];
+                pb2[r] = B.bin_pbox2[(size_t)bin * B.cap + e];
                 bk[r] = depth_bucket((unsigned)(ent[r] >> 32), B, bin);
                 loc[r] = atomicAdd(&s_cnt[bk[r]], 1);
             }
@@ -428,6 +475,7 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
             if (bk[r] >= 0) {
                 dst[s_base[bk[r]] + loc[r]] = ent[r];
                 B.bin_spbox[(size_t)bin * B.cap + s_base[bk[r]] + loc[r]] = pb[r];
+                B.bin_spbox2[(size_t)bin * B.cap + s_base[bk[r]] + loc[r]] = pb2[r];
             }
         __syncthreads();                                    // s_cnt / s_base reused by the next chunk
     }
@@ -453,6 +501,8 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     const bool any = x0 <= x1;
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
     const unsigned long long *list = B.bin_sorted + (size_t)bin * B.cap;
+    const unsigned long long *pboxes = ((tx % kBinTilesX) < kBinTilesX / 2 ? B.bin_spbox : B.bin_spbox2) +
+                                       (size_t)bin * B.cap;                         // the wave's half
     const int *boff = B.bkt_off + bin * (kDepthBuckets + 1);
     const unsigned *bmin_inv = B.bkt_min_inv + bin * kDepthBuckets;
     const float m = 0.5f;
@@ -477,7 +527,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
         for (int c0 = b0; c0 < b1; c0 += 64) {
             const bool in = c0 + lane < b1;
             const unsigned long long ent = in ? list[c0 + lane] : 0ull;
-            const unsigned long long pb = in ? B.bin_spbox[(size_t)bin * B.cap + c0 + lane] : 0ull;
+            const unsigned long long pb = in ? pboxes[c0 + lane] : 0ull;
             const int cand = (int)(unsigned)(ent & 0xffffffffull);
             // projected box first (no gather), then the key, then the wave certificate
             const bool keep = in && proj_meets(pb, x0, x1, y0, y1) &&
@@ -898,7 +948,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 4 * bins * (size_t)B.cap * 8 +
+    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 6 * bins * (size_t)B.cap * 8 +
            bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
            2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
 }
@@ -931,7 +981,9 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.bin_ent = (unsigned long long *)p;    p += bins * (size_t)B.cap * 8;
     B.bin_sorted = (unsigned long long *)p; p += bins * (size_t)B.cap * 8;
     B.bin_pbox = (unsigned long long *)p;   p += bins * (size_t)B.cap * 8;
-    B.bin_spbox = (unsigned long long *)p;
+    B.bin_spbox = (unsigned long long *)p;  p += bins * (size_t)B.cap * 8;
+    B.bin_pbox2 = (unsigned long long *)p;  p += bins * (size_t)B.cap * 8;
+    B.bin_spbox2 = (unsigned long long *)p;
 }
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
@@ -954,7 +1006,7 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
-    hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, B);
+    hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((bins + 255) / 256), dim3(256), 0, st, B, bins);
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, B);
     hipLaunchKernelGGL(rt_big_primary_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
