@@ -521,49 +521,74 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     // lane's sub-ray (FLT_MAX while one has no hit): a candidate whose key
     // exceeds it cannot win or tie for any of them
     float tb = FLT_MAX;
+    // Entries passing the box and key tests are queued in LDS and certified
+    // 64 at a time (full lanes for the FP64 certificate), the queue flushed
+    // at every bucket end so that tb tightens before the next bucket.
+    __shared__ int s_q[kRtThreads / 64][128];
+    int *q_w = s_q[wave];
+    int qn = 0;                                                    // wave-uniform
+    auto certify_walk = [&](int cnt) {                             // the first cnt (<= 64) queued entries
+        const int cand = lane < cnt ? q_w[lane] : -1;
+        const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
+        unsigned long long mask = __ballot(keep);
+        if (B.diag && lane == 0) {
+            atomicAdd(&B.diag[4], (unsigned long long)cnt);
+            atomicAdd(&B.diag[5], (unsigned long long)__popcll(mask));
+            atomicAdd(&B.diag[2], tb < FLT_MAX ? 1ull : 0ull);            // batches certified with a finite bound
+        }
+        while (mask) {
+            const int b = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+            const int k = __builtin_amdgcn_readlane(cand, b);
+            const RtTri T = tc[k];                                            // scalar loads
+            if (active) {
+#pragma unroll
+                for (int s = 0; s < 9; ++s) {
+                    const int i = s / 3 - 1, j = s % 3 - 1;
+                    vec3 nd = -v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
+                    tri_closest(T, k, nd, len[s], best[s], bt[s], bi[s]);
+                }
+            }
+        }
+        float lm = -FLT_MAX;
+        if (active) {
+#pragma unroll
+            for (int s = 0; s < 9; ++s) lm = fmaxf(lm, best[s]);
+        }
+        tb = wave_max(lm);
+    };
     for (int q = 0; any && q < kDepthBuckets; ++q) {
         const int b0 = boff[q], b1 = boff[q + 1];
         if (b0 == b1 || __uint_as_float(~bmin_inv[q]) > tb) continue;
+        // the next chunk's entries are loaded while this one is scanned
+        unsigned long long ent_n = b0 + lane < b1 ? list[b0 + lane] : 0ull;
+        unsigned long long pb_n = b0 + lane < b1 ? pboxes[b0 + lane] : 0ull;
         for (int c0 = b0; c0 < b1; c0 += 64) {
             const bool in = c0 + lane < b1;
-            const unsigned long long ent = in ? list[c0 + lane] : 0ull;
-            const unsigned long long pb = in ? pboxes[c0 + lane] : 0ull;
-            const int cand = (int)(unsigned)(ent & 0xffffffffull);
-            // projected box first (no gather), then the key, then the wave certificate
-            const bool keep = in && proj_meets(pb, x0, x1, y0, y1) &&
-                              !(__uint_as_float((unsigned)(ent >> 32)) > tb) &&
-                              !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
-            unsigned long long mask = __ballot(keep);
-            if (B.diag) {
-                const unsigned long long ex = __ballot(in && proj_meets(pb, x0, x1, y0, y1) &&
-                                                       !(__uint_as_float((unsigned)(ent >> 32)) > tb));
-                if (lane == 0) {
-                    atomicAdd(&B.diag[4], (unsigned long long)__popcll(ex));
-                    atomicAdd(&B.diag[5], (unsigned long long)__popcll(mask));
-                    atomicAdd(&B.diag[2], tb < FLT_MAX ? 1ull : 0ull);      // chunks walked with a finite bound
-                }
+            const unsigned long long ent = ent_n, pb = pb_n;
+            const int cn = c0 + 64 + lane;
+            ent_n = cn < b1 ? list[cn] : 0ull;
+            pb_n = cn < b1 ? pboxes[cn] : 0ull;
+            // projected box first (no gather), then the key
+            const bool pass = in && proj_meets(pb, x0, x1, y0, y1) && !(__uint_as_float((unsigned)(ent >> 32)) > tb);
+            const unsigned long long pm = __ballot(pass);
+            if (pass) q_w[qn + __popcll(pm & ((1ull << lane) - 1ull))] = (int)(unsigned)(ent & 0xffffffffull);
+            qn += __popcll(pm);
+            __builtin_amdgcn_wave_barrier();
+            if (qn >= 64) {
+                certify_walk(64);
+                const int rest = qn - 64;
+                const int moved = lane < rest ? q_w[64 + lane] : 0;
+                __builtin_amdgcn_wave_barrier();
+                if (lane < rest) q_w[lane] = moved;
+                qn = rest;
+                __builtin_amdgcn_wave_barrier();
             }
-            if (!mask) continue;
-            while (mask) {
-                const int b = __builtin_ctzll(mask);
-                mask &= mask - 1ull;
-                const int k = __builtin_amdgcn_readlane(cand, b);
-                const RtTri T = tc[k];                                                // scalar loads
-                if (active) {
-#pragma unroll
-                    for (int s = 0; s < 9; ++s) {
-                        const int i = s / 3 - 1, j = s % 3 - 1;
-                        vec3 nd = -v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
-                        tri_closest(T, k, nd, len[s], best[s], bt[s], bi[s]);
-                    }
-                }
-            }
-            float lm = -FLT_MAX;
-            if (active) {
-#pragma unroll
-                for (int s = 0; s < 9; ++s) lm = fmaxf(lm, best[s]);
-            }
-            tb = wave_max(lm);
+        }
+        if (qn > 0) {                                              // bucket end: flush
+            certify_walk(qn);
+            qn = 0;
+            __builtin_amdgcn_wave_barrier();
         }
     }
     LaneShadowBox sb;
