@@ -116,14 +116,18 @@ __device__ __forceinline__ bool tri_shadows(const RtTri &c, vec3 start, vec3 nd,
     float K4 = sy * c.e1z - c.e1y * sz;
     float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;
     if (surely_negative(detT, det, len) || surely_beyond(detT, det, len, rmag)) return false;
-    float t = detT / det;
-    float distance = t * len;
-    if (distance < 0.0f) return false;
-    if (distance >= rmag || distance > FLT_MAX) return false;
     float Q3 = nd.y * sz - sy * nd.z;
     float K3 = c.e1y * sz - sy * c.e1z;
     float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
     float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
+    // a certain u / v rejection (uv_decide: signs and the sum against det with
+    // rounding margins) needs no divide; the conditions are a conjunction, so
+    // testing them in another order gives the same verdict
+    if (uv_decide(det, detU, detV) == 0) return false;
+    float t = detT / det;
+    float distance = t * len;
+    if (distance < 0.0f) return false;
+    if (distance >= rmag || distance > FLT_MAX) return false;
     float u = detU / det;
     float v = detV / det;
     return (u >= 0) && (v >= 0) && ((u + v) <= 1);
@@ -880,14 +884,22 @@ __global__ __launch_bounds__(256) void rt_pending_test_kernel(RtFrame F, const R
         ok[r] = i < F.n_tris;
         T[r] = tc[ok[r] ? i : 0];
     }
-    for (int p = 0; p < np; ++p) {
-        const PendRay R = B.pend_ray[p];                       // uniform: scalar loads
-        const vec3 o = v3(R.ox, R.oy, R.oz), nd = v3(R.nx, R.ny, R.nz);
-        bool hit = false;
+    // rays staged through LDS 256 at a time (one coalesced load per thread)
+    __shared__ PendRay s_r[256];
+    for (int p0 = 0; p0 < np; p0 += 256) {
+        if (p0 + (int)threadIdx.x < np) s_r[threadIdx.x] = B.pend_ray[p0 + threadIdx.x];
+        __syncthreads();
+        const int pn = min(256, np - p0);
+        for (int p = 0; p < pn; ++p) {
+            const PendRay R = s_r[p];                          // uniform: LDS broadcast
+            const vec3 o = v3(R.ox, R.oy, R.oz), nd = v3(R.nx, R.ny, R.nz);
+            bool hit = false;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hit |= ok[r] && tri_shadows(T[r], o, nd, R.len, R.rmag);
-        if (__ballot(hit) != 0ull && (threadIdx.x & 63) == __builtin_ctzll(__ballot(hit)))
-            atomicOr(&B.sh_bits[R.pix], 1ull << R.bit);
+            for (int r = 0; r < 4; ++r) hit |= ok[r] && tri_shadows(T[r], o, nd, R.len, R.rmag);
+            const unsigned long long hm = __ballot(hit);
+            if (hm != 0ull && (threadIdx.x & 63) == __builtin_ctzll(hm)) atomicOr(&B.sh_bits[R.pix], 1ull << R.bit);
+        }
+        __syncthreads();
     }
 }
 
