@@ -15,7 +15,10 @@ constexpr int kRtTileH = 8;
 constexpr int kRtThreads = 256;
 constexpr int kLatTileW = 16, kLatTileH = 15;   // RT lattice kernel tile (cg_rt.hip): 33 x 31 lattice rays
 constexpr int kSup = 4;              // lattice super-tile: kSup x kSup tiles (two-level certificates)
-constexpr int kMaxFrameBatch = 16;   // frames per batched RT launch (cg_rt_render_frames_device)
+#ifndef CG_RT_FRAME_BATCH
+#define CG_RT_FRAME_BATCH 32   // 16: ~1 % slower on C2 (more launch tails)
+#endif
+constexpr int kMaxFrameBatch = CG_RT_FRAME_BATCH;   // frames per batched RT launch (cg_rt_render_frames_device)
 
 constexpr int kMaxBlocks = 64;       // row blocks of one assembly launch (cg_rt_assemble_device)
 

@@ -155,7 +155,7 @@ int cg_rt_render_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const
  * RGB24, d_out is a byte buffer and pixel offsets count 3 bytes).  All
  * cameras share width and height; lights and the shard are common.  Frames of
  * the unrotated one-light camera that differ only in cameraPos are rendered up
- * to 16 per kernel launch (a whole GPU's worth of tiles even for a small
+ * to 32 per kernel launch (a whole GPU's worth of tiles even for a small
  * shard); others are enqueued one by one.  Each frame equals
  * cg_rt_render_device's. */
 int cg_rt_render_frames_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cams,

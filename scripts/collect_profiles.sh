@@ -13,6 +13,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   cp gpurun_out/pmc_rt_$c/pmc_counter_collection.csv profiles/r01_pmc_rt_$c.csv
   cp gpurun_out/pmc_rast_$c/pmc_counter_collection.csv profiles/r01_pmc_rast_$c.csv
 done
-CG_PMC_RT_FRAMES=16 python3 scripts/pmc_summary.py r01 > /dev/null
+CG_PMC_RT_FRAMES=32 python3 scripts/pmc_summary.py r01 > /dev/null
 python3 scripts/sq_summary.py rt_lattice_kernel > /dev/null
 echo collected

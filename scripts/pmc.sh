@@ -8,7 +8,7 @@ cd /tmp
 for wl in rt rast; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$ROOT/gpurun_out/pmc_${wl}_$ctr" -o pmc -- \
-        python3 "$ROOT/bench.py" --workload $wl --steps 64 --warmup 16 --no-cpu-baseline \
+        python3 "$ROOT/bench.py" --workload $wl --steps 64 --warmup 32 --no-cpu-baseline \
         > "$ROOT/gpurun_out/pmc_${wl}_$ctr.log" 2>&1 || { echo "pmc $wl $ctr failed"; exit 1; }
   done
 done

@@ -32,7 +32,7 @@ for wl, kernels in DOMINANT.items():
     det = {k: {"fetch_kib_raw": f.get(k), "write_kib": w.get(k),
                "hbm_bytes_corrected": (2 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024} for k in kernels}
     out.setdefault(wl, {}).update({"kernels": det,
-                                   "frames_per_launch": int(os.environ.get("CG_PMC_RT_FRAMES", "16")) if wl == "rt" else 1,
+                                   "frames_per_launch": int(os.environ.get("CG_PMC_RT_FRAMES", "32")) if wl == "rt" else 1,
                                    "hbm_bytes_per_launch": sum(d["hbm_bytes_corrected"] for d in det.values())})
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 with open(path, "w") as fh:
