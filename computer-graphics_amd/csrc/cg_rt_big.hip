@@ -55,12 +55,14 @@ struct PendRay {
 struct BigBufs {
     int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
     // primary bin lists with keys: key bits << 32 | triangle, unsorted and by bucket
-    unsigned long long *bin_ent, *bin_sorted;          // [n_bins][cap]
-    unsigned long long *bin_pbox, *bin_spbox;          // [n_bins][cap]: projected boxes (proj_box16), same order,
-    unsigned long long *bin_pbox2, *bin_spbox2;        // for the bin's left half and (2) right half
-    int *bkt_cnt;                 // [n_bins][kDepthBuckets]: counts, then scatter cursors
-    int *bkt_off;                 // [n_bins][kDepthBuckets + 1]
-    unsigned *bkt_min_inv;        // [n_bins][kDepthBuckets]: ~(smallest key bits) (0 = empty)
+    unsigned long long *bin_ent;                       // [n_bins][cap], unsorted
+    unsigned long long *bin_pbox, *bin_pbox2;          // [n_bins][cap]: projected boxes (proj_box16) for the
+                                                       // bin's left / right half, same order
+    // per half-bin (sub = 2 bin + half): the entries whose box meets the half, by bucket
+    unsigned long long *bin_sorted, *bin_spbox;        // [2 n_bins][cap]
+    int *bkt_cnt;                 // [2 n_bins][kDepthBuckets]: counts, then scatter cursors
+    int *bkt_off;                 // [2 n_bins][kDepthBuckets + 1]
+    unsigned *bkt_min_inv;        // [2 n_bins][kDepthBuckets]: ~(smallest key bits) (0 = empty)
     unsigned *key_lo_inv, *key_hi;                     // [n_bins]: ~min / max bits of the positive keys
     int *sbin_list, *sbin_n;
     int *hit_bi;                  // [9][rows_out * W]
@@ -393,11 +395,11 @@ __global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTr
     bool hv[2];
     for (int h = 0; h < 2; ++h)
         hv[h] = bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, h, hx0[h], hx1[h], hy0[h], hy1[h]);
-    __shared__ int s_cnt[kDepthBuckets];
-    __shared__ unsigned s_min[kDepthBuckets];
-    if (threadIdx.x < kDepthBuckets) {
-        s_cnt[threadIdx.x] = 0;
-        s_min[threadIdx.x] = 0u;
+    __shared__ int s_cnt[2][kDepthBuckets];
+    __shared__ unsigned s_min[2][kDepthBuckets];
+    if (threadIdx.x < 2 * kDepthBuckets) {
+        (&s_cnt[0][0])[threadIdx.x] = 0;
+        (&s_min[0][0])[threadIdx.x] = 0u;
     }
     __syncthreads();
     const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
@@ -416,21 +418,24 @@ __global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTr
             }
             const unsigned kb = (unsigned)(list[e] >> 32);
             const int b = depth_bucket(kb, B, bin);
-            atomicAdd(&s_cnt[b], 1);
-            atomicMax(&s_min[b], ~kb);
+            for (int h = 0; h < 2; ++h)
+                if (hv[h] && proj_meets((h ? B.bin_pbox2 : B.bin_pbox)[at], hx0[h], hx1[h], hy0[h], hy1[h])) {
+                    atomicAdd(&s_cnt[h][b], 1);
+                    atomicMax(&s_min[h][b], ~kb);
+                }
         }
     __syncthreads();
-    if (threadIdx.x < kDepthBuckets && s_cnt[threadIdx.x]) {
-        atomicAdd(&B.bkt_cnt[bin * kDepthBuckets + threadIdx.x], s_cnt[threadIdx.x]);
-        atomicMax(&B.bkt_min_inv[bin * kDepthBuckets + threadIdx.x], s_min[threadIdx.x]);
+    if (threadIdx.x < 2 * kDepthBuckets && (&s_cnt[0][0])[threadIdx.x]) {   // [h][b] -> sub 2 bin + h
+        atomicAdd(&B.bkt_cnt[2 * bin * kDepthBuckets + threadIdx.x], (&s_cnt[0][0])[threadIdx.x]);
+        atomicMax(&B.bkt_min_inv[2 * bin * kDepthBuckets + threadIdx.x], (&s_min[0][0])[threadIdx.x]);
     }
 }
 
-// Per bin: bucket offsets; the counts become the scatter cursors.
-__global__ void rt_bin_scan_kernel(BigBufs B, int bins)
+// Per half-bin: bucket offsets; the counts become the scatter cursors.
+__global__ void rt_bin_scan_kernel(BigBufs B, int subs)
 {
-    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
-    if (bin >= bins) return;
+    const int bin = blockIdx.x * blockDim.x + threadIdx.x;   // sub-bin
+    if (bin >= subs) return;
     int *cnt = B.bkt_cnt + bin * kDepthBuckets, *off = B.bkt_off + bin * (kDepthBuckets + 1);
     int acc = 0;
     for (int b = 0; b < kDepthBuckets; ++b) {
@@ -442,45 +447,52 @@ __global__ void rt_bin_scan_kernel(BigBufs B, int bins)
     off[kDepthBuckets] = acc;
 }
 
-// Per bin: entries into their buckets (one global reservation per bucket and
-// 1024-entry chunk; workgroups stride over the list).
-__global__ __launch_bounds__(256) void rt_bin_scatter_kernel(BigBufs B)
+// Per bin: each entry into the bucket lists of the half-bins its box meets
+// (one global reservation per half, bucket and 1024-entry chunk).
+__global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs B)
 {
     const int bin = blockIdx.y, n = B.bin_n[bin];
-    __shared__ int s_cnt[kDepthBuckets], s_base[kDepthBuckets];
+    float hx0[2], hx1[2], hy0[2], hy1[2];
+    bool hv[2];
+    for (int h = 0; h < 2; ++h)
+        hv[h] = bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, h, hx0[h], hx1[h], hy0[h], hy1[h]);
+    __shared__ int s_cnt[2][kDepthBuckets], s_base[2][kDepthBuckets];
     const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
-    unsigned long long *dst = B.bin_sorted + (size_t)bin * B.cap;
     for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024) {
-        if (threadIdx.x < kDepthBuckets) s_cnt[threadIdx.x] = 0;
+        if (threadIdx.x < 2 * kDepthBuckets) (&s_cnt[0][0])[threadIdx.x] = 0;
         __syncthreads();
-        unsigned long long ent[4], pb[4], pb2[4];
-        int bk[4], loc[4];
+        unsigned long long ent[4], pb[4][2];
+        int bk[4], loc[4][2];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int e = e0 + r * 256 + (int)threadIdx.x;
             bk[r] = -1;
-            loc[r] = 0;
+            loc[r][0] = loc[r][1] = -1;
             ent[r] = 0ull;
-            pb[r] = pb2[r] = kProjAll;
+            pb[r][0] = pb[r][1] = kProjNone;
             if (e < n) {
                 ent[r] = list[e];
-                pb[r] = B.bin_pbox[(size_t)bin * B.cap + e];
-                pb2[r] = B.bin_pbox2[(size_t)bin * B.cap + e];
+                pb[r][0] = B.bin_pbox[(size_t)bin * B.cap + e];
+                pb[r][1] = B.bin_pbox2[(size_t)bin * B.cap + e];
                 bk[r] = depth_bucket((unsigned)(ent[r] >> 32), B, bin);
-                loc[r] = atomicAdd(&s_cnt[bk[r]], 1);
+                for (int h = 0; h < 2; ++h)
+                    if (hv[h] && proj_meets(pb[r][h], hx0[h], hx1[h], hy0[h], hy1[h]))
+                        loc[r][h] = atomicAdd(&s_cnt[h][bk[r]], 1);
             }
         }
         __syncthreads();
-        if (threadIdx.x < kDepthBuckets && s_cnt[threadIdx.x])
-            s_base[threadIdx.x] = atomicAdd(&B.bkt_cnt[bin * kDepthBuckets + threadIdx.x], s_cnt[threadIdx.x]);
+        if (threadIdx.x < 2 * kDepthBuckets && (&s_cnt[0][0])[threadIdx.x])
+            (&s_base[0][0])[threadIdx.x] = atomicAdd(&B.bkt_cnt[2 * bin * kDepthBuckets + threadIdx.x],
+                                                      (&s_cnt[0][0])[threadIdx.x]);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if (bk[r] >= 0) {
-                dst[s_base[bk[r]] + loc[r]] = ent[r];
-                B.bin_spbox[(size_t)bin * B.cap + s_base[bk[r]] + loc[r]] = pb[r];
-                B.bin_spbox2[(size_t)bin * B.cap + s_base[bk[r]] + loc[r]] = pb2[r];
-            }
+            for (int h = 0; h < 2; ++h)
+                if (loc[r][h] >= 0) {
+                    const size_t at = (size_t)(2 * bin + h) * B.cap + s_base[h][bk[r]] + loc[r][h];
+                    B.bin_sorted[at] = ent[r];
+                    B.bin_spbox[at] = pb[r][h];
+                }
         __syncthreads();                                    // s_cnt / s_base reused by the next chunk
     }
 }
@@ -504,11 +516,11 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
     const bool any = x0 <= x1;
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
-    const unsigned long long *list = B.bin_sorted + (size_t)bin * B.cap;
-    const unsigned long long *pboxes = ((tx % kBinTilesX) < kBinTilesX / 2 ? B.bin_spbox : B.bin_spbox2) +
-                                       (size_t)bin * B.cap;                         // the wave's half
-    const int *boff = B.bkt_off + bin * (kDepthBuckets + 1);
-    const unsigned *bmin_inv = B.bkt_min_inv + bin * kDepthBuckets;
+    const int sub = 2 * bin + ((tx % kBinTilesX) < kBinTilesX / 2 ? 0 : 1);          // the wave's half-bin
+    const unsigned long long *list = B.bin_sorted + (size_t)sub * B.cap;
+    const unsigned long long *pboxes = B.bin_spbox + (size_t)sub * B.cap;
+    const int *boff = B.bkt_off + sub * (kDepthBuckets + 1);
+    const unsigned *bmin_inv = B.bkt_min_inv + sub * kDepthBuckets;
     const float m = 0.5f;
     float best[9], bt[9], len[9];
     int bi[9];
@@ -977,7 +989,7 @@ BigBufs big_layout(const RtFrame &F, int cap)
 size_t big_counter_bytes(const BigBufs &B)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y;
-    return 2 * bins * 4 + 16 + 2 * bins * kDepthBuckets * 4 + 2 * bins * 4;
+    return 2 * bins * 4 + 16 + 4 * bins * kDepthBuckets * 4 + 2 * bins * 4;
 }
 
 // Bytes of device scratch for big_layout(F, cap), and its carving.
@@ -985,8 +997,8 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 6 * bins * (size_t)B.cap * 8 +
-           bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
+    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 7 * bins * (size_t)B.cap * 8 +
+           2 * bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
            2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
@@ -997,11 +1009,11 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears them
     B.sbin_n = (int *)p; p += bins * 4;
     B.pend_n = (int *)p; p += 16;
-    B.bkt_cnt = (int *)p;           p += bins * kDepthBuckets * 4;
-    B.bkt_min_inv = (unsigned *)p;  p += bins * kDepthBuckets * 4;
+    B.bkt_cnt = (int *)p;           p += 2 * bins * kDepthBuckets * 4;
+    B.bkt_min_inv = (unsigned *)p;  p += 2 * bins * kDepthBuckets * 4;
     B.key_lo_inv = (unsigned *)p;   p += bins * 4;
     B.key_hi = (unsigned *)p;       p += bins * 4;
-    B.bkt_off = (int *)p;           p += bins * (kDepthBuckets + 1) * 4;
+    B.bkt_off = (int *)p;           p += 2 * bins * (kDepthBuckets + 1) * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
@@ -1016,11 +1028,10 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.sbin_list = (int *)p; p += bins * B.cap * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.bin_ent = (unsigned long long *)p;    p += bins * (size_t)B.cap * 8;
-    B.bin_sorted = (unsigned long long *)p; p += bins * (size_t)B.cap * 8;
     B.bin_pbox = (unsigned long long *)p;   p += bins * (size_t)B.cap * 8;
-    B.bin_spbox = (unsigned long long *)p;  p += bins * (size_t)B.cap * 8;
     B.bin_pbox2 = (unsigned long long *)p;  p += bins * (size_t)B.cap * 8;
-    B.bin_spbox2 = (unsigned long long *)p;
+    B.bin_sorted = (unsigned long long *)p; p += 2 * bins * (size_t)B.cap * 8;
+    B.bin_spbox = (unsigned long long *)p;
 }
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
@@ -1044,8 +1055,8 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
-    hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((bins + 255) / 256), dim3(256), 0, st, B, bins);
-    hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, B);
+    hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((2 * bins + 255) / 256), dim3(256), 0, st, B, 2 * bins);
+    hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
     hipLaunchKernelGGL(rt_big_primary_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     if (!flags_fit) {
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
