@@ -43,6 +43,7 @@ constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
 static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
 constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
 constexpr int kMaxPend = 65536;               // pending shadow rays searched exhaustively in K5
+constexpr int kSupBins = 4;                   // a super-bin is 4 x 4 bins (512 x 128 px)
 constexpr int kDepthBuckets = 32;             // per bin: 0 = no key (det's sign uncertain), 1.. by key
 
 // A shadow ray K4 could not resolve (skeleton.cpp:394 arguments, reference
@@ -75,6 +76,8 @@ struct BigBufs {
     int *pend_n;                  // shadow rays left unresolved by K4 (counter, after bin_n/sbin_n)
     struct PendRay *pend_ray;     // [kMaxPend]
     int cap, bins_x, bins_y, tiles_x, tiles_y;
+    int *sup_list, *sup_n;        // [n_sups][cap], [n_sups]: triangles the super-bin's certificate keeps
+    int sups_x, sups_y;
     unsigned long long *diag;     // CG_RT_BIG_DIAG: [waves, survivors, walk steps, lit rays, primary cands, primary kept]
 };
 
@@ -145,6 +148,28 @@ __device__ bool bin_bundle(const RtFrame &F, int bx, int by, float &x0, float &x
     const int v0 = shard_row(F, L0);
     if (v0 >= F.H) return false;                      // padding rows only
     const int v1 = min(shard_row(F, L1), F.H - 1);   // shard_row is increasing in L
+    x0 = y0 = FLT_MAX;
+    x1 = y1 = -FLT_MAX;
+    const int us[2] = {u0, u1}, vs[2] = {v0, v1};
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            vec4 d = mat4_mul(F.R, v4((float)(us[a] - F.W / 2), (float)(vs[b] - F.H / 2), F.focal, 1.0f));
+            x0 = fminf(x0, d.x); x1 = fmaxf(x1, d.x);
+            y0 = fminf(y0, d.y); y1 = fmaxf(y1, d.y);
+        }
+    x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    return true;
+}
+
+// The same for the super-bin (sx, sy): kSupBins x kSupBins bins.
+__device__ bool sup_bundle(const RtFrame &F, int sx, int sy, float &x0, float &x1, float &y0, float &y1)
+{
+    const int u0 = sx * kSupBins * kBinW, u1 = min(F.W, u0 + kSupBins * kBinW) - 1;
+    const int L0 = sy * kSupBins * kBinH, L1 = min(F.rows_out, L0 + kSupBins * kBinH) - 1;
+    if (u0 > u1 || L0 > L1) return false;
+    const int v0 = shard_row(F, L0);
+    if (v0 >= F.H) return false;
+    const int v1 = min(shard_row(F, L1), F.H - 1);
     x0 = y0 = FLT_MAX;
     x1 = y1 = -FLT_MAX;
     const int us[2] = {u0, u1}, vs[2] = {v0, v1};
@@ -274,6 +299,24 @@ __device__ __forceinline__ bool proj_meets(unsigned long long b, float x0, float
     return !(x1 < bx0 || x0 > bx1 || y1 < by0 || y0 > by1);
 }
 
+// K00: camera-ray certificate per (super-bin, triangle) -> super list; the
+// bins then certify only their super-bin's survivors (a bin's bundle lies in
+// its super-bin's, so a triangle the super-bin culls is culled for the bin).
+__global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int sup = blockIdx.y;
+    float x0, x1, y0, y1;
+    if (!sup_bundle(F, sup % B.sups_x, sup / B.sups_x, x0, x1, y0, y1)) return;
+    const int base = blockIdx.x * kBinTris;
+    bool kept[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = base + r * 256 + (int)threadIdx.x;
+        kept[r] = i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal);
+    }
+    bin_append(kept, base, B.sup_list + (size_t)sup * B.cap, B.sup_n + sup);
+}
+
 // K0: camera-ray certificate per (bin, triangle), with the key: every float
 // distance fl(t |nd|) a ray of the bin computes for the triangle is >= key
 // (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23) since nd.z = f, :137).
@@ -283,24 +326,31 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
     const int bin = blockIdx.y;
     float x0, x1, y0, y1;
     if (!bin_bundle(F, bin % B.bins_x, bin / B.bins_x, x0, x1, y0, y1)) return;
-    const int base = blockIdx.x * kBinTris;
+    const int bx = bin % B.bins_x, by = bin / B.bins_x;
+    const int sup = (bx / kSupBins) + (by / kSupBins) * B.sups_x;
+    const int ns = B.sup_n[sup];
+    const int *slist = B.sup_list + (size_t)sup * B.cap;
     __shared__ int s_w[4][4];
     __shared__ int s_base;
     __shared__ unsigned s_lo, s_hi;
+    for (int base = blockIdx.x * kBinTris; base < ns; base += gridDim.x * kBinTris) {   // over the super list
     if (threadIdx.x == 0) {
         s_lo = 0u;
         s_hi = 0u;
     }
     bool kept[4];
+    int tri[4];
     unsigned kbits[4];
     unsigned long long pbox[4], pbox2[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int i = base + r * 256 + (int)threadIdx.x;
+        const int e = base + r * 256 + (int)threadIdx.x;
+        const int i = e < ns ? slist[e] : 0;
+        tri[r] = i;
         kept[r] = false;
         kbits[r] = 0u;
         pbox[r] = pbox2[r] = kProjAll;
-        if (i < F.n_tris) {
+        if (e < ns) {
             PrimDet pd;
             kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
             double tlo, thi;
@@ -362,11 +412,13 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
         for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
         if (kept[r]) {
             const size_t at = (size_t)bin * B.cap + off + before + __popcll(m[r] & lt);
-            B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)(base + r * 256 + (int)threadIdx.x);
+            B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)tri[r];
             B.bin_pbox[at] = pbox[r];
             B.bin_pbox2[at] = pbox2[r];
         }
         for (int q = 0; q < 4; ++q) off += s_w[r][q];
+    }
+    __syncthreads();                                        // s_w / s_base / s_lo reused by the next chunk
     }
 }
 
@@ -982,6 +1034,8 @@ BigBufs big_layout(const RtFrame &F, int cap)
     B.bins_y = (F.rows_out + kBinH - 1) / kBinH;
     B.tiles_x = (F.W + 7) / 8;
     B.tiles_y = (F.rows_out + 7) / 8;
+    B.sups_x = (B.bins_x + kSupBins - 1) / kSupBins;
+    B.sups_y = (B.bins_y + kSupBins - 1) / kSupBins;
     return B;
 }
 
@@ -989,7 +1043,8 @@ BigBufs big_layout(const RtFrame &F, int cap)
 size_t big_counter_bytes(const BigBufs &B)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y;
-    return 2 * bins * 4 + 16 + 4 * bins * kDepthBuckets * 4 + 2 * bins * 4;
+    const size_t sups = (size_t)B.sups_x * B.sups_y;
+    return 2 * bins * 4 + 16 + 4 * bins * kDepthBuckets * 4 + 2 * bins * 4 + sups * 4;
 }
 
 // Bytes of device scratch for big_layout(F, cap), and its carving.
@@ -998,6 +1053,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
     return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 7 * bins * (size_t)B.cap * 8 +
+           (size_t)B.sups_x * B.sups_y * B.cap * 4 +
            2 * bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
            2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
 }
@@ -1013,6 +1069,7 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.bkt_min_inv = (unsigned *)p;  p += 2 * bins * kDepthBuckets * 4;
     B.key_lo_inv = (unsigned *)p;   p += bins * 4;
     B.key_hi = (unsigned *)p;       p += bins * 4;
+    B.sup_n = (int *)p;             p += (size_t)B.sups_x * B.sups_y * 4;
     B.bkt_off = (int *)p;           p += 2 * bins * (kDepthBuckets + 1) * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
@@ -1031,7 +1088,8 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.bin_pbox = (unsigned long long *)p;   p += bins * (size_t)B.cap * 8;
     B.bin_pbox2 = (unsigned long long *)p;  p += bins * (size_t)B.cap * 8;
     B.bin_sorted = (unsigned long long *)p; p += 2 * bins * (size_t)B.cap * 8;
-    B.bin_spbox = (unsigned long long *)p;
+    B.bin_spbox = (unsigned long long *)p;  p += 2 * bins * (size_t)B.cap * 8;
+    B.sup_list = (int *)p;
 }
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
@@ -1052,7 +1110,9 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const bool flags_fit = 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    hipLaunchKernelGGL(rt_bin_primary_kernel, bgrid, dim3(256), 0, st, F, d_tc, d_tris, B);
+    hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, B.sups_x * B.sups_y), dim3(256), 0, st, F, d_tc, B);
+    hipLaunchKernelGGL(rt_bin_primary_kernel, dim3(std::min(64, (int)bgrid.x), bins), dim3(256), 0, st, F, d_tc,
+                       d_tris, B);
     const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((2 * bins + 255) / 256), dim3(256), 0, st, B, 2 * bins);
