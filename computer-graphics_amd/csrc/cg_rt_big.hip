@@ -879,6 +879,7 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
     return mat4_mul(F.R, v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f));   // :126-128
 }
 
+template <bool kNbr>
 __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
@@ -907,7 +908,17 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
                 int k = -1;
                 if (bi >= 0 && tri_shadows(tc[bi], q.origin, q.nd, q.len, q.rmag)) k = bi;
                 else if (last >= 0 && tri_shadows(tc[last], q.origin, q.nd, q.len, q.rmag)) k = last;
-                else k = grid_blocker(B.grid, tc, q, &gtests);
+                if (kNbr) {
+                    // unresolved rays try up to two distinct blockers the wave's
+                    // other rays found (neighbouring pixels, same light)
+                    unsigned long long have = __ballot(k >= 0);
+                    for (int rep = 0; rep < 2 && have != 0ull && __ballot(k < 0) != 0ull; ++rep) {
+                        const int kn = __shfl(k, __builtin_ctzll(have));
+                        have &= ~__ballot(k == kn);
+                        if (k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
+                    }
+                }
+                if (k < 0) k = grid_blocker(B.grid, tc, q, &gtests);
                 const unsigned long long bit = 1ull << (s * F.n_lights + l);
                 if (k >= 0) {
                     shadowed |= bit;
@@ -1122,7 +1133,12 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
     } else if (F.n_lights > 0) {
-        hipLaunchKernelGGL(rt_shadow_hints_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        static const bool nbr = !getenv("CG_RT_HINT_NBR") || atoi(getenv("CG_RT_HINT_NBR")) != 0;
+        if (nbr)
+            hipLaunchKernelGGL(rt_shadow_hints_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        else
+            hipLaunchKernelGGL(rt_shadow_hints_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+                               B);
         hipLaunchKernelGGL(rt_pending_test_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
     }
     hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
