@@ -909,10 +909,10 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
                 if (bi >= 0 && tri_shadows(tc[bi], q.origin, q.nd, q.len, q.rmag)) k = bi;
                 else if (last >= 0 && tri_shadows(tc[last], q.origin, q.nd, q.len, q.rmag)) k = last;
                 if (kNbr) {
-                    // unresolved rays try up to eight distinct blockers the wave's
+                    // unresolved rays try up to sixteen distinct blockers the wave's
                     // other rays found (neighbouring pixels, same light)
                     unsigned long long have = __ballot(k >= 0);
-                    for (int rep = 0; rep < 8 && have != 0ull && __ballot(k < 0) != 0ull; ++rep) {
+                    for (int rep = 0; rep < 16 && have != 0ull && __ballot(k < 0) != 0ull; ++rep) {
                         const int kn = __shfl(k, __builtin_ctzll(have));
                         have &= ~__ballot(k == kn);
                         if (k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
