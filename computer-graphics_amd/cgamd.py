@@ -131,8 +131,18 @@ _SIGS = {
     "cg_rast_draw": (C.c_int, [P, C.POINTER(RastParams), P, P, P, C.POINTER(Stats)]),
     "cg_rast_draw_device": (C.c_int, [P, C.POINTER(RastParams), P, P, P, P]),
     "cg_rast_draw_frames_device": (C.c_int, [P, C.POINTER(RastParams), C.c_int, P, P, P, C.c_size_t, P]),
+    "cg_image_jpeg_info": (C.c_int, [P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "cg_image_decode_jpeg": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
+    "cg_image_decode_jpeg_device": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t, P]),
 }
 EXPORTS = tuple(_SIGS)
+
+# skeleton.cpp:135-146: the file each cg_rast_textures map is read from
+TEXTURE_FILES = {"marble": "Marble2000x2000.jpg", "woven": "woven1024x1024.jpg",
+                 "woven_ao": "Wood_wicker_003_ambientOcclusion.jpg",
+                 "woven_opacity": "Wood_wicker_003_opacity.jpg", "woven_normal": "Wood_wicker_003_normal.jpg",
+                 "grill": "Metal_Grill_002_basecolor.jpg", "grill_opacity": "Metal_Grill_002_opacity.jpg",
+                 "grill_normal": "Metal_Grill_002_normal.jpg"}
 
 _lib = None
 
@@ -242,7 +252,7 @@ def rast_params(width, height, focal=512.0, cam=(0.0, 0.0, -3.001, 1.0), R=None,
     p = RastParams()
     p.width, p.height, p.focal = width, height, focal
     p.camera = Vec4(*cam)
-    p.R = R if R is not None else identity16()
+    p.R = (C.c_float * 16)(*R) if R is not None else identity16()
     p.light_scene = Vec4(*light)
     f = float(np.float32(20.0) * np.float32(1.0))
     p.light_power = Vec3(f, f, f)
@@ -312,6 +322,16 @@ def rast_prepare(params, room=None, nr=None, boxes=None, nb=None):
     n = lib.cg_rast_prepare(C.byref(params), room, nr, boxes, nb, out, n, C.byref(light))
     return out, n, light
 
+
+
+def jpeg_info(data: bytes):
+    """(width, height, channels) of a JPEG file's bytes (host-only, no GPU)."""
+    lib = load()
+    buf = np.frombuffer(data, np.uint8)
+    w, h, ch = C.c_int(), C.c_int(), C.c_int()
+    if lib.cg_image_jpeg_info(buf.ctypes.data_as(P), buf.size, C.byref(w), C.byref(h), C.byref(ch)) != 0:
+        raise ValueError("not a supported JPEG")
+    return w.value, h.value, ch.value
 
 class Context:
     """One GPU context (cg_create/cg_destroy)."""
@@ -452,6 +472,27 @@ class Context:
             arrs[k] = a
         t = RastTextures(**{k: a.ctypes.data for k, a in arrs.items()})
         self._check(self.lib.cg_rast_set_textures(self.h, C.byref(t)), "cg_rast_set_textures")
+
+    def decode_jpeg(self, data: bytes) -> np.ndarray:
+        """cv::imread(..., CV_LOAD_IMAGE_UNCHANGED) of JPEG bytes (skeleton.cpp:135-146) on
+        this context's GPU: uint8 (H, W, 3) BGR or (H, W) gray."""
+        w, h, ch = jpeg_info(data)
+        buf = np.frombuffer(data, np.uint8)
+        out = np.zeros((h, w, ch), np.uint8)
+        self._check(self.lib.cg_image_decode_jpeg(self.h, buf.ctypes.data_as(P), buf.size, out.ctypes.data_as(P),
+                                                  out.size), "cg_image_decode_jpeg")
+        return out if ch == 3 else out[:, :, 0]
+
+    def load_textures_jpeg(self, directory: str) -> dict:
+        """Decode the reference's texture files found in `directory` (names as
+        skeleton.cpp:135-146) -> {map name: BGR array}, ready for rast_set_textures."""
+        maps = {}
+        for name, fn in TEXTURE_FILES.items():
+            path = os.path.join(directory, fn)
+            if os.path.exists(path):
+                with open(path, "rb") as f:
+                    maps[name] = self.decode_jpeg(f.read())
+        return maps
 
     def rast_draw(self, params, want_depth=True, want_shadow=True):
         """Whole Draw on the device (geometry + fill + post)."""

@@ -98,6 +98,7 @@ struct cg_ctx {
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
     DevBuf rpc, rtl, rrnd, rjt;          // colour modes 1-2 (cg_rast_colour.hip)
     DevBuf sstars, sframe;               // starfield (cg_starfield.hip)
+    DevBuf iscratch;                     // JPEG decode (cg_image.hip)
     int n_room = -1, n_boxes = 0;
     int scene_tex = 0;                   // bit k: the uploaded room/boxes carry texture k
     // texture modes 1-3 (cg_rast_set_textures): device copies of the maps
@@ -136,12 +137,14 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
     case 14: b = &c->sstars; break;
     case 15: b = &c->sframe; break;
     case 16: b = &c->rtexel; break;
+    case 17: b = &c->iscratch; break;
     default: *e = hipErrorInvalidValue; return nullptr;
     }
     *e = b->ensure(bytes);
     return *e == hipSuccess ? b->p : nullptr;
 }
 hipStream_t ctx_stream(cg_ctx *c) { return c->stream; }
+int ctx_device(cg_ctx *c) { return c->device; }
 int ctx_invalid(cg_ctx *c, const char *what)
 {
     c->err = what;

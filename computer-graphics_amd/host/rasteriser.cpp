@@ -12,8 +12,8 @@
 // ' ' (SPACE) = colour mode, ESC = 'X'.
 // Texture modes (TestModelH.h:9-10 setting / settingBoxes, skeleton.cpp:135-170):
 // --setting / --setting-boxes pick the room's / boxes' texture, --textures DIR
-// holds the decoded maps as raw BGR files NAME.bgr (scripts/decode_textures.py;
-// names as cg_rast_textures: marble, woven, woven_ao, ...).
+// holds the reference's JPEG maps under their own file names (Textures/ in the
+// reference tree); they are decoded like cv::imread does (cg_image_decode_jpeg).
 //
 //   rasteriser [--width W] [--height H] [--focal F] [--keys KEYS] [--out FILE]
 //              [--setting S] [--setting-boxes B] [--textures DIR]
@@ -119,15 +119,29 @@ bool Update()
     return true;
 }
 
-// DIR/NAME.bgr of exactly `bytes` bytes, or empty if absent
-static vector<uint8_t> read_map(const string &dir, const char *name, size_t bytes)
+// cv::imread(DIR/FILE, CV_LOAD_IMAGE_UNCHANGED) (:135-146) for a map of
+// side n: BGR bytes, or empty if the file is absent (the reference then holds
+// an empty Mat and must not render that texture).
+static vector<uint8_t> read_map(const string &dir, const char *file, int n)
 {
-    vector<uint8_t> v;
-    FILE *f = fopen((dir + "/" + name + ".bgr").c_str(), "rb");
+    vector<uint8_t> bytes, v;
+    FILE *f = fopen((dir + "/" + file).c_str(), "rb");
     if (!f) return v;
-    v.resize(bytes);
-    if (fread(v.data(), 1, bytes, f) != bytes) v.clear();
+    uint8_t chunk[1 << 16];
+    size_t got;
+    while ((got = fread(chunk, 1, sizeof(chunk), f)) > 0) bytes.insert(bytes.end(), chunk, chunk + got);
     fclose(f);
+    int w = 0, h = 0, ch = 0;
+    int rc = cg_image_jpeg_info(bytes.data(), bytes.size(), &w, &h, &ch);
+    if (rc) die(rc, file);
+    if (w != n || h != n || ch != 3) {
+        cerr << file << ": " << w << "x" << h << "x" << ch << ", the reference indexes it as " << n << "x" << n
+             << " BGR" << endl;
+        exit(1);
+    }
+    v.resize((size_t)n * n * 3);
+    rc = cg_image_decode_jpeg(g_ctx, bytes.data(), bytes.size(), v.data(), v.size());
+    if (rc) die(rc, "cg_image_decode_jpeg");
     return v;
 }
 
@@ -154,9 +168,11 @@ int main(int argc, char *argv[])
     for (auto &t : originalbox) t.texture = setting_boxes;    // TestModelH.h:148-260
     vector<uint8_t> maps[8];
     if (!tex_dir.empty()) {                                   // :135-170
-        const char *names[8] = {"marble", "woven", "woven_ao", "woven_opacity", "woven_normal",
-                                "grill", "grill_opacity", "grill_normal"};
-        for (int k = 0; k < 8; ++k) maps[k] = read_map(tex_dir, names[k], k ? 1024u * 1024 * 3 : 2000u * 2000 * 3);
+        const char *files[8] = {"Marble2000x2000.jpg", "woven1024x1024.jpg",
+                                "Wood_wicker_003_ambientOcclusion.jpg", "Wood_wicker_003_opacity.jpg",
+                                "Wood_wicker_003_normal.jpg", "Metal_Grill_002_basecolor.jpg",
+                                "Metal_Grill_002_opacity.jpg", "Metal_Grill_002_normal.jpg"};
+        for (int k = 0; k < 8; ++k) maps[k] = read_map(tex_dir, files[k], k ? 1024 : 2000);
         auto ptr = [&](int k) { return maps[k].empty() ? nullptr : maps[k].data(); };
         cg_rast_textures tx = {ptr(0), ptr(1), ptr(2), ptr(3), ptr(4), ptr(5), ptr(6), ptr(7)};
         rc = cg_rast_set_textures(g_ctx, &tx);

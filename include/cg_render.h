@@ -283,6 +283,21 @@ int cg_rast_set_textures(cg_ctx *ctx, const cg_rast_textures *tex);
  * n texels in, n bytes (0 or 255) out. */
 int cg_rast_opacity_map(const uint8_t *bgr, int n, uint8_t *out);
 
+/* ---- texture loading (rasteriser/Source/skeleton.cpp:135-146) ----------- */
+/* The reference loads its maps with cv::imread(path, CV_LOAD_IMAGE_UNCHANGED)
+ * (OpenCV 3.4 over IJG libjpeg 9).  These decode a JPEG file's bytes to what
+ * that call returns: row-major BGR (3 bytes per pixel; gray for 1-component
+ * files), bit-identical to libjpeg 9's islow IDCT with 16x16 scaled chroma.
+ * Baseline and progressive Huffman JPEG, 8-bit, 1 or 3 components, 4:4:4 or
+ * 4:2:0; anything else is CG_E_INVALID.  Entropy decoding runs on the host,
+ * the IDCT and colour conversion on the context's GPU. */
+int cg_image_jpeg_info(const uint8_t *data, size_t n, int *width, int *height, int *channels);
+/* out: caller-owned host buffer of >= width * height * channels bytes (cap). */
+int cg_image_decode_jpeg(cg_ctx *ctx, const uint8_t *data, size_t n, uint8_t *out, size_t cap);
+/* Same into device memory, enqueued on `stream` (NULL: the context's). */
+int cg_image_decode_jpeg_device(cg_ctx *ctx, const uint8_t *data, size_t n, uint8_t *d_out, size_t cap,
+                                void *stream);
+
 /* ---- starfield (starfield/Source/skeleton.cpp) -------------------------- */
 /* n stars as (x, y, z) float triples from glibc rand() (:41-46, seed 1). */
 int cg_starfield_init(float *stars, int n);

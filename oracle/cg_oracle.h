@@ -13,13 +13,18 @@
  *
  * Pinning: the RT restatement is pinned bit-exactly by the reference's own
  * golden image raytracer/screenshot.bmp (tests/golden/rt_screenshot_320x256.bmp).
- * The RAST restatement is pinned by the reference's first-party
- * ComputePolygonRows KAT (rasteriser/Source/skeleton.cpp:183-199) and by the
- * frame fingerprints recorded in SURVEY.md section 8c.
+ * The RAST restatement is pinned bit-exactly by the reference's own
+ * rasteriser/screenshot.bmp (tests/golden/rast_screenshot_900x720.bmp.xz):
+ * at the key state that produced it (metal grill room, texels decoded as
+ * OpenCV 3.4 + libjpeg 9 do, cg_oracle_jpeg.c) every pixel that does not
+ * depend on the missing marble map -- 602,987 of 644,764 -- matches
+ * (tests/test_rast_screenshot.py); plus the first-party ComputePolygonRows
+ * KAT (rasteriser/Source/skeleton.cpp:183-199).
  */
 #ifndef CG_ORACLE_H
 #define CG_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -153,6 +158,14 @@ int  cgo_rast_polygon_rows(const cgo_pixel *vp, cgo_pixel *left, cgo_pixel *righ
  * are float[3*W*H]. */
 void cgo_rast_draw(const cgo_rast_params *p, uint32_t *argb, float *depth, int32_t *shadow,
                    float *screen_buf, float *low_buf, float *high_buf, cgo_rast_counters *cnt);
+
+/* ------------------------- texture loading ----------------------------- */
+/* cv::imread(path, CV_LOAD_IMAGE_UNCHANGED) of a JPEG as the reference's
+ * OpenCV 3.4 + IJG libjpeg 9 build returns it (see cg_oracle_jpeg.c): BGR (or
+ * gray) bytes, row-major.  0 or a negative error (-1 not a JPEG, -2 memory,
+ * -3 corrupt, -4 unsupported, -5 out too small). */
+int cgo_jpeg_info(const uint8_t *data, size_t n, int *w, int *h, int *nc);
+int cgo_jpeg_decode(const uint8_t *data, size_t n, uint8_t *out, size_t cap);
 
 /* ---------------------------- starfield -------------------------------- */
 void cgo_starfield_init(float *stars, int n);

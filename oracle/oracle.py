@@ -132,6 +132,9 @@ def load():
         "cgo_rast_set_textures": (None, [C.POINTER(RastTextures)]),
         "cgo_rast_opacity_map": (None, [P, C.c_int, P]),
         "cgo_mat4_inverse": (None, [P, P]),
+        "cgo_jpeg_info": (C.c_int, [P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_int)]),
+        "cgo_jpeg_decode": (C.c_int, [P, C.c_size_t, P, C.c_size_t]),
         "cgo_starfield_init": (None, [P, C.c_int]),
         "cgo_starfield_update": (None, [P, C.c_int, C.c_float]),
         "cgo_starfield_draw": (None, [P, C.c_int, C.c_int, C.c_int, P]),
@@ -297,6 +300,21 @@ def mat4_inverse(R):
     out = np.zeros(16, np.float32)
     load().cgo_mat4_inverse(m.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p))
     return out
+
+
+def jpeg_decode(data: bytes) -> np.ndarray:
+    """cv::imread(..., CV_LOAD_IMAGE_UNCHANGED) of JPEG bytes as the reference's OpenCV 3.4 +
+    libjpeg 9 build returns it: uint8 (H, W, 3) BGR or (H, W) gray."""
+    lib = load()
+    buf = np.frombuffer(data, np.uint8)
+    w, h, nc = C.c_int(), C.c_int(), C.c_int()
+    if lib.cgo_jpeg_info(buf.ctypes.data, buf.size, C.byref(w), C.byref(h), C.byref(nc)) != 0:
+        raise ValueError("not a JPEG")
+    out = np.zeros((h.value, w.value, nc.value), np.uint8)
+    r = lib.cgo_jpeg_decode(buf.ctypes.data, buf.size, out.ctypes.data, out.size)
+    if r != 0:
+        raise ValueError(f"cgo_jpeg_decode failed: {r}")
+    return out if nc.value == 3 else out[:, :, 0]
 
 
 def rast_geometry(p):

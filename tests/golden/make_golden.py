@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import hashlib
+import math
 import json
 import os
 import struct
@@ -149,6 +150,79 @@ def screenshot_argb(path=os.path.join(HERE, "rt_screenshot_320x256.bmp")) -> np.
     if h > 0:
         img = img[::-1]          # BMP rows are bottom-up
     return np.ascontiguousarray(img).reshape(-1)
+
+
+# ---- rasteriser/screenshot.bmp (the reference's own RAST output, 900 x 720) ----
+# TestModelH.h:9-10 as committed: setting = 2 (metal grill room), settingBoxes = 1
+# (marble boxes; Marble2000x2000.jpg is absent from the reference tree).  The
+# camera/light state was recovered by a silhouette fit of the room followed by a
+# search over Update()'s key counts and orders (rasteriser/Source/skeleton.cpp:
+# 334-409); every screenshot pixel that does not depend on the marble texels
+# then matches the restatement bit for bit.  Key letters as the host app's
+# --keys: n/m yaw, L/R/U/D camera x/z, a/d/q/e/w/s light.
+RAST_SCREENSHOT_KEYS = "m" + "n" * 6 + "L" * 20 + "R" * 2 + "U" * 14 + "d" * 3 + "a" * 13 + "e" * 8 + "s" * 4
+RAST_SCREENSHOT_PATH = os.path.join(HERE, "rast_screenshot_900x720.bmp.xz")
+TEXTURE_DIR = os.path.join(HERE, "textures")
+
+
+def rast_replay_keys(keys):
+    """Update() (rasteriser skeleton.cpp:334-409) over scripted keys: the globals after them.
+    float32 vec4 adds; yaw -= 0.174533 is a double subtraction rounded to float; R from
+    cos/sin of the float yaw (correctly rounded)."""
+    f = np.float32
+    cam = [f(0), f(0), f(-3.001), f(1)]
+    light = [f(0), f(-0.5), f(0), f(1)]
+    yaw, focal = f(0), f(512)
+    step = {"U": (cam, 2, 0.1), "D": (cam, 2, -0.1), "L": (cam, 0, -0.1), "R": (cam, 0, 0.1),
+            "z": (cam, 1, -0.1), "x": (cam, 1, 0.1), "w": (light, 2, 0.1), "s": (light, 2, -0.1),
+            "a": (light, 0, -0.1), "d": (light, 0, 0.1), "q": (light, 1, -0.1), "e": (light, 1, 0.1)}
+    for k in keys:
+        if k in step:
+            vec, i, d = step[k]
+            vec[i] = f(vec[i] + f(d))
+        elif k in "nm":
+            yaw = f(float(yaw) + (0.174533 if k == "m" else -0.174533))
+        elif k in "fg":
+            focal = f(focal + (5 if k == "f" else -5))
+    R = None
+    if any(k in "nm" for k in keys):
+        c, s_ = f(math.cos(float(yaw))), f(math.sin(float(yaw)))
+        R = [1.0 if i % 5 == 0 else 0.0 for i in range(16)]
+        R[0], R[2], R[8], R[10] = float(c), -float(s_), float(s_), float(c)
+    return dict(cam=[float(v) for v in cam], light=[float(v) for v in light], yaw=float(yaw),
+                focal=float(focal), R=R)
+
+
+def rast_screenshot_argb() -> np.ndarray:
+    import lzma
+    with open(RAST_SCREENSHOT_PATH, "rb") as fh:
+        raw = lzma.decompress(fh.read())
+    tmp = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"cg_rast_shot_{os.getpid()}.bmp")
+    with open(tmp, "wb") as fh:
+        fh.write(raw)
+    try:
+        return screenshot_argb(tmp)
+    finally:
+        os.unlink(tmp)
+
+
+def rast_screenshot_params(width=900, height=720):
+    st = rast_replay_keys(RAST_SCREENSHOT_KEYS)
+    return oracle.rast_params(width, height, st["focal"], tuple(st["cam"]), st["R"], tuple(st["light"]),
+                              f32(0.2), 0, 0, setting=2, setting_boxes=1, yaw=st["yaw"])
+
+
+def texture_jpegs():
+    """{map name: JPEG bytes} of the reference texture files kept in tests/golden/textures."""
+    files = {"woven": "woven1024x1024.jpg", "woven_ao": "Wood_wicker_003_ambientOcclusion.jpg",
+             "woven_opacity": "Wood_wicker_003_opacity.jpg", "woven_normal": "Wood_wicker_003_normal.jpg",
+             "grill": "Metal_Grill_002_basecolor.jpg", "grill_opacity": "Metal_Grill_002_opacity.jpg",
+             "grill_normal": "Metal_Grill_002_normal.jpg"}
+    out = {}
+    for k, fn in files.items():
+        with open(os.path.join(TEXTURE_DIR, fn), "rb") as fh:
+            out[k] = fh.read()
+    return out
 
 
 def mg_sha_ok(a, want):

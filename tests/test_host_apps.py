@@ -73,21 +73,33 @@ def test_rasteriser_app_colour_modes(tmp_path):
 
 
 def _write_maps(d, seed=11):
+    """Synthetic maps written as JPEG files under the reference's names (4:2:0, progressive
+    and baseline); returns what the reference's imread would hand Draw (the oracle's
+    libjpeg-9 restatement of the same bytes)."""
+    from PIL import Image
+    import cgamd
     rng = np.random.default_rng(seed)
     u = np.arange(1024)
     op = np.where((((u[:, None] // 40) + (u[None, :] // 40)) % 2) == 0, 200, 30).astype(np.uint8)
-    maps = {k: rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8)
-            for k in ("woven", "woven_ao", "woven_normal", "grill", "grill_normal")}
-    maps["grill_opacity"] = np.repeat(op[:, :, None], 3, axis=2)
-    maps["woven_opacity"] = np.repeat(op.T[:, :, None], 3, axis=2).copy()
-    maps["marble"] = rng.integers(0, 256, (2000, 2000, 3), dtype=np.uint8)
-    for k, v in maps.items():
-        v.tofile(os.path.join(d, k + ".bgr"))
+    def smooth(n):
+        base = rng.integers(0, 256, (n // 16, n // 16, 3), dtype=np.uint8)
+        img = np.repeat(np.repeat(base, 16, 0), 16, 1)
+        return (img // 2 + rng.integers(0, 128, (n, n, 3), dtype=np.uint8)).astype(np.uint8)
+    rgb = {k: smooth(1024) for k in ("woven", "woven_ao", "woven_normal", "grill", "grill_normal")}
+    rgb["grill_opacity"] = np.repeat(op[:, :, None], 3, axis=2)
+    rgb["woven_opacity"] = np.repeat(op.T[:, :, None], 3, axis=2).copy()
+    rgb["marble"] = smooth(2000)
+    maps = {}
+    for i, (k, v) in enumerate(rgb.items()):
+        path = os.path.join(d, cgamd.TEXTURE_FILES[k])
+        Image.fromarray(v).save(path, quality=90, subsampling=2, progressive=bool(i % 2))
+        with open(path, "rb") as fh:
+            maps[k] = oracle.jpeg_decode(fh.read())
     return maps
 
 
 def test_rasteriser_app_textures(tmp_path):
-    """--setting 2 --setting-boxes 3 over maps from DIR/NAME.bgr: frame 1 (the
+    """--setting 2 --setting-boxes 3 over the JPEG maps in DIR: frame 1 (the
     0.15 first-fragment quirk, found among opaque texels) then UP; and a
     colour-mode-1 frame, whose rand() stream starts after the marble noise
     map's 12,000,000 calls (skeleton.cpp:158-170)."""
