@@ -38,6 +38,26 @@ void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b);
 constexpr int kSetupThreads = 256;
 constexpr int kRastMaxRows = 4096;   // LDS rows per triangle in span setup (H <= 4096)
 
+// Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.
+// The row-ordered kernels renumber them so that each group of kXcdRows rows
+// is handled by one XCD (a row's records are then fetched into one L2, not
+// all eight), with the groups dealt round-robin to keep the XCDs balanced
+// (row cost varies a lot over the frame).  A kernel whose row group is
+// `per_group` workgroups wide launches xcd_grid(H, per_group) of them.
+constexpr int kXcds = 8, kXcdRows = 8;
+__host__ __device__ constexpr int xcd_grid(int H, int per_group)
+{
+    return kXcds * ((((H + kXcdRows - 1) / kXcdRows) + kXcds - 1) / kXcds) * per_group;
+}
+// -> row group of this workgroup (-1: idle padding) and its index m within the group
+__device__ __forceinline__ int xcd_group(int H, int per_group, int &m)
+{
+    const int k = (int)(blockIdx.x % kXcds), l = (int)(blockIdx.x / kXcds);
+    m = l % per_group;
+    const int g = k + kXcds * (l / per_group);
+    return g < (H + kXcdRows - 1) / kXcdRows ? g : -1;
+}
+
 struct Pix {                // rasteriser Pixel (:88-94) minus w
     int x, y;
     float zinv, X, Y;
@@ -246,7 +266,7 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
                 }
             }
         }
-        spans[(size_t)t * A.H + ylo + k] = s;
+        spans[(size_t)(ylo + k) * A.n + t] = s;              // row-major: a row's spans are contiguous
     }
     if (shade_tri) {
         __syncthreads();
@@ -267,7 +287,10 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
                                                        const int *__restrict__ first_tri,
                                                        RowRec *__restrict__ recs, int *__restrict__ count)
 {
-    const int y = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int m;
+    const int g = xcd_group(A.H, kXcdRows / 4, m);
+    if (g < 0) return;
+    const int y = g * kXcdRows + m * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (y >= A.H) return;
     const int ft = A.want_first ? *first_tri : INT_MAX;
@@ -281,7 +304,7 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
         if (t < n) {
             h = hdr[t];
             if (h.ylo <= y && y <= h.yhi) {
-                sp = spans[(size_t)t * A.H + y];
+                sp = spans[(size_t)y * A.n + t];
                 // fragments x in [lx, rx - 1] (:504) intersecting [0, W)
                 keep = sp.rx > sp.lx && sp.rx - 1 >= 0 && sp.lx <= A.W - 1;
             }
@@ -305,60 +328,46 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
     if (lane == 0) count[y] = c;
 }
 
-// Per-pixel shade state between fill and post: .x = triangle index (as bits;
-// -1 none; bit 30 = shaded by the frame's first fragment), .yzw = D.
-// One wave per kFillPx-pixel row segment, kFillPx/64 pixels per lane, state in
+// Colour mode 0: fill -> post state, 4 bytes per pixel: 1 + the row record of
+// the last shading fragment (0 none) | the shadow mark << 31.  The post-pass
+// rebuilds that fragment from the record -- zinv = lz + sz * i (:543) and the
+// pos3d numerators with the same float ops, the normal, the texels -- and
+// evaluates calculateIllumination there, so the fill keeps only what its
+// ordered walk decides.
+constexpr uint32_t kStShadow = 0x80000000u;
+
+// One wave per kFillPx-pixel row segment, one pixel per lane, state in
 // registers; records walked in triangle order (the reference's ordered
 // z-buffer), one uniform overlap test per record.
-#ifndef CG_RAST_FILL_PX
-#define CG_RAST_FILL_PX 64
-#endif
-constexpr int kFillPx = CG_RAST_FILL_PX;   // pixels per wave; 128 / 256 measured 3 % / 10 % slower (C3)
-constexpr int kFillPerLane = kFillPx / 64;
+constexpr int kFillPx = 64;   // pixels per wave; 128 / 256 measured 3 % / 10 % slower (C3, round 1)
 
 // TEX: texture modes 1-3 possible (A.textured): a fragment of texture 2/3
 // that passes the depth test but hits a transparent texel sets the depth to 0
-// and shades nothing (:619, :643, :665) -- decided in the ordered walk; the
-// winner's texel word goes to texel_out for the post-pass.
+// and shades nothing (:619, :643, :665) -- decided in the ordered walk.
 template <bool TEX>
-__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRec *__restrict__ recs,
-                                                       const int *__restrict__ count,
-                                                       float4 *__restrict__ state,
-                                                       float *__restrict__ depth_out,
-                                                       int32_t *__restrict__ shadow_out,
-                                                       uint32_t *__restrict__ texel_out)
+__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec *__restrict__ recs,
+                                                       const int *__restrict__ count, uint32_t *__restrict__ state,
+                                                       float *__restrict__ depth_out, int32_t *__restrict__ shadow_out)
 {
-    RastArgs A = A0;
-    if (A.d_light) {                                      // light from the device geometry (:223)
-        const cg_vec4 L = *A.d_light;
-        A.light[0] = L.x; A.light[1] = L.y; A.light[2] = L.z;
-    }
     const int segs = (A.W + kFillPx - 1) / kFillPx;
     // wave-uniform by construction; readfirstlane lets the compiler keep the
-    // record walk on the scalar unit (s_load per record, uniform branches)
-    const int seg = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // record walk on the scalar unit (uniform branches)
+    int m;
+    const int g = xcd_group(A.H, (segs * kXcdRows + 3) / 4, m);
+    if (g < 0) return;
+    const int unit = m * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (row, segment) in the group
     const int lane = threadIdx.x & 63;
-    const int y = seg / segs;
-    if (y >= A.H) return;
-    const int x0 = (seg - y * segs) * kFillPx;
-    float depth[kFillPerLane], win_z[kFillPerLane];
-    int shadow[kFillPerLane], win[kFillPerLane];
-#pragma unroll
-    for (int p = 0; p < kFillPerLane; ++p) {
-        depth[p] = 0.0f;                                  // :247
-        win_z[p] = 0.0f;                                  // zinv of the last shading fragment
-        shadow[p] = 0;                                    // :259
-        win[p] = -1;                                      // record of the last shading fragment
-    }
+    const int y = g * kXcdRows + unit / segs;
+    if (unit >= segs * kXcdRows || y >= A.H) return;
+    const int x0 = (unit % segs) * kFillPx;
+    const int x = x0 + lane;
+    float depth = 0.0f;                                   // :247
+    int shadow = 0, win = -1;                             // :259; record of the last shading fragment
     const int cnt = count[y];
     const RowRec *rr = recs + (size_t)y * A.n;
     // 64 records per round trip: lane q loads record base+q (coalesced), a
     // ballot keeps those with a fragment in this segment, and the set bits are
     // walked in ascending order (= triangle order) with readlane broadcasts.
-    // Shading is deferred: a later shading fragment overwrites every buffer
-    // the earlier one wrote (:580-585, :665), so only the last one per pixel
-    // is evaluated, after the walk -- bit-identical, far less work in the
-    // ordered loop.
     for (int base = 0; base < cnt; base += 64) {
         const int q = base + lane;
         int mlx = 0, mrx = 0, msh = 0, mtex = 0, midx = 0;
@@ -382,65 +391,40 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A0, const RowRe
             const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlz), b));
             const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msz), b));
             const int shd = __builtin_amdgcn_readlane(msh, b);
-            int tex = 0, idx = 0;
-            float lX = 0.f, sX = 0.f, lY = 0.f, sY = 0.f;
-            if (TEX) {
-                tex = __builtin_amdgcn_readlane(mtex, b);
-                if (tex >= 2) {                                        // opacity-tested textures
-                    idx = __builtin_amdgcn_readlane(midx, b);
-                    lX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlX), b));
-                    sX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msX), b));
-                    lY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlY), b));
-                    sY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msY), b));
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < kFillPerLane; ++p) {
-                const int x = x0 + lane + 64 * p;
-                const int i = x - lx;
-                if (!(x < A.W && i >= 0 && x < rx)) continue;          // :504, :573
-                const float zinv = lz + (sz * (float)i);               // :543
-                if (!shd) {
-                    if (zinv >= depth[p]) {                            // :574
-                        if (TEX && tex >= 2 &&
-                            !rast_opaque(A, tex, idx, zinv, lX + (sX * (float)i), lY + (sY * (float)i))) {
-                            depth[p] = 0.0f;                           // p.zinv = 0 (:619, :643), :665
-                        } else {
-                            depth[p] = zinv;                           // :665
-                            win_z[p] = zinv;
-                            win[p] = base + b;
+            const int i = x - lx;
+            if (!(x < A.W && i >= 0 && x < rx)) continue;          // :504, :573
+            const float zinv = lz + (sz * (float)i);               // :543
+            if (!shd) {
+                if (zinv >= depth) {                               // :574
+                    bool opaque = true;
+                    if (TEX) {
+                        const int tex = __builtin_amdgcn_readlane(mtex, b);
+                        if (tex >= 2) {                            // opacity-tested textures
+                            const int idx = __builtin_amdgcn_readlane(midx, b);
+                            const float lX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlX), b));
+                            const float sX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msX), b));
+                            const float lY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlY), b));
+                            const float sY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msY), b));
+                            opaque = rast_opaque(A, tex, idx, zinv, lX + (sX * (float)i), lY + (sY * (float)i));
                         }
                     }
-                } else if (zinv > depth[p]) {                          // :668-669
-                    shadow[p] = 1;
+                    if (opaque) {
+                        depth = zinv;                              // :665
+                        win = base + b;
+                    } else {
+                        depth = 0.0f;                              // p.zinv = 0 (:619, :643), :665
+                    }
                 }
+            } else if (zinv > depth) {                             // :668-669
+                shadow = 1;
             }
         }
     }
-#pragma unroll
-    for (int p = 0; p < kFillPerLane; ++p) {
-        const int x = x0 + lane + 64 * p;
-        if (x < A.W) {
-            int tri = -1;
-            vec3 D = v3(0.f, 0.f, 0.f);
-            uint32_t texel = 0u;
-            if (win[p] >= 0) {
-                const RowRec r = rr[win[p]];
-                const int i = x - r.lx;
-                const float X = r.lX + (r.sX * (float)i);              // :547-548 numerators
-                const float Y = r.lY + (r.sY * (float)i);
-                vec3 N = v3(r.nx, r.ny, r.nz);
-                if (TEX && r.tex != 0 && rast_tex_present(A, r.tex))
-                    N = rast_tex_normal(A, r.tex, r.index, win_z[p], X, Y, x, y, N, texel);
-                D = illum_D(A, win_z[p], X, Y, N);                     // :580-585 (:590-645)
-                tri = r.t | (x == r.first_x ? (1 << 30) : 0);
-            }
-            size_t o = (size_t)y * A.W + x;
-            if (TEX) texel_out[o] = texel;
-            state[o] = make_float4(__int_as_float(tri), D.x, D.y, D.z);
-            if (depth_out) depth_out[o] = depth[p];
-            shadow_out[o] = shadow[p];
-        }
+    if (x < A.W) {
+        const size_t o = (size_t)y * A.W + x;
+        state[o] = (uint32_t)(win + 1) | (shadow ? kStShadow : 0u);
+        if (depth_out) depth_out[o] = depth;
+        if (shadow_out) shadow_out[o] = shadow;
     }
 }
 
@@ -500,30 +484,70 @@ __device__ __forceinline__ float darken_at(const int *sh, int ld, int cy, int cx
     return 0.3f;
 }
 
-// Post-pass (:283-307) on a 64x8 tile: the shadow plane (halo 2) goes to LDS,
+// Post-pass (:283-307) on a 64x8 tile: the shadow marks (halo 2) go to LDS,
 // then every pixel of the tile and its 1-pixel halo gets its three shade
 // buffers and its darkening computed once, then each interior pixel runs
 // antiAliasing (:1736-1753) on its 5 taps from LDS.  Raster order: the pixel
 // itself and its up/left neighbours are seen darkened, down/right not (a
-// darkening of 0 subtracts exactly nothing).
+// darkening of 0 subtracts exactly nothing).  DIRECT (colour modes 1-2): the
+// state is the colour fill's float4 (cg_rast_colour.hip) instead of the fill's
+// record word, and the shadow marks come from the shadow plane.
 constexpr int kPostTW = 64, kPostTH = 8;
 constexpr int kPostHW = kPostTW + 2, kPostHH = kPostTH + 2;      // shade halo 1
 constexpr int kPostSW = kPostTW + 4, kPostSH = kPostTH + 4;      // shadow halo 2
 
+// A shading fragment rebuilt from its row record (DrawPolygonRows' Interpolate,
+// :543-548) and shaded (PixelShader :559-645 + calculateIllumination :674-683).
 template <bool TEX>
-__global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
-                                                       const float4 *__restrict__ state,
-                                                       const int32_t *__restrict__ sh,
-                                                       uint32_t *__restrict__ argb,
-                                                       const uint32_t *__restrict__ texels)
+__device__ __forceinline__ void shade_from_record(const cg_rtri *__restrict__ tris, const RastArgs &A,
+                                                  const RowRec *__restrict__ rr, uint32_t st, int x, int y, vec3 &sc,
+                                                  vec3 &lo, vec3 &hi)
 {
+    const int rec = (int)(st & ~kStShadow) - 1;
+    if (rec < 0) {
+        sc = lo = hi = v3(0.f, 0.f, 0.f);
+        return;
+    }
+    const RowRec r = rr[rec];
+    const float fi = (float)(x - r.lx);
+    const float z = r.lz + (r.sz * fi);                                    // :543, as the fill evaluated it
+    const float X = r.lX + (r.sX * fi), Y = r.lY + (r.sY * fi);            // :547-548 numerators
+    vec3 N = v3(r.nx, r.ny, r.nz);
+    int tex = 0;
+    uint32_t texel = 0u;
+    if (TEX && r.tex != 0 && rast_tex_present(A, r.tex)) {
+        tex = r.tex;
+        N = rast_tex_normal(A, tex, r.index, z, X, Y, x, y, N, texel);
+    }
+    const vec3 D = illum_D(A, z, X, Y, N);                                 // :580-585 (:590-645)
+    const float4 s4 = make_float4(__int_as_float(r.t | (x == r.first_x ? (1 << 30) : 0)), D.x, D.y, D.z);
+    shade3c(A, s4, tris[r.t].color, sc, lo, hi, tex, texel);
+}
+
+template <bool DIRECT, bool TEX>
+__global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A0,
+                                                       const void *__restrict__ state_v,
+                                                       const RowRec *__restrict__ recs,
+                                                       const int32_t *__restrict__ sh,
+                                                       uint32_t *__restrict__ argb)
+{
+    RastArgs A = A0;
+    if (!DIRECT && A.d_light) {                           // light from the device geometry (:223)
+        const cg_vec4 L = *A.d_light;
+        A.light[0] = L.x; A.light[1] = L.y; A.light[2] = L.z;
+    }
     __shared__ int s_sh[kPostSH][kPostSW];
     __shared__ float s_c[9][kPostHH][kPostHW];      // sc.xyz, lo.xyz, hi.xyz
     __shared__ float s_d[kPostHH][kPostHW];
     const int W = A.W, H = A.H;
-    const int gx0 = blockIdx.x * kPostTW, gy0 = blockIdx.y * kPostTH;
-    // all global loads first (shadow tile, shade state, then the colour
-    // gathers they index), so each thread has them in flight together
+    static_assert(kPostTH == kXcdRows, "a post tile row is one XCD row group");
+    int m;
+    const int g = xcd_group(H, (W + kPostTW - 1) / kPostTW, m);
+    if (g < 0) return;
+    const int gx0 = m * kPostTW, gy0 = g * kPostTH;
+    const uint32_t *st4 = static_cast<const uint32_t *>(state_v);
+    const float4 *st16 = static_cast<const float4 *>(state_v);
+    // all global loads first (shadow marks, shade state), so each thread has them in flight together
     constexpr int kShR = (kPostSH * kPostSW + 255) / 256, kStR = (kPostHH * kPostHW + 255) / 256;
     int shv[kShR];
 #pragma unroll
@@ -531,37 +555,9 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         const int i = threadIdx.x + 256 * r;
         const int cy = i / kPostSW, cx = i - cy * kPostSW;
         const int gx = gx0 - 2 + cx, gy = gy0 - 2 + cy;
-        shv[r] = (i < kPostSH * kPostSW && gx >= 0 && gy >= 0 && gx < W && gy < H) ? sh[(size_t)gy * W + gx] : 0;
-    }
-    float4 stv[kStR];
-    bool inb[kStR];
-#pragma unroll
-    for (int r = 0; r < kStR; ++r) {
-        const int i = threadIdx.x + 256 * r;
-        const int cy = i / kPostHW, cx = i - cy * kPostHW;
-        const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
-        inb[r] = i < kPostHH * kPostHW && gx >= 0 && gy >= 0 && gx < W && gy < H;
-        stv[r] = inb[r] ? state[(size_t)gy * W + gx] : make_float4(__int_as_float(-1), 0.f, 0.f, 0.f);
-    }
-    cg_vec3 col[kStR];
-    int texm[kStR];
-    uint32_t txl[kStR];
-#pragma unroll
-    for (int r = 0; r < kStR; ++r) {
-        const int tb = __float_as_int(stv[r].x);
-        const bool tri = tb >= 0 && !(tb & kStateDirect);
-        col[r] = tri ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f};
-        texm[r] = 0;
-        txl[r] = 0u;
-        if (TEX && tri) {
-            texm[r] = tris[tb & ~(1 << 30)].texture;
-            if (!rast_tex_present(A, texm[r])) texm[r] = 0;           // as the fill shaded it
-            if (texm[r] != 0) {
-                const int i = threadIdx.x + 256 * r;
-                const int cy = i / kPostHW, cx = i - cy * kPostHW;
-                txl[r] = texels[(size_t)(gy0 - 1 + cy) * W + (gx0 - 1 + cx)];
-            }
-        }
+        const bool in = i < kPostSH * kPostSW && gx >= 0 && gy >= 0 && gx < W && gy < H;
+        if (DIRECT) shv[r] = in ? sh[(size_t)gy * W + gx] : 0;
+        else shv[r] = in ? (int)(st4[(size_t)gy * W + gx] >> 31) : 0;
     }
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
@@ -577,8 +573,16 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
         vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
         float d = 0.0f;
-        if (inb[r]) {
-            shade3c(A, stv[r], col[r], sc, lo, hi, texm[r], txl[r]);
+        if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
+            const size_t o = (size_t)gy * W + gx;
+            if (DIRECT) {
+                const float4 s4 = st16[o];
+                const int tb = __float_as_int(s4.x);
+                const bool tri = tb >= 0 && !(tb & kStateDirect);
+                shade3c(A, s4, tri ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f}, sc, lo, hi);
+            } else {
+                shade_from_record<TEX>(tris, A, recs + (size_t)gy * A.n, st4[o], gx, gy, sc, lo, hi);
+            }
             if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
         }
         s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
@@ -700,8 +704,7 @@ int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri
     ctx_events(c, &e0, &e1);
     if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
     if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, tris + 2 * (size_t)cap,
-                                  tris + 3 * (size_t)cap, cap, geo, (cg_vec4 *)(geo + 4), st)) !=
-        hipSuccess)
+                                  tris + 3 * (size_t)cap, cap, geo, (cg_vec4 *)(geo + 4), st)) != hipSuccess)
         return ctx_fail(c, e, "rast_geometry launch");
     if (n_out) *n_out = geo;
     return rast_pipeline(c, tris, cap, geo, p, cg_vec4{0, 0, 0, 1}, (const cg_vec4 *)(geo + 4), d_argb, d_depth,
@@ -721,15 +724,16 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     if (!spans) return ctx_fail(c, e, "alloc spans");
     RastHdr *hdr = (RastHdr *)ctx_buf(c, 1, (size_t)nn * sizeof(RastHdr), &e);
     if (!hdr) return ctx_fail(c, e, "alloc hdr");
-    float4 *state = (float4 *)ctx_buf(c, 3, npx * sizeof(float4), &e);
+    // fill -> post state: 4 B/pixel in colour mode 0, the colour fill's 16 B in modes 1-2
+    void *state = ctx_buf(c, 3, npx * (p->colour_mode == 0 ? sizeof(uint32_t) : sizeof(float4)), &e);
     if (!state) return ctx_fail(c, e, "alloc state");
     int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16) * sizeof(int), &e);   // count[H] | first_tri
     if (!misc) return ctx_fail(c, e, "alloc counts");
     int *count = misc, *first_tri = misc + H;
     RowRec *recs = (RowRec *)ctx_buf(c, 8, (size_t)H * nn * sizeof(RowRec), &e);
     if (!recs) return ctx_fail(c, e, "alloc row records");
-    int32_t *shadow = d_shadow;
-    if (!shadow) {
+    int32_t *shadow = d_shadow;   // mode 0 carries the marks in the state; modes 1-2 need the plane
+    if (!shadow && p->colour_mode != 0) {
         shadow = (int32_t *)ctx_buf(c, 6, npx * sizeof(int32_t), &e);
         if (!shadow) return ctx_fail(c, e, "alloc shadow");
     }
@@ -754,11 +758,6 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     A.use_inv = p->yaw != 0.0f;
     A.cam[0] = p->camera.x; A.cam[1] = p->camera.y; A.cam[2] = p->camera.z; A.cam[3] = p->camera.w;
     mat4_inverse_glm(p->R, A.Rinv);
-    uint32_t *texels = nullptr;
-    if (A.textured) {
-        texels = (uint32_t *)ctx_buf(c, 16, npx * sizeof(uint32_t), &e);
-        if (!texels) return ctx_fail(c, e, "alloc texels");
-    }
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
     if (stats && !events_open && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
@@ -770,32 +769,32 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
                            spans, hdr, first_tri);
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
     }
-    hipLaunchKernelGGL(rast_rows_kernel, dim3((H + 3) / 4), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,
+    hipLaunchKernelGGL(rast_rows_kernel, dim3(xcd_grid(H, kXcdRows / 4)), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,
                        first_tri, recs, count);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rows launch");
+    const int post_grid = xcd_grid(H, (W + kPostTW - 1) / kPostTW);
     if (p->colour_mode != 0) {
         long long ns = 0;
-        const int rc = rast_colour_fill(c, A, p, recs, count, hdr, n_dev, nn, state, d_depth, shadow, st, &ns);
+        const int rc = rast_colour_fill(c, A, p, recs, count, hdr, n_dev, nn, (float4 *)state, d_depth, shadow, st, &ns);
         if (rc) return rc;
         if (stats) stats->n_shaded = ns;
+        hipLaunchKernelGGL((rast_post_kernel<true, false>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
+                           (const void *)state, (const RowRec *)recs, shadow, d_argb);
     } else {
-        const int fsegs = (W + kFillPx - 1) / kFillPx;
-        if (A.textured)
-            hipLaunchKernelGGL(rast_fill_kernel<true>, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs, count,
-                               state, d_depth, shadow, texels);
-        else
-            hipLaunchKernelGGL(rast_fill_kernel<false>, dim3((fsegs * H + 3) / 4), dim3(256), 0, st, A, recs,
-                               count, state, d_depth, shadow, (uint32_t *)nullptr);
-        if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_fill launch");
+        const int fgrid = xcd_grid(H, ((W + kFillPx - 1) / kFillPx * kXcdRows + 3) / 4);
+        if (A.textured) {
+            hipLaunchKernelGGL(rast_fill_kernel<true>, dim3(fgrid), dim3(256), 0, st, A, recs, count, (uint32_t *)state,
+                               d_depth, d_shadow);
+            hipLaunchKernelGGL((rast_post_kernel<false, true>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
+                               (const void *)state, (const RowRec *)recs, (const int32_t *)nullptr, d_argb);
+        } else {
+            hipLaunchKernelGGL(rast_fill_kernel<false>, dim3(fgrid), dim3(256), 0, st, A, recs, count, (uint32_t *)state,
+                               d_depth, d_shadow);
+            hipLaunchKernelGGL((rast_post_kernel<false, false>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
+                               (const void *)state, (const RowRec *)recs, (const int32_t *)nullptr, d_argb);
+        }
         if (stats) stats->n_shaded = -1;
     }
-    const bool tex_post = A.textured && p->colour_mode == 0;
-    if (tex_post)
-        hipLaunchKernelGGL(rast_post_kernel<true>, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH),
-                           dim3(256), 0, st, d_tris, A, state, shadow, d_argb, (const uint32_t *)texels);
-    else
-        hipLaunchKernelGGL(rast_post_kernel<false>, dim3((W + kPostTW - 1) / kPostTW, (H + kPostTH - 1) / kPostTH),
-                           dim3(256), 0, st, d_tris, A, state, shadow, d_argb, (const uint32_t *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_post launch");
     if (stats && (e = hipEventRecord(e1, st)) != hipSuccess) return ctx_fail(c, e, "event");
     if (stats) {
