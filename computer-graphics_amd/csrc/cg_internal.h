@@ -15,10 +15,7 @@ constexpr int kRtTileH = 8;
 constexpr int kRtThreads = 256;
 constexpr int kLatTileW = 16, kLatTileH = 15;   // RT lattice kernel tile (cg_rt.hip): 33 x 31 lattice rays
 constexpr int kSup = 4;              // lattice super-tile: kSup x kSup tiles (two-level certificates)
-#ifndef CG_RT_FRAME_BATCH
-#define CG_RT_FRAME_BATCH 32   // 16: ~1 % slower on C2 (more launch tails)
-#endif
-constexpr int kMaxFrameBatch = CG_RT_FRAME_BATCH;   // frames per batched RT launch (cg_rt_render_frames_device)
+constexpr int kMaxFrameBatch = 32;   // frames per batched RT launch (cg_rt_render_frames_device); 16: ~1 % slower on C2
 
 constexpr int kMaxBlocks = 64;       // row blocks of one assembly launch (cg_rt_assemble_device)
 
@@ -89,7 +86,7 @@ struct RtFrame {
     int row0;      // first global row (band shards; 0 for stripes): v = row0 + stripe map of L
     int out_fmt;   // CG_PIX_ARGB8888 (uint32 per pixel) or CG_PIX_RGB24 (3 bytes: B, G, R)
     int wcol0, wcols;   // RGB24 output window: columns wcol0 .. wcol0 + wcols - 1 (wcols 0: all)
-    int cull_primary, cull_shadow;   // certificates on (CG_RT_CULL env: 0 none, 1 primary, 2 both)
+    int cull_primary, cull_shadow;   // certificates on (always, except inside the probes)
     const RtLight *lights;           // n_lights entries, device memory
     // The light set as the shadow certificate sees it: componentwise min/max
     // of the positions, a centre lc and rho >= max_k |L_k - lc| (FP64, rounded up).

@@ -70,18 +70,6 @@ __host__ __device__ __forceinline__ int rt_cert_units(const RtFrame &F, int sup)
 // the tile's exact lattice box), so the lattice kernel starts from its mask.
 // blockIdx.y = frame of a batched launch (camera cams.c[frame]; its RtTri at
 // out + frame * n, its masks at lat_masks + frame * tiles).
-#ifndef CG_RT_OWN_SHADOW
-#define CG_RT_OWN_SHADOW 1
-#endif
-#ifndef CG_RT_TRI_CLIP
-#define CG_RT_TRI_CLIP 1
-#endif
-#ifndef CG_RT_OCCLUSION
-#define CG_RT_OCCLUSION 1
-#endif
-#ifndef CG_RT_SPH_SHADOW_CERT
-#define CG_RT_SPH_SHADOW_CERT 1
-#endif
 // Per tile it stores two masks: [0] the primary certificate (bit 63: a
 // sphere may be hit), [1] the shadow certificate for every hit the tile's
 // rays can produce (primary_hit_box / sphere_hit_box), so the lattice kernel
@@ -167,7 +155,6 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
             thi = INFINITY;
         }
     }
-#if CG_RT_OCCLUSION
     // Occlusion: a triangle A that every ray of the tile certainly hits
     // (primary_covers) hides every triangle B whose t certainly exceeds A's:
     // t_B >= tlo_B > thi_A (1 + 2^-18) gives distance_B > distance_A for every
@@ -177,9 +164,8 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     double occ = (keep && primary_covers(c, pd)) ? thi : INFINITY;
     for (int o = lpt >> 1; o > 0; o >>= 1) occ = fmin(occ, __shfl_xor(occ, o, 64));
     if (keep && tlo > occ * (1.0 + 0x1p-18)) keep = false;
-#endif
     const cg_tri *Tp = (act && sl < n) ? &tris[sl] : nullptr;
-    if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi, CG_RT_TRI_CLIP ? Tp : nullptr))
+    if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi, Tp))
         for (int k = 0; k < 3; ++k) {
             pb.lo[k] = -INFINITY;
             pb.hi[k] = INFINITY;
@@ -209,19 +195,17 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     bool keep_s = true;
     if (cert && act && m != 0ull && sl < n && blo[0] <= bhi[0])
         keep_s = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, blo, bhi));
-#if CG_RT_OWN_SHADOW
     // a tile whose every hit lies on one triangle k: k never shadows its own hits
     if (cert && keep && keep_s && m == (1ull << sl) && F.n_lights == 1) {
         const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};
         if (own_shadow_rejects(tris[sl], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, blo, bhi)) keep_s = false;
     }
-#endif
     unsigned long long sm = (__ballot(keep_s && sl < n) >> (sub * lpt)) & half;
     bool sph_shadow = F.n_sph > 0;   // bit 63 of the shadow mask: a sphere may block a shadow ray
     if (m == 0ull) {
         sm = 0ull;                   // no ray of the tile can hit anything: no shadow rays
         sph_shadow = false;
-    } else if (CG_RT_SPH_SHADOW_CERT && cert && F.n_lights == 1 && blo[0] <= bhi[0]) {
+    } else if (cert && F.n_lights == 1 && blo[0] <= bhi[0]) {
         const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // one light: lc = its position
         bool any = false;
         for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed(sph[q], Lp, blo, bhi);
@@ -320,13 +304,11 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
                 thi = INFINITY;
             }
         }
-#if CG_RT_OCCLUSION
         double occ = (keep && primary_covers(c, pd)) ? thi : INFINITY;
         for (int o = cp >> 1; o > 0; o >>= 1) occ = fmin(occ, __shfl_xor(occ, o, 64));
         if (keep && tlo > occ * (1.0 + 0x1p-18)) keep = false;
-#endif
         if (keep && !primary_hit_box(c, pd, camf, x0, x1, y0, y1, F.focal, pb.lo, pb.hi,
-                                     CG_RT_TRI_CLIP ? &tris[k] : nullptr))
+                                     &tris[k]))
             for (int q = 0; q < 3; ++q) {
                 pb.lo[q] = -INFINITY;
                 pb.hi[q] = INFINITY;
@@ -353,10 +335,8 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
             bhi[q] = hi;
         }
         bool own = false;
-#if CG_RT_OWN_SHADOW
         if (cert && keep && m == (1ull << k) && F.n_lights == 1)
             own = own_shadow_rejects(tris[k], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, blo, bhi);
-#endif
         const unsigned long long ownm = seg_or(own ? (1ull << k) : 0ull, cp);
         if (tl < kT && ci == 0) {
             const bool live = tile_of(tl, t, G);
@@ -368,7 +348,7 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
                 s_box[tl][3 + q] = bhi[q];
             }
             bool sphsh = F.n_sph > 0 && (SS >> 63);
-            if (live && m != 0ull && CG_RT_SPH_SHADOW_CERT && cert && F.n_lights == 1 && blo[0] <= bhi[0] && sphsh) {
+            if (live && m != 0ull && cert && F.n_lights == 1 && blo[0] <= bhi[0] && sphsh) {
                 bool any = false;
                 for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed(sph[q], Lp, blo, bhi);
                 sphsh = any;
@@ -410,14 +390,9 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
 
 // Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
 // one certificate mask per wave (lane k certifies triangle k).
-#ifndef CG_RT_MIN_WAVES
-#define CG_RT_MIN_WAVES 6   // 80 VGPRs + some scratch; measured fastest (5: no scratch, ~1% slower)
-#endif
-#ifndef CG_RT_POSBOX
-#define CG_RT_POSBOX 1
-#endif
+constexpr int kRtMinWaves = 6;   // waves per SIMD: 80 VGPRs + some scratch; measured fastest (5: no scratch, ~1% slower)
 template <bool CULL>
-__global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                               const RtShade *__restrict__ shade,
                                                               const RtSphere *__restrict__ sph,
                                                               uint32_t *__restrict__ out)
@@ -474,7 +449,6 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
     // one mask for every light of the set (the mask walk must stop at n_tris)
     unsigned long long smask = F.n_tris >= 64 ? ~0ull : ((1ull << F.n_tris) - 1ull);
     if (CULL && F.cull_shadow && F.n_lights > 0) {
-#if CG_RT_POSBOX
         LanePosBox pb;
         pb.init();
         if (active)
@@ -487,28 +461,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
                 pb.add(v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z));   // :326/:345
             }
         smask = shadow_mask_box(F, tc, shadow_box_of_positions(F, pb), lane);
-#else
-        LaneShadowBox sb;
-        sb.init();
-        const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
-        if (active)
-            for (int k = 0; k < 9; ++k) {
-                const int bi = s_bi[k][threadIdx.x];
-                if (bi == INT_MIN) continue;
-                const float t = s_t[k][threadIdx.x];
-                const int i = k / 3 - 1, j = k % 3 - 1;
-                vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
-                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
-                shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, bi, pos));
-            }
-        smask = shadow_mask_of(F, tc, sb, lane);
-#endif
     }
-#ifdef CG_ABLATE_SHADE
-    if (active)
-        for (int k = 0; k < 9; ++k) px += (uint32_t)s_bi[k][threadIdx.x] + __float_as_uint(s_t[k][threadIdx.x]);
-    if (0)
-#endif
     if (active) {
         // Pass 2: shading in the reference's order (:143-157)
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
@@ -529,9 +482,6 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));             // :160-166
     }
-#ifdef CG_RT_DIAG_MASKS
-    px = ((uint32_t)__popcll(mask) << 8) | (uint32_t)__popcll(smask);   // diagnostics build only
-#endif
     if (inside) out[(size_t)L * F.W + u] = px;
 }
 
@@ -548,36 +498,9 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_pixel_kernel(R
 // pixel then adds its nine contributions in the reference's order
 // (pc += DirectLight; pc += objColor * indirect, k = 0..8), so the float sums
 // are formed exactly as the reference forms them.
-#ifndef CG_RT_LAT_PAIR
-#define CG_RT_LAT_PAIR 1   // pass 1 traces CG_RT_LAT_PAIR + 1 lattice points per lane per step
-#endif
-// Phase timing of the lattice kernel (diagnostic builds only: -DCG_RT_LAT_STAMPS):
-// per wave, s_memtime deltas accumulated into cg_lat_stamps[phase].
-#ifdef CG_RT_LAT_STAMPS
-constexpr int kStampWaves = 16 * 8640 * 4;   // one 16-frame 1080p batch
-__device__ unsigned int cg_lat_stamps[kStampWaves][6];
-#define LAT_STAMP(ph)                                                                  \
-    do {                                                                               \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                  \
-        stamps_[ph] = (unsigned int)(now_ - stamp_);                                   \
-        stamp_ = now_;                                                                 \
-    } while (0)
-#else
-#define LAT_STAMP(ph) \
-    do {              \
-    } while (0)
-#endif
-#ifdef CG_RT_SHADOW_STATS
-// Diagnostic builds: pass-2 wave steps by shadow class (all lit / all shadowed
-// / mixed) and shadow-loop iterations now vs. with the best single blocker first.
-__device__ unsigned long long cg_shadow_stats[8];
-#endif
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
 
-#ifndef CG_RT_LAT_PAIR2
-#define CG_RT_LAT_PAIR2 0   // 1: pass 2 takes two lattice points per lane per step (measured 12% slower: 69 VGPRs)
-#endif
 // Pass 2 of rt_lattice_kernel for lattice points p and p + 64: DirectLight
 // (skeleton.cpp:366-415, as direct_light<true> with light 0) of each point
 // that hit, written over its LDS slot.  The shadow loop walks the tile's
@@ -641,7 +564,7 @@ __device__ __forceinline__ void direct_light_pair(const RtFrame &F, const RtTri 
 // blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
 // tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
 // out + frame * out_stride.
-__global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph,
                                                                   const unsigned long long *__restrict__ lat_masks,
@@ -671,10 +594,6 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
     // sphere may be hit) and shadow mask for every hit the tile can produce
-#ifdef CG_RT_LAT_STAMPS
-    unsigned long long stamp_ = __builtin_amdgcn_s_memtime();
-    unsigned int stamps_[6] = {0, 0, 0, 0, 0, 0};
-#endif
     // RGB24 window (a caller's contract: the columns outside are black): tiles
     // outside it store nothing; windows are 16-pixel aligned
     const int pitch = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcols : F.W;
@@ -707,25 +626,10 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
         return;                            // the whole workgroup (m0 is uniform)
     }
     __syncthreads();                       // s_shade
-#ifndef CG_RT_OBJCOL_LDS
-#define CG_RT_OBJCOL_LDS 0   // 1: no flat loads, but measured 5 % slower (C2 52.1 vs 49.3 us)
-#endif
-    // objColor of a hit (:143-149): triangles from the LDS copy, the first
-    // sphere from registers (uniform), any other sphere by a guarded load --
-    // explicit address spaces, so no generic (flat) load per sample
-    const vec3 sph0_col = F.n_sph > 0 ? v3(sph[0].cr, sph[0].cg, sph[0].cb) : v3(0.0f, 0.0f, 0.0f);
-    auto obj_col = [&](int bi) -> vec3 {
-        const RtShade sh = s_shade[bi < 0 ? 0 : bi];
-        vec3 c = v3(sh.cr, sh.cg, sh.cb);
-        if (bi == -1) c = sph0_col;
-        if (bi < -1) c = v3(sph[-1 - bi].cr, sph[-1 - bi].cg, sph[-1 - bi].cb);
-        return c;
-    };
     // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
-#if CG_RT_LAT_PAIR
-    // CG_RT_LAT_PAIR + 1 points per lane per step (p, p + 64, ...): one triangle
+    // two points per lane per step (p, p + 64): one triangle
     // load for all of them
-    constexpr int NP = CG_RT_LAT_PAIR + 1;
+    constexpr int NP = 2;
     for (int p0 = p_lo; p0 < p_hi; p0 += 64 * NP) {
         float X[NP], Y[NP];
         bool live[NP];
@@ -767,37 +671,11 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             s_pt[pp[n]] = make_float4(t[n], 0.0f, 0.0f, __int_as_float(bi[n]));
         }
     }
-#else
-    for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
-        const int p = p0 + lane;
-        const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
-        if (p < p_hi && cx < cols) {
-            const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
-            float t;
-            const int bi = closest_primary<true>(Fp, tc, sph, v3(X, Y, F.focal), t, mask);
-            s_pt[idx] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
-        }
-    }
-#endif
-    LAT_STAMP(0);   // pass 1
     // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
     // attributes from the LDS copy
-#if CG_RT_LAT_PAIR2
-    // two points per lane per step (p, p + 64): two independent chains for the
-    // issue slots, one scalar load of each shadow candidate for both
-    for (int p0 = p_lo; p0 < p_hi; p0 += 128)
-        direct_light_pair(Fs, tc, s_shade, sph, s_pt, smask, p0 + lane, p_hi, cols, ax0, ay0);
-#else
-#ifdef CG_ABLATE_SHADE
-    if (smask == 12345ull)
-#endif
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
         const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
-#ifdef CG_RT_SHADOW_STATS
-        bool st_act = false;
-        unsigned long long st_blk = 0ull;   // bit j: the j-th candidate (ctz order, spheres last) blocks
-#endif
         if (p < p_hi && cx < cols) {
             const float4 q = s_pt[idx];
             const int bi = __float_as_int(q.w);
@@ -805,63 +683,12 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
                 const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
                 const float t = q.x;
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-#ifdef CG_RT_SHADOW_STATS
-                {
-                    st_act = true;
-                    const RtLight Lt = Fs.lights[0];
-                    const vec3 r = v3(Lt.x, Lt.y, Lt.z) - pos;
-                    const float rmag = light_rmag(r);
-                    const vec3 o = pos + hit_normal(s_shade, sph, bi, pos) * 0.00001f;
-                    const vec3 nd = -r;
-                    const float len = length(r);
-                    unsigned long long m = smask;
-                    int j = 0;
-                    for (; m; ++j) {
-                        const int k = __builtin_ctzll(m);
-                        m &= m - 1ull;
-                        if (tri_shadow_hit(tc[k], o, nd, len, rmag)) st_blk |= 1ull << j;
-                    }
-                    for (int k = 0; k < Fs.n_sph; ++k, ++j) {
-                        float ts;
-                        if (sphere_intersect(sph[k], o, r, ts) && ts < rmag) st_blk |= 1ull << j;
-                    }
-                }
-#endif
-#if CG_RT_OBJCOL_LDS
-                const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, obj_col(bi), 0, smask);
-#else
                 const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
-#endif
                 s_pt[idx] = make_float4(dl.x, dl.y, dl.z, q.w);
             }
         }
-#ifdef CG_RT_SHADOW_STATS
-        {
-            const int ncand = __builtin_popcountll(smask) + Fs.n_sph;
-            const unsigned long long act = __ballot(st_act), shd = __ballot(st_act && st_blk != 0ull);
-            // iterations now: all candidates if any lane is lit, else the latest first blocker
-            int it = st_act && st_blk ? __builtin_ctzll(st_blk) + 1 : 0;
-            for (int o = 32; o; o >>= 1) it = max(it, __shfl_xor(it, o));
-            unsigned long long common = st_act ? st_blk : ~0ull;
-            for (int o = 32; o; o >>= 1) {
-                const unsigned lo = __shfl_xor((unsigned)common, o), hi = __shfl_xor((unsigned)(common >> 32), o);
-                common &= ((unsigned long long)hi << 32) | lo;
-            }
-            if (lane == 0 && act) {
-                const int cls = shd == 0ull ? 0 : (shd == act ? 1 : 2);
-                const int cur = cls == 1 ? it : ncand;
-                atomicAdd(&cg_shadow_stats[cls], 1ull);
-                atomicAdd(&cg_shadow_stats[3 + cls], (unsigned long long)cur);
-                if (cls == 1) atomicAdd(&cg_shadow_stats[6], (unsigned long long)(common ? 1 : cur));
-                atomicAdd(&cg_shadow_stats[7], (unsigned long long)__popcll(act));
-            }
-        }
-#endif
     }
-#endif
-    LAT_STAMP(3);   // pass 2
     __syncthreads();
-    LAT_STAMP(4);   // pass-2 barrier
     // Pixels: the nine contributions in the reference's order (:134-166)
     const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
     const bool have = tx < nu && ty < nv;
@@ -879,11 +706,7 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             if (bi == INT_MIN) continue;
             valid = true;
             pc = pc + v3(q.x, q.y, q.z);                                                  // :151-153
-#if CG_RT_OBJCOL_LDS
-            pc = pc + (obj_col(bi) * ind);                                                // :156
-#else
             pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
-#endif
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
         if (F.out_fmt == CG_PIX_ARGB8888) out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
@@ -912,15 +735,6 @@ __global__ __launch_bounds__(kRtThreads, CG_RT_MIN_WAVES) void rt_lattice_kernel
             q[2] = (uint8_t)(px >> 16);
         }
     }
-    LAT_STAMP(5);   // pixels + stores
-#ifdef CG_RT_LAT_STAMPS
-    const size_t wid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave;
-    if (lane < 6 && wid < (size_t)kStampWaves) {
-        unsigned int v = 0;
-        for (int k = 0; k < 6; ++k) v = lane == k ? stamps_[k] : v;
-        cg_lat_stamps[wid][lane] = v;
-    }
-#endif
 }
 
 // ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): rows
@@ -1134,11 +948,7 @@ static bool rt_lattice_ok(const RtFrame &F)
 // caller has rt_prepare_kernel certify its tiles first).
 bool rt_use_lattice(const RtFrame &F)
 {
-    static const bool lattice_on = [] {
-        const char *e = getenv("CG_RT_LATTICE");
-        return !e || atoi(e) != 0;
-    }();
-    return lattice_on && F.n_tris > 0 && F.n_tris <= 62 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
+    return F.n_tris > 0 && F.n_tris <= 62 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
 }
 
 size_t rt_lattice_tiles(const RtFrame &F)
@@ -1175,39 +985,6 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         hipLaunchKernelGGL(rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     return hipGetLastError();
-}
-
-// Diagnostic builds: read and clear the pass-2 shadow statistics.
-bool rt_shadow_stats(unsigned long long out[8], hipStream_t st)
-{
-#ifdef CG_RT_SHADOW_STATS
-    if (hipStreamSynchronize(st) != hipSuccess) return false;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cg_shadow_stats), 64) != hipSuccess) return false;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(cg_shadow_stats), z, 64) == hipSuccess;
-#else
-    (void)out;
-    (void)st;
-    return false;
-#endif
-}
-
-// Diagnostic builds: read and clear the lattice phase stamps (cycles summed over waves).
-bool rt_lat_stamps(unsigned long long out[8], hipStream_t st)
-{
-#ifdef CG_RT_LAT_STAMPS
-    if (hipStreamSynchronize(st) != hipSuccess) return false;
-    std::vector<unsigned int> v((size_t)kStampWaves * 6);
-    if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(cg_lat_stamps), v.size() * 4) != hipSuccess) return false;
-    for (int k = 0; k < 8; ++k) out[k] = 0;
-    for (size_t w = 0; w < (size_t)kStampWaves; ++w)
-        for (int k = 0; k < 6; ++k) out[k] += v[w * 6 + k];
-    return true;
-#else
-    (void)out;
-    (void)st;
-    return false;
-#endif
 }
 
 hipError_t launch_rt_pack_rgb24(const uint32_t *d_src, int W, int rows, int wcol0, int wcols, uint8_t *d_dst,

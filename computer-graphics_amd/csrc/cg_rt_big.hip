@@ -78,7 +78,6 @@ struct BigBufs {
     int cap, bins_x, bins_y, tiles_x, tiles_y;
     int *sup_list, *sup_n;        // [n_sups][cap], [n_sups]: triangles the super-bin's certificate keeps
     int sups_x, sups_y;
-    unsigned long long *diag;     // CG_RT_BIG_DIAG: [waves, survivors, walk steps, lit rays, primary cands, primary kept]
 };
 
 // ---------------------------------------------------------------------------
@@ -360,14 +359,7 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
                 if ((double)k > kd) k = nextafterf(k, 0.0f);
                 kbits[r] = __float_as_uint(k);
             }
-            if (kept[r]) {
-                pbox[r] = pbox2[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
-                if (B.diag) {
-                    atomicAdd(&B.diag[6], pbox[r] == kProjAll ? 1ull : 0ull);
-                    const float w = (float)(short)((pbox[r] >> 16) & 0xffff) - (float)(short)(pbox[r] & 0xffff);
-                    if (pbox[r] != kProjAll) atomicAdd(&B.diag[1], (unsigned long long)w);
-                }
-            }
+            if (kept[r]) pbox[r] = pbox2[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
         }
     }
     __syncthreads();
@@ -599,11 +591,6 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
         const int cand = lane < cnt ? q_w[lane] : -1;
         const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
         unsigned long long mask = __ballot(keep);
-        if (B.diag && lane == 0) {
-            atomicAdd(&B.diag[4], (unsigned long long)cnt);
-            atomicAdd(&B.diag[5], (unsigned long long)__popcll(mask));
-            atomicAdd(&B.diag[2], tb < FLT_MAX ? 1ull : 0ull);            // batches certified with a finite bound
-        }
         while (mask) {
             const int b = __builtin_ctzll(mask);
             mask &= mask - 1ull;
@@ -776,22 +763,13 @@ __device__ __forceinline__ vec3 big_direct_light(const RtFrame &F, const RtSpher
 
 // any-hit of one shadow ray over a uniform list of triangle indices: the
 // blocking triangle, or -1.
-__device__ __forceinline__ int any_hit(const RtTri *__restrict__ tc, const int *list, int n, const ShadowRay &q,
-                                       unsigned long long *diag = nullptr)
+__device__ __forceinline__ int any_hit(const RtTri *__restrict__ tc, const int *list, int n, const ShadowRay &q)
 {
-    int i = 0, hit = -1;
-    for (; i < n; ++i) {
+    for (int i = 0; i < n; ++i) {
         const int k = __builtin_amdgcn_readfirstlane(list[i]);
-        if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) {
-            hit = k;
-            break;
-        }
+        if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) return k;
     }
-    if (diag) {
-        atomicAdd(&diag[2], (unsigned long long)(i + 1));
-        atomicAdd(&diag[6], 1ull);
-    }
-    return hit;
+    return -1;
 }
 
 // Blocker search along the shadow segment S + t (L - P), t in [0, 1], through
@@ -879,7 +857,6 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
     return mat4_mul(F.R, v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f));   // :126-128
 }
 
-template <bool kNbr>
 __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
@@ -908,9 +885,11 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
                 int k = -1;
                 if (bi >= 0 && tri_shadows(tc[bi], q.origin, q.nd, q.len, q.rmag)) k = bi;
                 else if (last >= 0 && tri_shadows(tc[last], q.origin, q.nd, q.len, q.rmag)) k = last;
-                if (kNbr) {
-                    // unresolved rays try up to sixteen distinct blockers the wave's
-                    // other rays found (neighbouring pixels, same light)
+                {
+                    // unresolved rays try up to sixteen distinct blockers other rays of
+                    // the wave found.  They are only hints: each is re-tested with the
+                    // exact tri_shadows, so the verdict does not depend on which lanes
+                    // (pixels, sub-rays) contributed them
                     unsigned long long have = __ballot(k >= 0);
                     for (int rep = 0; rep < 16 && have != 0ull && __ballot(k < 0) != 0ull; ++rep) {
                         const int kn = __shfl(k, __builtin_ctzll(have));
@@ -935,11 +914,6 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
         }
         B.sh_bits[pix] = shadowed;
         B.pend_bits[pix] = pending;
-    }
-    if (B.diag) {
-        atomicAdd(&B.diag[3], (unsigned long long)__popcll(pending));
-        atomicAdd(&B.diag[7], (unsigned long long)gtests);
-        if (lane == 0) atomicAdd(&B.diag[0], 1ull);
     }
 }
 
@@ -1109,12 +1083,6 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     BigBufs B = big_layout(F, F.n_tris);
     big_carve(B, F, scratch);
     B.grid = grid;
-    static const bool diag = getenv("CG_RT_BIG_DIAG") != nullptr;
-    if (diag) {
-        B.diag = (unsigned long long *)((char *)scratch + big_scratch_bytes(B, F) - 64);
-        hipError_t e = hipMemsetAsync(B.diag, 0, 64, st);
-        if (e != hipSuccess) return e;
-    }
     const int bins = B.bins_x * B.bins_y;
     hipError_t e = hipMemsetAsync(B.bin_n, 0, big_counter_bytes(B), st);
     if (e != hipSuccess) return e;
@@ -1133,46 +1101,11 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
     } else if (F.n_lights > 0) {
-        static const bool nbr = !getenv("CG_RT_HINT_NBR") || atoi(getenv("CG_RT_HINT_NBR")) != 0;
-        if (nbr)
-            hipLaunchKernelGGL(rt_shadow_hints_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-        else
-            hipLaunchKernelGGL(rt_shadow_hints_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                               B);
+        hipLaunchKernelGGL(rt_shadow_hints_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         hipLaunchKernelGGL(rt_pending_test_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
     }
     hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     return hipGetLastError();
-}
-
-// Diagnostics (CG_RT_BIG_DIAG=1): bin list sizes of the last frame.
-void rt_big_diag(const RtFrame &F, void *scratch, hipStream_t st)
-{
-    BigBufs B = big_layout(F, F.n_tris);
-    big_carve(B, F, scratch);
-    const int bins = B.bins_x * B.bins_y;
-    std::vector<int> n(2 * (size_t)bins);
-    if (hipMemcpyAsync(n.data(), B.bin_n, n.size() * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return;
-    long long s0 = 0, s1 = 0;
-    int m0 = 0, m1 = 0;
-    for (int b = 0; b < bins; ++b) {
-        s0 += n[b]; s1 += n[bins + b];
-        m0 = std::max(m0, n[b]); m1 = std::max(m1, n[bins + b]);
-    }
-    fprintf(stderr, "[cg_rt_big] bins %d: primary lists mean %lld max %d; shadow lists mean %lld max %d\n", bins,
-            s0 / bins, m0, s1 / bins, m1);
-    int np = 0;
-    if (hipMemcpy(&np, B.pend_n, 4, hipMemcpyDeviceToHost) == hipSuccess)
-        fprintf(stderr, "[cg_rt_big] pending shadow rays %d (searched exhaustively: %d)\n", np, std::min(np, kMaxPend));
-    unsigned long long d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpy(d, (char *)scratch + big_scratch_bytes(B, F) - 64, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess)
-        fprintf(stderr, "[cg_rt_big] waves %llu: grid tests %llu; unresolved after hints+grid %llu rays; "
-                "pending waves %llu with %llu certified candidates in total; primary candidates examined %llu, "
-                "tested %llu, chunks with a finite bound %llu (primary-only runs: bin entries without a projected "
-                "box = the pending-wave count, box widths summed = the candidate count)\n",
-                d[0], d[7], d[3], d[6], d[1], d[4], d[5], d[2]);
 }
 
 // Host build of the scene grid: cubic cells sized for ~2 triangle centroids

@@ -2,14 +2,6 @@
 // (cg_rt.hip, <= 64 triangles, one certificate mask per wave) and the
 // large-scene binned kernels (cg_rt_big.hip).  Every float op follows
 // raytracer/Source/skeleton.cpp + GLM 0.9.7.2 association (see cg_math.h).
-//
-// Cost-attribution switches (scripts/build_variant.sh only; the images they
-// render are wrong by design and no shipped build defines them):
-//   CG_ABLATE_SPHERE  skip the sphere in primary and shadow tests
-//   CG_ABLATE_SHADOW  skip shadow rays
-//   CG_ABLATE_SHADOW_TESTS  skip the shadow tests but keep their certificate
-//   CG_ABLATE_SHADE   (cg_rt.hip) skip pass 2: closest hits only
-//   CG_RT_DIAG_MASKS  (cg_rt.hip) write certificate-mask popcounts as pixels
 #pragma once
 
 #include <float.h>
@@ -621,12 +613,6 @@ __device__ __forceinline__ bool surely_beyond(float detT, float det, float len, 
 // |detT|, |detU|, |detV| <= 2^40, 2^-20 <= len <= 2^20 -- the quotients and
 // distances then stay in the normal range (no underflow, no overflow);
 // anything else (NaN, det = 0, extreme scales) is undecided.
-#ifndef CG_RT_PREFETCH
-#define CG_RT_PREFETCH 0
-#endif
-#ifndef CG_RT_DIVFREE
-#define CG_RT_DIVFREE 0   // 1: bit-exact too, but measured slower (C2 85.6 -> 98 us/frame, C4 20 -> 25 ms)
-#endif
 __device__ __forceinline__ bool fsign(float x) { return (__float_as_uint(x) >> 31) != 0u; }
 
 // distance = fl(fl(detT/det) * len) against the reference's tests
@@ -689,22 +675,11 @@ __device__ __forceinline__ bool tri_accept(float detT, float det, float len, flo
 {
     const float bound = FLT_MAX;
     float detU, detV;
-#if CG_RT_DIVFREE
-    const int td = t_decide(detT, det, len, best);
-    if (td == 0) return false;
-    uvf(detU, detV);
-    const int ud = td == 1 ? uv_decide(det, detU, detV) : -1;
-    if (ud == 0) return false;
-#endif
     const float t = detT / det;                               // :306
     const float distance = t * len;                           // :307
     if (distance < 0.0f) return false;                        // :311
     if (distance >= best || distance > bound) return false;   // :313
-#if CG_RT_DIVFREE
-    if (ud < 0)
-#else
     uvf(detU, detV);
-#endif
     {
         const float u = detU / det, v = detV / det;           // :317-321
         if (!((u >= 0) && (v >= 0) && ((u + v) <= 1))) return false;   // :328-335
@@ -752,9 +727,6 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
         }
     }
     const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
-#ifdef CG_ABLATE_SPHERE
-    if (0)
-#endif
     for (int k = 0; k < F.n_sph; ++k) {                       // :341-355
         float t;
         const RtSphere S = sph[k];
@@ -791,26 +763,10 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
         bt[n] = 0.f;
         bi[n] = INT_MIN;
     }
-#if CG_RT_PREFETCH
-    // software pipelining: the next triangle's constants are loaded while
-    // this one is tested
-    int kn = mask ? __builtin_ctzll(mask) : 0;
-    RtTri cn = tc[kn];
-#endif
     while (mask != 0ull) {
-#if CG_RT_PREFETCH
-        const int k = kn;
-        const RtTri c = cn;
-        mask &= mask - 1ull;
-        if (mask) {
-            kn = __builtin_ctzll(mask);
-            cn = tc[kn];
-        }
-#else
         const int k = __builtin_ctzll(mask);
         mask &= mask - 1ull;
         const RtTri c = tc[k];
-#endif
 #pragma unroll
         for (int n = 0; n < N; ++n) {
             if (!live[n]) continue;
@@ -832,9 +788,6 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
         }
     }
     const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
-#ifdef CG_ABLATE_SPHERE
-    if (0)
-#endif
     for (int q = 0; q < F.n_sph; ++q) {                           // :341-355
         const RtSphere S = sph[q];
         const vec3 L = s3 - v3(S.cx, S.cy, S.cz);                 // camera-constant (:48, :51)
@@ -918,9 +871,6 @@ __device__ __forceinline__ void closest_primary_group(const RtFrame &F, const Rt
         }
     }
     const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
-#ifdef CG_ABLATE_SPHERE
-    if (0)
-#endif
     for (int q = 0; q < F.n_sph; ++q) {                        // :341-355
         const RtSphere S = sph[q];
         const vec3 L = s3 - v3(S.cx, S.cy, S.cz);              // camera-constant (:48, :51)
@@ -948,9 +898,6 @@ __device__ __forceinline__ void closest_primary_group(const RtFrame &F, const Rt
 // running minimum, only on `distance < rmag` here).
 // One triangle of the shadow test (skeleton.cpp:289-335 from a generic
 // start): an accepted hit with distance < rmag (:394-395).
-#ifndef CG_RT_UV_FIRST
-#define CG_RT_UV_FIRST 0   // 1: measured 6 % slower on C2 (52.2 vs 49.3 us); the large-scene test uses it
-#endif
 __device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 nd, float len, float rmag)
 {
     float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
@@ -960,33 +907,6 @@ __device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 
     float K2 = sy * c.e2z - c.e2y * sz;
     float K4 = sy * c.e1z - c.e1y * sz;
     float detT = (sx * c.K1 - c.e1x * K2) + c.e2x * K4;                    // det(s, e1, e2)
-#if CG_RT_DIVFREE
-    // the shadow verdict needs only the comparisons: divide-free when certain
-    {
-        const int td = t_decide(detT, det, len, rmag);
-        if (td == 0) return false;
-        if (td == 1) {
-            float Q3 = nd.y * sz - sy * nd.z;
-            float K3 = c.e1y * sz - sy * c.e1z;
-            const int ud = uv_decide(det, (nd.x * K2 - sx * Q2) + c.e2x * Q3, (nd.x * K3 - c.e1x * Q3) + sx * Q1);
-            if (ud >= 0) return ud == 1;
-        }
-    }
-#endif
-#if CG_RT_UV_FIRST
-    // a certain u / v rejection first (no divide; the verdict is a conjunction,
-    // so the order of its tests does not matter): a wave whose rays all miss
-    // the candidate skips the three IEEE divides
-    float Q3 = nd.y * sz - sy * nd.z;
-    float K3 = c.e1y * sz - sy * c.e1z;
-    float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
-    float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
-    if (uv_decide(det, detU, detV) == 0) return false;
-    float t = detT / det;
-    float distance = t * len;
-    if (distance < 0.0f) return false;
-    if (distance >= rmag || distance > FLT_MAX) return false;
-#else
     float t = detT / det;
     float distance = t * len;
     if (distance < 0.0f) return false;
@@ -995,7 +915,6 @@ __device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 
     float K3 = c.e1y * sz - sy * c.e1z;
     float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
     float detV = (nd.x * K3 - c.e1x * Q3) + sx * Q1;
-#endif
     float u = detU / det;
     float v = detV / det;
     return (u >= 0) && (v >= 0) && ((u + v) <= 1);
@@ -1006,9 +925,6 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
                                          const RtSphere *__restrict__ sph, vec3 start, vec3 d,
                                          float rmag, unsigned long long mask)
 {
-#ifdef CG_ABLATE_SHADOW_TESTS
-    return mask == (unsigned long long)F.W * 0x9E3779B97F4A7C15ull;   // opaque: keeps the certificate live
-#endif
     vec3 nd = -d;
     float len = length(d);
     for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
@@ -1019,9 +935,6 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
         }
         if (tri_shadow_hit(tc[k], start, nd, len, rmag)) return true;
     }
-#ifdef CG_ABLATE_SPHERE
-    if (0)
-#endif
     for (int k = 0; k < F.n_sph; ++k) {
         float t;
         if (sphere_intersect(sph[k], start, d, t) && t < rmag) return true;
@@ -1064,9 +977,7 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
     float rmag = light_rmag(r);                                          // :371
     vec3 normal = hit_normal(shade, sph, bi, pos);
     vec3 origin = pos + normal * 0.00001f;                              // :394
-#ifndef CG_ABLATE_SHADOW
     if (shadowed<CULL>(F, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);  // :394-398
-#endif
     return direct_light_lit(Lt, r, rmag, normal, objColor);
 }
 

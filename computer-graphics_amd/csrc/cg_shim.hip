@@ -24,14 +24,11 @@ hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShad
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             const unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
-bool rt_lat_stamps(unsigned long long out[8], hipStream_t st);
-bool rt_shadow_stats(unsigned long long out[8], hipStream_t st);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t, const cg_tri *);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &);
-void rt_big_diag(const RtFrame &, void *, hipStream_t);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
 hipError_t launch_rt_pack_rgb24(const uint32_t *, int, int, int, int, uint8_t *, hipStream_t);
 hipError_t launch_rt_assemble(const uint8_t *, const RtBlocks &, int, uint32_t *, size_t, hipStream_t);
@@ -389,12 +386,8 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
         F.wcol0 = s->col0;
         F.wcols = s->cols;
     }
-    static int cull = [] {
-        const char *e = getenv("CG_RT_CULL");
-        return e ? atoi(e) : 2;
-    }();
-    F.cull_primary = cull >= 1;
-    F.cull_shadow = cull >= 2;
+    F.cull_primary = 1;   // exact certificates (cg_rt_dev.h); the probes run without them
+    F.cull_shadow = 1;
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     return set_lights(c, lights, n_lights, st, F);
 }
@@ -412,17 +405,6 @@ extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
 }
 
 static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st);
-
-// Two-level tile certificates (super-tiles, then tiles); CG_RT_TWO_LEVEL=0
-// selects the single-level path (A/B only: both are exact).
-static bool rt_two_level()
-{
-    static const bool on = [] {
-        const char *e = getenv("CG_RT_TWO_LEVEL");
-        return !e || atoi(e) != 0;
-    }();
-    return on;
-}
 
 static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t st)
 {
@@ -453,7 +435,7 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
     RtFrameCams cams{};
     for (int k = 0; k < 4; ++k) cams.c[0][k] = F.cam[k];
     unsigned long long *supm = nullptr;
-    if (lat && rt_two_level()) {
+    if (lat) {   // two-level tile certificates: super-tiles, then tiles
         CG_TRY(c, c->supmask.ensure(rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
         supm = (unsigned long long *)c->supmask.p;
     }
@@ -464,8 +446,6 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
         CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
                                 c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p), "rt_big launch");
-        static const bool diag = getenv("CG_RT_BIG_DIAG") != nullptr;
-        if (diag) rt_big_diag(F, c->big.p, st);
         return CG_OK;
     }
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
@@ -491,11 +471,7 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
                                     void *d_out, size_t stride, hipStream_t st)
 {
-    static const bool pipe = [] {
-        const char *e = getenv("CG_RT_PIPE");
-        return !e || atoi(e) != 0;
-    }();
-    if (pipe && !c->aux) {
+    if (!c->aux) {
         CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
         for (int k = 0; k < 2; ++k) {
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_cert[k], hipEventDisableTiming), "aux event");
@@ -503,12 +479,11 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
             CG_TRY(c, hipEventRecord(c->ev_lat[k], c->aux), "aux event");
         }
     }
-    // pipelined: this call's slot (its buffers were last read by the lattice
-    // launch two calls ago, ev_lat[k]); otherwise the context's own buffers
+    // this call's slot (its buffers were last read by the lattice launch two
+    // calls ago, ev_lat[k])
     const int k = c->slot;
-    if (pipe) c->slot ^= 1;
-    DevBuf &btc = pipe ? c->ptc[k] : c->tc, &bsh = pipe ? c->pshade[k] : c->shade;
-    DevBuf &blat = pipe ? c->plat[k] : c->latmask, &bsup = pipe ? c->psup[k] : c->supmask;
+    c->slot ^= 1;
+    DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k];
     const size_t tiles = rt_lattice_tiles(F);
     CG_TRY(c, blat.ensure((size_t)nf * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
     CG_TRY(c, btc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
@@ -519,83 +494,20 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
         fc.c[f][2] = cams[f].camera.z; fc.c[f][3] = cams[f].camera.w;
     }
     unsigned long long *lat = (unsigned long long *)blat.p;
-    unsigned long long *supm = nullptr;
-    if (rt_two_level()) {
-        CG_TRY(c, bsup.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)),
-               "alloc super-tile masks");
-        supm = (unsigned long long *)bsup.p;
-    }
-    hipStream_t cst = st;
-    if (pipe) {   // certificates on aux, after the slot's previous reader
-        cst = c->aux;
-        CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
-    }
+    CG_TRY(c, bsup.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
+    unsigned long long *supm = (unsigned long long *)bsup.p;
+    // certificates on aux, after the slot's previous reader
+    hipStream_t cst = c->aux;
+    CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)btc.p,
                                 (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm),
            "rt_prepare launch");
-    if (pipe) {
-        CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
-        CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
-    }
+    CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
+    CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
                                        (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st),
            "rt_lattice launch");
-    if (pipe) CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
-    static const bool diag = getenv("CG_RT_LAT_DIAG") != nullptr;
-    if (diag) {   // certificate statistics of frame 0's tiles (diagnostics only: synchronises)
-        std::vector<unsigned long long> m(2 * tiles);
-        if (hipMemcpyAsync(m.data(), lat, tiles * 16, hipMemcpyDeviceToHost, st) == hipSuccess &&
-            hipStreamSynchronize(st) == hipSuccess) {
-            for (int which = 0; which < 2; ++which) {
-                long long sum = 0, sph = 0;
-                int mx = 0, hist[65] = {0};
-                for (size_t t = 0; t < tiles; ++t) {
-                    const unsigned long long x = m[2 * t + which] & (which ? ~0ull : ~(1ull << 63));
-                    sph += which ? 0 : (long long)(m[2 * t] >> 63);
-                    const int p = __builtin_popcountll(x);
-                    sum += p;
-                    mx = std::max(mx, p);
-                    ++hist[p];
-                }
-                fprintf(stderr, "[cg_rt_lattice] tiles %zu: %s triangles per tile mean %.2f max %d%s; histogram",
-                        tiles, which ? "shadow-certified" : "primary-certified", (double)sum / tiles, mx,
-                        which ? "" : (std::string(", sphere in ") + std::to_string(sph)).c_str());
-                for (int p = 0; p <= mx; ++p) fprintf(stderr, " %d", hist[p]);
-                fprintf(stderr, "\n");
-            }
-            {
-                int shown = 0;
-                const int tx = (F.W + kLatTileW - 1) / kLatTileW;
-                for (size_t t = 0; t < tiles && shown < 12; ++t)
-                    if (__builtin_popcountll(m[2 * t + 1]) >= (getenv("CG_RT_LAT_DIAG_MIN") ? atoi(getenv("CG_RT_LAT_DIAG_MIN")) : 11) && (t % 37 == 0)) {
-                        fprintf(stderr, "[cg_rt_lattice] tile (%d,%d) primary %016llx shadow %016llx\n", (int)(t % tx),
-                                (int)(t / tx), m[2 * t], m[2 * t + 1]);
-                        ++shown;
-                    }
-            }
-            if (getenv("CG_RT_LAT_DIAG_MAP")) {   // per-tile popcounts (primary/shadow), 0-9 then a-z
-                const int tx = (F.W + kLatTileW - 1) / kLatTileW;
-                for (int which = 0; which < 2; ++which)
-                    for (size_t t = 0; t < tiles; ++t) {
-                        const int p = __builtin_popcountll(m[2 * t + which]);
-                        fputc(p < 10 ? '0' + p : 'a' + std::min(25, p - 10), stderr);
-                        if ((int)(t % tx) == tx - 1) fputc('\n', stderr);
-                    }
-            }
-        }
-        unsigned long long ss[8];
-        if (rt_shadow_stats(ss, st))
-            fprintf(stderr,
-                    "[cg_rt_lattice] pass-2 wave steps lit %llu shadowed %llu mixed %llu; shadow iterations "
-                    "lit %llu shadowed %llu (best-first %llu) mixed %llu; lanes %llu\n",
-                    ss[0], ss[1], ss[2], ss[3], ss[4], ss[6], ss[5], ss[7]);
-        unsigned long long ph[8];
-        if (rt_lat_stamps(ph, st)) {
-            const double waves = (double)nf * tiles * (kRtThreads / 64);
-            fprintf(stderr, "[cg_rt_lattice] cycles per wave: pass1 %.0f, pass2 %.0f, barrier %.0f, pixels %.0f\n",
-                    ph[0] / waves, ph[3] / waves, ph[4] / waves, ph[5] / waves);
-        }
-    }
+    CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
     return CG_OK;
 }
 
@@ -887,11 +799,7 @@ extern "C" int cg_rast_draw_frames_device(cg_ctx *c, const cg_rast_params *ps, i
             return ctx_invalid(c, "draw_frames: colour mode 0 frames of one size (modes 1-2 chain rand offsets)");
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    static const int env_lanes = [] {
-        const char *e = getenv("CG_RAST_LANES");
-        return e ? std::max(1, std::min(cg_ctx::kRastLanes, atoi(e))) : 2;   // measured: 2 > 4 > 3 (C3)
-    }();
-    const int L = std::min(env_lanes, n_frames);
+    const int L = std::min(2, n_frames);   // lanes in flight: 2 measured faster than 3 or 4 (C3, round 1)
     if (!c->start_ev) CG_TRY(c, hipEventCreateWithFlags(&c->start_ev, hipEventDisableTiming), "event");
     for (int k = 0; k < L; ++k) {
         if (!c->lanes[k]) {

@@ -19,9 +19,6 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
-#ifdef CGO_DEBUG
-#include <stdio.h>
-#endif
 
 static inline cgo_v3 v3(float x, float y, float z) { cgo_v3 r = {x, y, z}; return r; }
 static inline cgo_v4 v4(float x, float y, float z, float w) { cgo_v4 r = {x, y, z, w}; return r; }
@@ -347,18 +344,6 @@ int cgo_rast_geometry(const cgo_rast_params *p, cgo_rast_tri *out, int cap, cgo_
     /* clip planes 1..6 (:236-241) */
     for (int plane = 1; plane <= 6; ++plane) {
         int k = cgo_rast_clip(A, n, plane, p, B, MAXT);
-#ifdef CGO_DEBUG
-        for (int q = 0; q < n; ++q) {
-            cgo_rast_tri tmp1[4]; int kk = cgo_rast_clip(&A[q], 1, plane, p, tmp1, 4);
-            for (int z = 0; z < kk; ++z) { const float *f = (const float *)&tmp1[z]; int b = 0;
-              for (int u = 0; u < 12; ++u) if (!isfinite(f[u]) || (u % 4 == 2 && f[u] < 0)) b = 1;
-              if (b) { printf("plane %d in#%d -> out#%d/%d\n", plane, q, z, kk);
-                const cgo_rast_tri *t = &A[q];
-                printf(" IN v0(%g %g %g %g) v1(%g %g %g %g) v2(%g %g %g %g)\n",t->v0.x,t->v0.y,t->v0.z,t->v0.w,t->v1.x,t->v1.y,t->v1.z,t->v1.w,t->v2.x,t->v2.y,t->v2.z,t->v2.w);
-                t = &tmp1[z];
-                printf(" OUT v0(%g %g %g %g) v1(%g %g %g %g) v2(%g %g %g %g)\n",t->v0.x,t->v0.y,t->v0.z,t->v0.w,t->v1.x,t->v1.y,t->v1.z,t->v1.w,t->v2.x,t->v2.y,t->v2.z,t->v2.w);} }
-        }
-#endif
         if (k > MAXT) k = MAXT;
         cgo_rast_tri *tmp = A; A = B; B = tmp;
         n = k;
