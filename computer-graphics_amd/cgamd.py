@@ -132,6 +132,7 @@ _SIGS = {
     "cg_rast_draw_device": (C.c_int, [P, C.POINTER(RastParams), P, P, P, P]),
     "cg_rast_draw_frames_device": (C.c_int, [P, C.POINTER(RastParams), C.c_int, P, P, P, C.c_size_t, P]),
     "cg_image_jpeg_info": (C.c_int, [P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "cg_image_jpeg_check": (C.c_int, [P, C.c_size_t]),
     "cg_image_decode_jpeg": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
     "cg_image_decode_jpeg_device": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t, P]),
 }

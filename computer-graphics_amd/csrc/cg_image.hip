@@ -695,6 +695,14 @@ extern "C" int cg_image_jpeg_info(const uint8_t *data, size_t n, int *width, int
     return CG_OK;
 }
 
+extern "C" int cg_image_jpeg_check(const uint8_t *data, size_t n)
+{
+    if (!data) return CG_E_INVALID;
+    JpegFrame f;
+    JpegDecoder dec(f);
+    return dec.parse(data, n, false) ? CG_E_INVALID : CG_OK;
+}
+
 extern "C" int cg_image_decode_jpeg(cg_ctx *ctx, const uint8_t *data, size_t n, uint8_t *out, size_t cap)
 {
     if (!ctx || !data || !out) return CG_E_INVALID;

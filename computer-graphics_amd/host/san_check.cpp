@@ -1,0 +1,118 @@
+// san_check.cpp -- the library's host-side code under AddressSanitizer and
+// UBSan (Makefile `sanitize`; no GPU needed): every C-ABI entry that runs on
+// the host -- scene builders, the rasteriser's host geometry (camera space,
+// shadow volumes, the six clip planes with the plane-6 quirks,
+// rasteriser/Source/skeleton.cpp:205-241, 720-1673), the RT column window,
+// the opacity maps, glibc rand(), the starfield, and the JPEG parser and
+// entropy decoder on the reference's textures and on damaged copies.
+//   san_check TEXTURE_DIR
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cg_render.h"
+
+static std::vector<uint8_t> slurp(const std::string &path)
+{
+    std::vector<uint8_t> v;
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return v;
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0) v.insert(v.end(), buf, buf + n);
+    fclose(f);
+    return v;
+}
+
+static void fail(const char *what, int rc)
+{
+    fprintf(stderr, "%s failed: %d\n", what, rc);
+    exit(1);
+}
+
+int main(int argc, char **argv)
+{
+    const std::string dir = argc > 1 ? argv[1] : "tests/golden/textures";
+    // JPEG: the reference's maps, truncated and corrupted copies
+    const char *files[] = {"Metal_Grill_002_basecolor.jpg", "Metal_Grill_002_opacity.jpg", "Metal_Grill_002_normal.jpg",
+                           "woven1024x1024.jpg", "Wood_wicker_003_ambientOcclusion.jpg", "Wood_wicker_003_opacity.jpg",
+                           "Wood_wicker_003_normal.jpg"};
+    int checked = 0;
+    for (const char *fn : files) {
+        std::vector<uint8_t> j = slurp(dir + "/" + fn);
+        if (j.empty()) fail(fn, -1);
+        int w, h, c;
+        if (int rc = cg_image_jpeg_info(j.data(), j.size(), &w, &h, &c)) fail("cg_image_jpeg_info", rc);
+        if (int rc = cg_image_jpeg_check(j.data(), j.size())) fail("cg_image_jpeg_check", rc);
+        for (size_t cut = 2; cut < j.size(); cut = cut * 3 + 5) (void)cg_image_jpeg_check(j.data(), cut);
+        std::vector<uint8_t> bad = j;
+        for (size_t k = bad.size() / 4; k < bad.size(); k += 1013) bad[k] ^= 0xa5;
+        (void)cg_image_jpeg_check(bad.data(), bad.size());
+        for (size_t k = 2; k + 1 < bad.size() && k < 700; k += 7) bad[k] = 0xff;   // damaged headers
+        (void)cg_image_jpeg_info(bad.data(), bad.size(), &w, &h, &c);
+        (void)cg_image_jpeg_check(bad.data(), bad.size());
+        ++checked;
+    }
+    // rasteriser host geometry over cameras inside / outside / behind the near plane, yawed
+    cg_rtri room[16], boxes[32];
+    int nr = 0, nb = 0;
+    if (int rc = cg_rast_load_test_model(room, 16, &nr, boxes, 32, &nb); rc < 0) fail("cg_rast_load_test_model", rc);
+    std::vector<cg_rtri> out(32 * (nr + 7 * nb));
+    const float cams[][3] = {{0, 0, -3.001f}, {0, 0, -1.2f}, {0.9f, 0.5f, -0.2f}, {-1.8f, 0, -1.6f},
+                             {0, 0, 0.95f}, {3, -2, 2}, {0, 0, -0.99f}, {0.3f, 0.99f, -3}};
+    long tris = 0;
+    for (const auto &cam : cams)
+        for (float yaw : {0.0f, 0.174533f, -0.8726650476455688f, 3.0f})
+            for (int W : {3, 161, 900}) {
+                cg_rast_params p{};
+                p.width = W;
+                p.height = W * 3 / 4 + 1;
+                p.focal = 0.6f * (float)W;
+                p.camera = cg_vec4{cam[0], cam[1], cam[2], 1.0f};
+                for (int k = 0; k < 16; ++k) p.R[k] = (k % 5 == 0) ? 1.0f : 0.0f;
+                p.R[0] = cosf(yaw); p.R[2] = -sinf(yaw); p.R[8] = sinf(yaw); p.R[10] = cosf(yaw);
+                p.light_scene = cg_vec4{0, -0.5f, 0, 1};
+                p.light_power = cg_vec3{20, 20, 20};
+                p.indirect_first = 0.2f;
+                p.yaw = yaw;
+                cg_vec4 light;
+                int n = cg_rast_prepare(&p, room, nr, boxes, nb, out.data(), (int)out.size(), &light);
+                if (n < 0) fail("cg_rast_prepare", n);
+                tris += n;
+            }
+    // RT scenes, column windows, lights, rand, opacity, starfield
+    cg_tri t[64];
+    cg_sphere sph;
+    int n = cg_rt_load_test_model(t, 64, &sph);
+    if (n < 0) fail("cg_rt_load_test_model", n);
+    std::vector<cg_tri> rnd(5000);
+    if (int rc = cg_rt_random_scene(0x5EED, 5000, rnd.data()); rc < 0) fail("cg_rt_random_scene", rc);
+    for (float z : {-3.0f, -1.5f, 0.0f, 2.0f}) {
+        cg_rt_camera cam{};
+        cam.width = 1920; cam.height = 1080; cam.focal = 1080.0f;
+        cam.camera = cg_vec4{0, 0, z, 1};
+        for (int k = 0; k < 16; ++k) cam.R[k] = (k % 5 == 0) ? 1.0f : 0.0f;
+        cam.indirect = 0.5f;
+        int c0 = 0, c1 = 0;
+        (void)cg_rt_frame_columns(t, n, &sph, 1, &cam, &c0, &c1);
+        (void)cg_rt_frame_columns(rnd.data(), 5000, nullptr, 0, &cam, &c0, &c1);
+    }
+    cg_light centre{{0, -0.5f, -0.7f, 1}, {14, 14, 14}}, area[64];
+    if (int rc = cg_rt_area_lights(&centre, 0.1f, 8, area, 64); rc < 0) fail("cg_rt_area_lights", rc);
+    std::vector<int32_t> r(4096);
+    if (int rc = cg_glibc_rand(0, 4096, r.data())) fail("cg_glibc_rand", rc);
+    if (int rc = cg_glibc_rand(11999000, 4096, r.data())) fail("cg_glibc_rand", rc);
+    std::vector<uint8_t> bgr(3 * 4096), op(4096);
+    for (size_t i = 0; i < bgr.size(); ++i) bgr[i] = (uint8_t)(i * 37);
+    if (int rc = cg_rast_opacity_map(bgr.data(), 4096, op.data())) fail("cg_rast_opacity_map", rc);
+    std::vector<float> stars(3 * 1000);
+    if (int rc = cg_starfield_init(stars.data(), 1000)) fail("cg_starfield_init", rc);
+    for (int k = 0; k < 100; ++k) cg_starfield_update(stars.data(), 1000, 16.0f);
+    cg_rt_shard sh{1, 3, 15, 0, 0, 0, 0};
+    (void)cg_rt_shard_rows(1080, &sh);
+    printf("sanitized host code: %d JPEGs, %ld clipped triangles, clean\n", checked, tris);
+    return 0;
+}

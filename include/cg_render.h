@@ -292,6 +292,9 @@ int cg_rast_opacity_map(const uint8_t *bgr, int n, uint8_t *out);
  * 4:2:0; anything else is CG_E_INVALID.  Entropy decoding runs on the host,
  * the IDCT and colour conversion on the context's GPU. */
 int cg_image_jpeg_info(const uint8_t *data, size_t n, int *width, int *height, int *channels);
+/* Host-only: entropy-decode the whole file without a device (0, or CG_E_INVALID
+ * for a corrupt or unsupported stream). */
+int cg_image_jpeg_check(const uint8_t *data, size_t n);
 /* out: caller-owned host buffer of >= width * height * channels bytes (cap). */
 int cg_image_decode_jpeg(cg_ctx *ctx, const uint8_t *data, size_t n, uint8_t *out, size_t cap);
 /* Same into device memory, enqueued on `stream` (NULL: the context's). */
