@@ -501,63 +501,123 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_pixel_kernel(RtFra
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
 
-// Pass 2 of rt_lattice_kernel for lattice points p and p + 64: DirectLight
-// (skeleton.cpp:366-415, as direct_light<true> with light 0) of each point
-// that hit, written over its LDS slot.  The shadow loop walks the tile's
-// candidates once for both points; each point stops at its first blocker.
-__device__ __forceinline__ void direct_light_pair(const RtFrame &F, const RtTri *__restrict__ tc,
-                                                  const RtShade *__restrict__ shade,
-                                                  const RtSphere *__restrict__ sph, float4 *s_pt,
-                                                  unsigned long long smask, int p, int p_hi, int cols, int ax0,
-                                                  int ay0)
+// Shared pieces of the two lattice kernels.
+//
+// Output of one tile: the pixel value px of (tx, ty) (have = inside the tile),
+// stored as ARGB at row L0 + ty, or in the RGB24 wire format (the pixel's low
+// three bytes, B, G, R; alpha is always 128) inside the output window, full
+// tiles writing each row's 48 bytes as 12 dwords through s_px.  Called by
+// every thread of the workgroup (RGB24 has a barrier).
+struct LatOut {
+    uint32_t *out;
+    uint8_t *out8;
+    int pitch, wc0;
+};
+__device__ __forceinline__ LatOut lat_out(const RtFrame &F, int frame, size_t out_stride, uint32_t *out)
 {
-    const RtLight Lt = F.lights[0];
-    const vec3 lp = v3(Lt.x, Lt.y, Lt.z);
-    bool hit[2], done[2];
-    int bi[2], pp[2];
-    vec3 pos[2], r[2], normal[2], origin[2];
-    float rmag[2], len[2];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        pp[n] = p + 64 * n;
-        const int cy = pp[n] / kLatW, cx = pp[n] - cy * kLatW;
-        float4 q = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(INT_MIN));
-        if (pp[n] < p_hi && cx < cols) q = s_pt[pp[n]];
-        bi[n] = __float_as_int(q.w);
-        hit[n] = bi[n] != INT_MIN;
-        const int b = hit[n] ? bi[n] : 0;
-        const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy), t = q.x;
-        pos[n] = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-        r[n] = lp - pos[n];                                               // :370
-        rmag[n] = light_rmag(r[n]);                                       // :371
-        normal[n] = hit_normal(shade, sph, b, pos[n]);                    // :377-387
-        origin[n] = pos[n] + normal[n] * 0.00001f;                        // :394
-        len[n] = length(r[n]);
-        done[n] = !hit[n];
+    LatOut o;
+    o.out8 = (uint8_t *)out + (size_t)frame * out_stride * 3;   // CG_PIX_RGB24
+    o.out = out + (size_t)frame * out_stride;
+    // RGB24 window (a caller's contract: the columns outside are black);
+    // windows are 16-pixel aligned
+    o.pitch = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcols : F.W;
+    o.wc0 = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcol0 : 0;
+    return o;
+}
+__device__ __forceinline__ void lat_store(const RtFrame &F, const LatTile &G, const LatOut &o, uint32_t px, int tx,
+                                          int ty, uint32_t *s_px)
+{
+    const bool have = tx < G.nu && ty < G.nv;
+    if (F.out_fmt == CG_PIX_ARGB8888) {
+        if (have) o.out[(size_t)(G.L0 + ty) * F.W + G.u0 + tx] = px;
+        return;
     }
-    bool shadow[2] = {false, false};
-    unsigned long long m = smask;
-    while (m != 0ull && !(done[0] && done[1])) {                         // :394-398
-        const int k = __builtin_ctzll(m);
-        m &= m - 1ull;
-        const RtTri c = tc[k];
+    if (have) s_px[ty * kLatTileW + tx] = px;
+    __syncthreads();
+    if (G.nu == kLatTileW && (o.pitch & 3) == 0 && ((uintptr_t)o.out8 & 3) == 0) {
+        const int t = threadIdx.x, row = t / 12, j = t - 12 * row;
+        if (row < G.nv) {
+            uint32_t w = 0u;
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-            if (!done[n] && tri_shadow_hit(c, origin[n], -r[n], len[n], rmag[n])) shadow[n] = done[n] = true;
-    }
-    for (int k = 0; k < F.n_sph; ++k) {
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            float ts;
-            if (!done[n] && sphere_intersect(sph[k], origin[n], r[n], ts) && ts < rmag[n]) shadow[n] = done[n] = true;
+            for (int b = 0; b < 4; ++b) {
+                const int byte = 4 * j + b, p = byte / 3, ch = byte - 3 * p;
+                w |= ((s_px[row * kLatTileW + p] >> (8 * ch)) & 0xffu) << (8 * b);
+            }
+            *(uint32_t *)(o.out8 + ((size_t)(G.L0 + row) * o.pitch + (G.u0 - o.wc0)) * 3 + 4 * j) = w;
         }
+    } else if (have) {
+        uint8_t *q = o.out8 + ((size_t)(G.L0 + ty) * o.pitch + (G.u0 - o.wc0) + tx) * 3;
+        q[0] = (uint8_t)px;
+        q[1] = (uint8_t)(px >> 8);
+        q[2] = (uint8_t)(px >> 16);
     }
+}
+
+// Pass 1 of the lattice kernels: the closest hit (:140) of lattice points
+// p_lo .. p_hi - 1 (row-major at pitch kLatW; columns >= cols exist only in
+// tiles cut by the right edge), two points per lane per step (p, p + 64) with
+// one triangle load for both; store(p, t, hit index) for each needed point.
+// covered: the tile's one candidate triangle k is certainly accepted by every
+// ray (rt_tile_cert_kernel: t > 0, u, v inside, nothing else can be hit), so
+// the reference's closest hit is k with t = detT / det (:306), formed with
+// closest_primary_n's float ops; the u, v tests and the distance are not needed.
+template <class Store>
+__device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__restrict__ tc,
+                                            const RtSphere *__restrict__ sph, unsigned long long mask, bool covered,
+                                            const LatTile &G, int p_lo, int p_hi, int lane, Store store)
+{
+    constexpr int NP = 2;
+    for (int p0 = p_lo; p0 < p_hi; p0 += 64 * NP) {
+        float X[NP], Y[NP];
+        bool live[NP];
+        int pp[NP];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        if (!hit[n]) continue;
-        const vec3 dl = shadow[n] ? v3(0.0f, 0.0f, 0.0f)
-                                  : direct_light_lit(Lt, r[n], rmag[n], normal[n], object_colour(shade, sph, bi[n]));
-        s_pt[pp[n]] = make_float4(dl.x, dl.y, dl.z, __int_as_float(bi[n]));
+        for (int n = 0; n < NP; ++n) {
+            const int p = p0 + 64 * n + lane;
+            const int cy = p / kLatW, cx = p - cy * kLatW;
+            pp[n] = p;
+            live[n] = p < p_hi && cx < G.cols;
+            X[n] = 0.5f * (float)(G.ax0 + cx);
+            Y[n] = 0.5f * (float)(G.ay0 + cy);
+        }
+        int bi[NP];
+        float t[NP];
+        if (covered) {
+            const int k = __builtin_ctzll(mask);
+            const RtTri c = tc[k];
+#pragma unroll
+            for (int n = 0; n < NP; ++n) {
+                const vec3 nd = -v3(X[n], Y[n], Fp.focal);
+                const float Q2 = nd.y * c.e2z - c.e2y * nd.z;
+                const float Q1 = nd.y * c.e1z - c.e1y * nd.z;
+                const float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;   // :289
+                t[n] = c.detT / det;                                         // :306
+                bi[n] = k;
+            }
+        } else {
+            closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t);   // :140
+        }
+#pragma unroll
+        for (int n = 0; n < NP; ++n)
+            if (live[n]) store(pp[n], t[n], bi[n]);
+    }
+}
+
+// A tile no ray of which can hit anything (certified): every pixel is
+// PutPixelSDL(0, 0, 0) = 0x80000000 (:160-166).
+__device__ __forceinline__ void lat_store_black(const RtFrame &F, const LatTile &G, const LatOut &o)
+{
+    const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+    if (tx < G.nu && ty < G.nv) {
+        const uint32_t px = put_pixel(v3(0.0f, 0.0f, 0.0f));
+        if (F.out_fmt == CG_PIX_ARGB8888) {
+            o.out[(size_t)(G.L0 + ty) * F.W + G.u0 + tx] = px;
+        } else {
+            const size_t q = (size_t)(G.L0 + ty) * o.pitch + (G.u0 - o.wc0) + tx;
+            o.out8[3 * q] = (uint8_t)px;
+            o.out8[3 * q + 1] = (uint8_t)(px >> 8);
+            o.out8[3 * q + 2] = (uint8_t)(px >> 16);
+        }
     }
 }
 
@@ -577,100 +637,41 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
     tc += (size_t)frame * F.n_tris;
     lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
-    uint8_t *out8 = (uint8_t *)out + (size_t)frame * out_stride * 3;   // CG_PIX_RGB24
-    out += (size_t)frame * out_stride;
+    const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
-    const int u0 = G.u0, L0 = G.L0, nu = G.nu, nv = G.nv, ax0 = G.ax0, ay0 = G.ay0;
-    const int cols = G.cols, rows = G.rows;
+    const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
     // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
     __shared__ float4 s_pt[kLatN];
     __shared__ RtShade s_shade[64];
+    __shared__ uint32_t s_px[kLatTileH * kLatTileW];
     if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
-    // the needed points, walked row-major at the full pitch kLatW (columns >=
-    // cols exist only in tiles cut by the right edge); wave w takes the w-th quarter
+    // the needed points, walked row-major at the full pitch kLatW; wave w takes
+    // the w-th quarter
     const int npts = kLatW * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
+    if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window: whole workgroup
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
-    // sphere may be hit) and shadow mask for every hit the tile can produce
-    // RGB24 window (a caller's contract: the columns outside are black): tiles
-    // outside it store nothing; windows are 16-pixel aligned
-    const int pitch = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcols : F.W;
-    const int wc0 = (F.out_fmt == CG_PIX_RGB24 && F.wcols) ? F.wcol0 : 0;
-    if (u0 + nu <= wc0 || u0 >= wc0 + pitch) return;   // whole workgroup
+    // sphere may be hit; bit 62: covered) and shadow mask for every hit the
+    // tile can produce
     const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
     const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
-    const bool covered = (m0 >> 62) & 1ull;   // one triangle, hit by every ray of the tile (certified)
+    const bool covered = (m0 >> 62) & 1ull;
     RtFrame Fp = F;                        // pass 1: spheres only where one may be hit
     if (!(m0 >> 63)) Fp.n_sph = 0;
     RtFrame Fs = F;                        // pass 2: spheres only where one may block a shadow ray
     if (!(s0 >> 63)) Fs.n_sph = 0;
     if (m0 == 0ull) {
-        // no ray of the tile can hit anything (certified): every pixel is
-        // PutPixelSDL(0, 0, 0) = 0x80000000 (:160-166)
-        const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
-        if (tx < nu && ty < nv) {
-            const uint32_t px = put_pixel(v3(0.0f, 0.0f, 0.0f));
-            if (F.out_fmt == CG_PIX_ARGB8888) {
-                out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
-            } else {
-                const size_t o = (size_t)(L0 + ty) * pitch + (u0 - wc0) + tx;
-                out8[3 * o] = (uint8_t)px;
-                out8[3 * o + 1] = (uint8_t)(px >> 8);
-                out8[3 * o + 2] = (uint8_t)(px >> 16);
-            }
-        }
+        lat_store_black(F, G, o);
         return;                            // the whole workgroup (m0 is uniform)
     }
     __syncthreads();                       // s_shade
-    // Pass 1: closest hits (:140) of the wave's lattice rays, staged in LDS
-    // two points per lane per step (p, p + 64): one triangle
-    // load for all of them
-    constexpr int NP = 2;
-    for (int p0 = p_lo; p0 < p_hi; p0 += 64 * NP) {
-        float X[NP], Y[NP];
-        bool live[NP];
-        int pp[NP];
-#pragma unroll
-        for (int n = 0; n < NP; ++n) {
-            const int p = p0 + 64 * n + lane;
-            const int cy = p / kLatW, cx = p - cy * kLatW;
-            pp[n] = p;
-            live[n] = p < p_hi && cx < cols;
-            X[n] = 0.5f * (float)(ax0 + cx);
-            Y[n] = 0.5f * (float)(ay0 + cy);
-        }
-        int bi[NP];
-        float t[NP];
-        if (covered) {
-            // the tile's one candidate triangle k is certainly accepted by every
-            // ray (rt_tile_cert_kernel: t > 0, u, v inside, nothing else can be
-            // hit): the reference's closest hit is k with t = detT / det (:306),
-            // formed with closest_primary_n's float ops; the u, v tests and the
-            // distance are not needed
-            const int k = __builtin_ctzll(mask);
-            const RtTri c = tc[k];
-#pragma unroll
-            for (int n = 0; n < NP; ++n) {
-                const vec3 nd = -v3(X[n], Y[n], F.focal);
-                const float Q2 = nd.y * c.e2z - c.e2y * nd.z;
-                const float Q1 = nd.y * c.e1z - c.e1y * nd.z;
-                const float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;   // :289
-                t[n] = c.detT / det;                                         // :306
-                bi[n] = k;
-            }
-        } else {
-            closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t);                   // :140
-        }
-#pragma unroll
-        for (int n = 0; n < NP; ++n) {
-            if (!live[n]) continue;
-            s_pt[pp[n]] = make_float4(t[n], 0.0f, 0.0f, __int_as_float(bi[n]));
-        }
-    }
+    lat_closest(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
+        s_pt[p] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
+    });
     // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
     // attributes from the LDS copy
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
@@ -691,9 +692,8 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
     __syncthreads();
     // Pixels: the nine contributions in the reference's order (:134-166)
     const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
-    const bool have = tx < nu && ty < nv;
     uint32_t px = 0u;
-    if (have) {
+    if (tx < G.nu && ty < G.nv) {
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
@@ -709,32 +709,164 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
             pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
-        if (F.out_fmt == CG_PIX_ARGB8888) out[(size_t)(L0 + ty) * F.W + u0 + tx] = px;
     }
-    if (F.out_fmt == CG_PIX_RGB24) {
-        // wire format: the pixel's low three bytes (B, G, R; alpha is always 128).
-        // Full tiles write each row's 48 bytes as 12 dwords.
-        __shared__ uint32_t s_px[kLatTileH * kLatTileW];
-        if (have) s_px[ty * kLatTileW + tx] = px;
-        __syncthreads();
-        if (nu == kLatTileW && (pitch & 3) == 0 && ((uintptr_t)out8 & 3) == 0) {
-            const int t = threadIdx.x, row = t / 12, j = t - 12 * row;
-            if (row < nv) {
-                uint32_t w = 0u;
+    lat_store(F, G, o, px, tx, ty, s_px);
+}
+
+// ---------------------------------------------------------------------------
+// Lattice form of Draw for a light set (C4's 8 x 8 area light: 2..64 lights),
+// unrotated camera.  A pixel forms
+//   pc = (((0 + DL(s0, l0)) + DL(s0, l1)) + ... + DL(s0, l_last)) + amb(s0) + DL(s1, l0) ...
+// (:134-157): each lattice ray's per-light values are pixel-independent, but
+// their sum is not -- float addition is ordered -- so a pixel needs every
+// (sub-ray, light) value individually, in order.  Pixel (tx, ty)'s sub-rays
+// are lattice points (2tx + 1 + i, 2ty + 1 + j), i outer: in column-major
+// order they INCREASE (column first, then row).  So the tile sweeps its lattice
+// columns left to right: step c computes DirectLight of every point of column
+// c for every light into an LDS column buffer (all 256 threads, one (point,
+// light) pair each), and the next step -- while column c + 1 is being
+// computed into the other buffer -- 48 lanes fold column c into the pixels
+// that use it (an even column is the first column of pixel c/2 and the last
+// of pixel c/2 - 1, an odd one the middle column of pixel (c - 1)/2), one lane
+// per (pixel, component), adding the column's three points in row order, each
+// point's lights in order and then its ambient term.  Every sum is the
+// reference's sum; each (point, light) pair is computed once instead of for
+// up to four pixels (1023 points for 240 pixels instead of 2160 sub-rays).
+// The tile's 15 pixel rows are swept in two halves (pixel rows 0-7 and
+// 8-14; lattice row 16 is computed by both) so the column buffers stay small
+// (2 x 17 rows x 3 x 64 floats).
+constexpr int kLatHalfH = 8;                        // pixel rows per half
+constexpr int kLatHalfRows = 2 * kLatHalfH + 1;     // lattice rows per half
+constexpr int kLatMaxLights = 64;
+
+__global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+                                                                          const RtShade *__restrict__ shade,
+                                                                          const RtSphere *__restrict__ sph,
+                                                                          const unsigned long long *__restrict__ lat_masks,
+                                                                          RtFrameCams cams, size_t out_stride,
+                                                                          uint32_t *__restrict__ out)
+{
+    const int frame = blockIdx.z;
+    RtFrame F = F0;
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int byte = 4 * j + b, p = byte / 3, ch = byte - 3 * p;
-                    w |= ((s_px[row * kLatTileW + p] >> (8 * ch)) & 0xffu) << (8 * b);
-                }
-                *(uint32_t *)(out8 + ((size_t)(L0 + row) * pitch + (u0 - wc0)) * 3 + 4 * j) = w;
-            }
-        } else if (have) {
-            uint8_t *q = out8 + ((size_t)(L0 + ty) * pitch + (u0 - wc0) + tx) * 3;
-            q[0] = (uint8_t)px;
-            q[1] = (uint8_t)(px >> 8);
-            q[2] = (uint8_t)(px >> 16);
+    for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
+    tc += (size_t)frame * F.n_tris;
+    lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
+    const LatOut o = lat_out(F, frame, out_stride, out);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
+    const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
+    __shared__ float2 s_hit[kLatN];                                   // (t, hit index bits)
+    __shared__ RtShade s_shade[64];
+    __shared__ float s_dl[2][kLatHalfRows][3][kLatMaxLights];         // column buffers
+    __shared__ float s_pc[kLatTileH][kLatTileW][3];                   // pixel sums
+    __shared__ uint8_t s_valid[kLatTileH][kLatTileW];
+    if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
+    const int npts = kLatW * rows;
+    const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
+    if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window
+    const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
+    const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
+    const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
+    const bool covered = (m0 >> 62) & 1ull;
+    RtFrame Fp = F;
+    if (!(m0 >> 63)) Fp.n_sph = 0;
+    RtFrame Fs = F;
+    if (!(s0 >> 63)) Fs.n_sph = 0;
+    if (m0 == 0ull) {
+        lat_store_black(F, G, o);
+        return;
+    }
+    {
+        const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+        if (ty < kLatTileH) {
+            s_pc[ty][tx][0] = s_pc[ty][tx][1] = s_pc[ty][tx][2] = 0.0f;
+            s_valid[ty][tx] = 0;
         }
     }
+    __syncthreads();                       // s_shade
+    lat_closest(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
+        s_hit[p] = make_float2(t, __int_as_float(bi));
+    });
+    __syncthreads();
+    const int nL = F.n_lights;
+    const float ind = F.indirect;
+    // folding lanes: wave 3, lane = 24 k + 3 pr + comp (k = 0: the pixel whose
+    // first or middle column this is, k = 1: the pixel whose last column it is)
+    const bool folder = wave == 3 && lane < 48;
+    const int fk = lane / 24, fpr = (lane % 24) / 3, fcomp = lane % 3;
+    for (int h = 0; h * kLatHalfH < G.nv; ++h) {
+        const int pr0 = h * kLatHalfH, npr = min(kLatHalfH, G.nv - pr0);
+        const int lr0 = 2 * pr0, nlr = 2 * npr + 1, items = nlr * nL;
+        for (int step = 0; step <= cols; ++step) {
+            if (step < cols) {   // DirectLight of column `step`, every light (:151-153, :366-415)
+                const int cx = step;
+                const float X = 0.5f * (float)(ax0 + cx);
+                for (int it = threadIdx.x; it < items; it += kRtThreads) {
+                    const int r = it / nL, l = it - r * nL;
+                    const int cy = lr0 + r;
+                    const float2 hq = s_hit[cy * kLatW + cx];
+                    const int bi = __float_as_int(hq.y);
+                    if (bi == INT_MIN) continue;
+                    const float Y = 0.5f * (float)(ay0 + cy), t = hq.x;
+                    const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
+                    const RtLight Lt = F.lights[l];
+                    const vec3 r3 = v3(Lt.x, Lt.y, Lt.z) - pos;                   // :370
+                    const float rmag = light_rmag(r3);                            // :371
+                    const vec3 normal = hit_normal(s_shade, sph, bi, pos);        // :377-387
+                    const vec3 origin = pos + normal * 0.00001f;                  // :394
+                    vec3 dl = v3(0.0f, 0.0f, 0.0f);
+                    if (!shadowed<true>(Fs, tc, sph, origin, r3, rmag, smask))    // :394-398
+                        dl = direct_light_lit(Lt, r3, rmag, normal, object_colour(s_shade, sph, bi));
+                    float *b = &s_dl[step & 1][r][0][l];
+                    b[0] = dl.x;
+                    b[kLatMaxLights] = dl.y;
+                    b[2 * kLatMaxLights] = dl.z;
+                }
+            }
+            if (step > 0 && folder) {   // fold column step - 1 into its pixels
+                const int cx = step - 1;
+                const int tx = fk == 0 ? cx / 2 : cx / 2 - 1;
+                const bool use = fpr < npr && tx >= 0 && tx < G.nu && (fk == 0 || (cx & 1) == 0);
+                if (use) {
+                    const int ty = pr0 + fpr;
+                    float pc = s_pc[ty][tx][fcomp];
+                    bool valid = false;
+                    const float *buf = &s_dl[cx & 1][0][0][0];
+                    for (int j = 0; j < 3; ++j) {
+                        const int r = 2 * fpr + j;
+                        const int bi = __float_as_int(s_hit[(lr0 + r) * kLatW + cx].y);
+                        if (bi == INT_MIN) continue;
+                        valid = true;
+                        const float *b = buf + (r * 3 + fcomp) * kLatMaxLights;
+                        int l = 0;
+                        for (; l + 4 <= nL; l += 4) {
+                            const float4 v = *(const float4 *)(b + l);
+                            pc = pc + v.x;
+                            pc = pc + v.y;
+                            pc = pc + v.z;
+                            pc = pc + v.w;
+                        }
+                        for (; l < nL; ++l) pc = pc + b[l];
+                        const vec3 oc = object_colour(s_shade, sph, bi);          // :147-148
+                        const float a = fcomp == 0 ? oc.x : (fcomp == 1 ? oc.y : oc.z);
+                        pc = pc + (a * ind);                                      // :156
+                    }
+                    s_pc[ty][tx][fcomp] = pc;
+                    if (valid && fcomp == 0) s_valid[ty][tx] = 1;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+    uint32_t px = 0u;
+    if (tx < G.nu && ty < G.nv) {
+        const vec3 pc = v3(s_pc[ty][tx][0], s_pc[ty][tx][1], s_pc[ty][tx][2]);
+        px = s_valid[ty][tx] ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
+    }
+    lat_store(F, G, o, px, tx, ty, (uint32_t *)&s_dl[0][0][0][0]);
 }
 
 // ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): rows
@@ -948,7 +1080,8 @@ static bool rt_lattice_ok(const RtFrame &F)
 // caller has rt_prepare_kernel certify its tiles first).
 bool rt_use_lattice(const RtFrame &F)
 {
-    return F.n_tris > 0 && F.n_tris <= 62 && F.cull_primary && F.n_lights == 1 && rt_lattice_ok(F);
+    return F.n_tris > 0 && F.n_tris <= 62 && F.cull_primary && F.n_lights >= 1 && F.n_lights <= kLatMaxLights &&
+           rt_lattice_ok(F);
 }
 
 size_t rt_lattice_tiles(const RtFrame &F)
@@ -963,9 +1096,13 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
                                     const RtFrameCams &cams, int nframes, size_t out_stride, uint32_t *d_out,
                                     hipStream_t st)
 {
-    hipLaunchKernelGGL(rt_lattice_kernel,
-                       dim3((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes),
-                       dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks, cams, out_stride, d_out);
+    const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
+    if (F.n_lights == 1)
+        hipLaunchKernelGGL(rt_lattice_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
+                           cams, out_stride, d_out);
+    else
+        hipLaunchKernelGGL(rt_lattice_lights_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+                           d_lat_masks, cams, out_stride, d_out);
     return hipGetLastError();
 }
 

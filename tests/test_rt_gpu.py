@@ -79,6 +79,35 @@ def test_rt_vs_live_oracle_diff_report(rt):
     assert bad.size == 0, f"{bad.size} pixels differ, first {bad[:8]} gpu {argb[bad[:4]]} ref {ref[bad[:4]]}"
 
 
+_LIGHT_SET = [((0.0, -0.5, -0.7, 1.0), (14.0, 14.0, 14.0)), ((0.3, -0.6, 0.2, 1.0), (3.0, 1.5, 0.5)),
+              ((-0.5, -0.2, -0.3, 1.0), (0.25, 2.0, 1.0)), ((0.2, 0.1, -0.9, 1.0), (1.0, 1.0, 6.0)),
+              ((0.0, -0.9, 0.0, 1.0), (2.5, 2.5, 2.5))]
+
+
+@pytest.mark.parametrize("case", ["lattice5", "lattice64", "yaw5", "yaw64"])
+def test_rt_light_sets_vs_oracle(rt, case):
+    """Light sets against the live oracle at a ragged size (partial lattice
+    tiles on both edges): unrotated cameras take rt_lattice_lights_kernel,
+    yawed ones rt_pixel_kernel.  5 lights (not a multiple of the fold's
+    4-light vector reads) and C4's 8 x 8 area light."""
+    W, H, f = 200, 118, 150.0
+    if case.endswith("64"):
+        lights = oracle.rt_area_lights((0.0, -0.5, -0.7, 1.0), (14.0, 14.0, 14.0), 0.1, 8)
+    else:
+        lights = _LIGHT_SET
+    R = cgamd.yaw_matrix(0.1) if case.startswith("yaw") else None
+    cam_pos = (0.05, -0.1, -2.7, 1.0)
+    p = oracle.rt_params(W, H, f, cam_pos, list(R) if R is not None else None, lights=lights)
+    ref = oracle.rt_draw(p, threads=os.cpu_count() or 8)
+    arr = (cgamd.Light * len(lights))()
+    for i, (pos, col) in enumerate(lights):
+        arr[i].position = cgamd.Vec4(*pos)
+        arr[i].colour = cgamd.Vec3(*col)
+    argb, _ = rt.rt_render(cgamd.rt_camera(W, H, f, cam_pos, R), arr)
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"{case}: {bad.size} pixels differ, first {bad[:8]}"
+
+
 def test_rt_probe_closest_and_direct_light(rt, golden):
     rays = golden["rt_rays"]
     out, hit = rt.rt_probe_closest([r["start"] for r in rays], [r["dir"] for r in rays])
