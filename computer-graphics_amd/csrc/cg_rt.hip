@@ -196,19 +196,19 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     if (cert && act && m != 0ull && sl < n && blo[0] <= bhi[0])
         keep_s = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, blo, bhi));
     // a tile whose every hit lies on one triangle k: k never shadows its own hits
-    if (cert && keep && keep_s && m == (1ull << sl) && F.n_lights == 1) {
-        const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};
-        if (own_shadow_rejects(tris[sl], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, blo, bhi)) keep_s = false;
+    if (cert && keep && keep_s && m == (1ull << sl)) {
+        const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // the light set's centre
+        if (own_shadow_rejects(tris[sl], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, F.lrho, blo, bhi))
+            keep_s = false;
     }
     unsigned long long sm = (__ballot(keep_s && sl < n) >> (sub * lpt)) & half;
     bool sph_shadow = F.n_sph > 0;   // bit 63 of the shadow mask: a sphere may block a shadow ray
     if (m == 0ull) {
         sm = 0ull;                   // no ray of the tile can hit anything: no shadow rays
         sph_shadow = false;
-    } else if (cert && F.n_lights == 1 && blo[0] <= bhi[0]) {
-        const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // one light: lc = its position
+    } else if (cert && blo[0] <= bhi[0]) {
         bool any = false;
-        for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed(sph[q], Lp, blo, bhi);
+        for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed_set(sph[q], F, blo, bhi);
         sph_shadow = any;
     }
     sm = (sm & ~(1ull << 63)) | (sph_shadow ? (1ull << 63) : 0ull);
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
     const unsigned long long SP = sup_masks[0], SS = sup_masks[1];
     const unsigned long long SPt = SP & ~(1ull << 63), SSt = SS & ~(1ull << 63);
     const bool cert = F.cull_shadow && F.n_lights > 0;
-    const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // one light: lc = its position
+    const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // the light set's centre
     __shared__ unsigned long long s_pm[kT], s_own[kT];
     __shared__ float s_box[kT][6];
     __shared__ int s_sphsh[kT];
@@ -335,8 +335,8 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
             bhi[q] = hi;
         }
         bool own = false;
-        if (cert && keep && m == (1ull << k) && F.n_lights == 1)
-            own = own_shadow_rejects(tris[k], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, blo, bhi);
+        if (cert && keep && m == (1ull << k))
+            own = own_shadow_rejects(tris[k], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, F.lrho, blo, bhi);
         const unsigned long long ownm = seg_or(own ? (1ull << k) : 0ull, cp);
         if (tl < kT && ci == 0) {
             const bool live = tile_of(tl, t, G);
@@ -348,9 +348,9 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
                 s_box[tl][3 + q] = bhi[q];
             }
             bool sphsh = F.n_sph > 0 && (SS >> 63);
-            if (live && m != 0ull && cert && F.n_lights == 1 && blo[0] <= bhi[0] && sphsh) {
+            if (live && m != 0ull && cert && blo[0] <= bhi[0] && sphsh) {
                 bool any = false;
-                for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed(sph[q], Lp, blo, bhi);
+                for (int q = 0; q < F.n_sph; ++q) any |= !sphere_shadow_surely_missed_set(sph[q], F, blo, bhi);
                 sphsh = any;
             }
             s_sphsh[tl] = sphsh ? 1 : 0;
@@ -735,6 +735,24 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
 // The tile's 15 pixel rows are swept in two halves (pixel rows 0-7 and
 // 8-14; lattice row 16 is computed by both) so the column buffers stay small
 // (2 x 17 rows x 3 x 64 floats).
+// Whether triangle c stays a shadow candidate for hits in [lo, hi] of camera
+// rays (X, [y0, y1], focal) towards the frame's light set: cull_shadow, and
+// when every hit lies on c (own) the own-triangle certificate.
+__device__ __forceinline__ bool lat_unit_keeps(const RtFrame &F, const RtTri &c, const RtShade &sh, bool own, float X,
+                                            float y0, float y1, const float (&lo)[3], const float (&hi)[3])
+{
+    if (cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, lo, hi))) return false;
+    if (!own) return true;
+    PrimDet pd;
+    double tlo, thi;
+    if (cull_primary(c, X, X, y0, y1, F.focal, &pd) || !primary_t_range(c, pd, tlo, thi)) return true;
+    cg_tri T{};
+    T.v0.x = c.v0x; T.v0.y = c.v0y; T.v0.z = c.v0z;
+    T.normal.x = sh.nx; T.normal.y = sh.ny; T.normal.z = sh.nz;
+    const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};
+    return !own_shadow_rejects(T, c, pd, thi, F.cam, X, X, y0, y1, F.focal, Lp, F.lrho, lo, hi);
+}
+
 constexpr int kLatHalfH = 8;                        // pixel rows per half
 constexpr int kLatHalfRows = 2 * kLatHalfH + 1;     // lattice rows per half
 constexpr int kLatMaxLights = 64;
@@ -790,8 +808,67 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
         s_hit[p] = make_float2(t, __int_as_float(bi));
     });
     __syncthreads();
+    // Shadow candidates per (half, column) unit: the tile's shadow mask
+    // re-certified over the unit's exact hit positions (pos as DirectLight
+    // forms it below), plus the own-triangle certificate when every hit of the
+    // unit lies on one triangle -- the same exact functions as
+    // rt_tile_cert_kernel, over a box of up to 17 points instead of the tile's.
+    __shared__ unsigned long long s_umask[2][kLatW];
+    // the units' boxes and sole hit triangles (-1: several, -2: no hit) live
+    // in the column buffers, which the sweep below has not started using yet
+    static_assert(sizeof(s_dl) >= 2 * kLatW * 7 * sizeof(float), "unit scratch");
+    float(*s_ubox)[kLatW][6] = (float(*)[kLatW][6]) & s_dl[0][0][0][0];
+    int(*s_uone)[kLatW] = (int(*)[kLatW]) & s_dl[1][0][0][0];
+    const int nhalf = (G.nv + kLatHalfH - 1) / kLatHalfH;
+    if (threadIdx.x < 2 * kLatW) {
+        const int h = threadIdx.x / kLatW, cx = threadIdx.x - h * kLatW;
+        if (h < nhalf && cx < cols) {
+            const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
+            LanePosBox pb;
+            pb.init();
+            int one = -2;
+            const float X = 0.5f * (float)(ax0 + cx);
+            for (int r = 0; r < nlr; ++r) {
+                const float2 hq = s_hit[(lr0 + r) * kLatW + cx];
+                const int bi = __float_as_int(hq.y);
+                if (bi == INT_MIN) continue;
+                const float Y = 0.5f * (float)(ay0 + lr0 + r), t = hq.x;
+                pb.add(v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal));
+                one = (one == -2 || one == bi) ? bi : -1;
+            }
+            for (int k = 0; k < 3; ++k) {
+                s_ubox[h][cx][k] = pb.lo[k];
+                s_ubox[h][cx][3 + k] = pb.hi[k];
+            }
+            s_uone[h][cx] = one;
+            s_umask[h][cx] = 0ull;
+        }
+    }
+    __syncthreads();
+    {
+        const int nc = __popcll(smask), pairs = nhalf * kLatW * nc;
+        for (int it = threadIdx.x; it < pairs; it += kRtThreads) {
+            const int unit = it / nc, ci = it - unit * nc;
+            const int h = unit / kLatW, cx = unit - h * kLatW;
+            if (cx >= cols) continue;
+            const int one = s_uone[h][cx];
+            if (one == -2) continue;   // no hit, no shadow ray
+            const int k = nth_bit(smask, ci);
+            const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
+            const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
+            const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
+            const float X = 0.5f * (float)(ax0 + cx);
+            const float y0 = 0.5f * (float)(ay0 + lr0), y1 = 0.5f * (float)(ay0 + lr0 + nlr - 1);
+            if (lat_unit_keeps(F, tc[k], s_shade[k], one == k, X, y0, y1, lo, hi))
+                atomicOr(&s_umask[h][cx], 1ull << k);
+        }
+    }
+    __syncthreads();
     const int nL = F.n_lights;
     const float ind = F.indirect;
+    const bool fixed_l = kRtThreads % nL == 0;
+    const int my_l = threadIdx.x % nL, r_first = threadIdx.x / nL, r_stride = kRtThreads / nL;
+    const RtLight my_light = F.lights[my_l];
     // folding lanes: wave 3, lane = 24 k + 3 pr + comp (k = 0: the pixel whose
     // first or middle column this is, k = 1: the pixel whose last column it is)
     const bool folder = wave == 3 && lane < 48;
@@ -802,27 +879,34 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
         for (int step = 0; step <= cols; ++step) {
             if (step < cols) {   // DirectLight of column `step`, every light (:151-153, :366-415)
                 const int cx = step;
+                const unsigned long long um = uniform_u64(s_umask[h][cx]);
                 const float X = 0.5f * (float)(ax0 + cx);
-                for (int it = threadIdx.x; it < items; it += kRtThreads) {
-                    const int r = it / nL, l = it - r * nL;
+                auto item = [&](int r, int l, const RtLight &Lt) {
                     const int cy = lr0 + r;
                     const float2 hq = s_hit[cy * kLatW + cx];
                     const int bi = __float_as_int(hq.y);
-                    if (bi == INT_MIN) continue;
+                    if (bi == INT_MIN) return;
                     const float Y = 0.5f * (float)(ay0 + cy), t = hq.x;
                     const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                    const RtLight Lt = F.lights[l];
                     const vec3 r3 = v3(Lt.x, Lt.y, Lt.z) - pos;                   // :370
                     const float rmag = light_rmag(r3);                            // :371
                     const vec3 normal = hit_normal(s_shade, sph, bi, pos);        // :377-387
                     const vec3 origin = pos + normal * 0.00001f;                  // :394
                     vec3 dl = v3(0.0f, 0.0f, 0.0f);
-                    if (!shadowed<true>(Fs, tc, sph, origin, r3, rmag, smask))    // :394-398
+                    if (!shadowed<true>(Fs, tc, sph, origin, r3, rmag, um))       // :394-398
                         dl = direct_light_lit(Lt, r3, rmag, normal, object_colour(s_shade, sph, bi));
                     float *b = &s_dl[step & 1][r][0][l];
                     b[0] = dl.x;
                     b[kLatMaxLights] = dl.y;
                     b[2 * kLatMaxLights] = dl.z;
+                };
+                if (fixed_l) {   // nL divides 256: each thread keeps one light (in registers)
+                    for (int r = r_first; r < nlr; r += r_stride) item(r, my_l, my_light);
+                } else {
+                    for (int it = threadIdx.x; it < items; it += kRtThreads) {
+                        const int r = it / nL, l = it - r * nL;
+                        item(r, l, F.lights[l]);
+                    }
                 }
             }
             if (step > 0 && folder) {   // fold column step - 1 into its pixels

@@ -352,10 +352,13 @@ __device__ __forceinline__ bool primary_covers(const RtTri &c, const PrimDet &pd
 // 1e-5 |n.N| exceeds that noise (each term is an upper bound; 5 % slack).  det = -d.N with d = L - pos:
 // -(L - v0).N up to (Delta + rounding of d) |N| + its det3 error.  Opposite
 // certain signs give t < 0 (|t| far from underflow): rejected at :311, for
-// every hit position in the box [blo, bhi] of hits on k.
+// every hit position in the box [blo, bhi] of hits on k.  A light set (every
+// light within rho of Lp) widens d by rho per component and moves -(L - v0).N
+// by at most rho |N|.
 __device__ static bool own_shadow_rejects(const cg_tri &T, const RtTri &c, const PrimDet &pd, double thi,
                                           const float cam[4], float x0, float x1, float y0, float y1, float f,
-                                          const double Lp[3], const float blo[3], const float bhi[3])
+                                          const double Lp[3], double rho_l, const float blo[3],
+                                          const float bhi[3])
 {
     const double eps = 5.9604644775390625e-8;   // 2^-24
     double dmin;
@@ -385,7 +388,7 @@ __device__ static bool own_shadow_rejects(const cg_tri &T, const RtTri &c, const
         rho2 += rk * rk;
         Sa[k] = fmax(fabs((double)blo[k] - v0[k]), fabs((double)bhi[k] - v0[k])) + o * fabs(n[k]) + rk;
         S2 += Sa[k] * Sa[k];
-        da[k] = fmax(fabs(Lp[k] - (double)blo[k]), fabs(Lp[k] - (double)bhi[k]));
+        da[k] = fmax(fabs(Lp[k] - (double)blo[k]), fabs(Lp[k] - (double)bhi[k])) + rho_l;
         d2 += da[k] * da[k];
     }
     const double Delta = sqrt(D2), rho = sqrt(rho2);
@@ -395,7 +398,7 @@ __device__ static bool own_shadow_rejects(const cg_tri &T, const RtTri &c, const
     const double aN = (Lp[0] - v0[0]) * N[0] + (Lp[1] - v0[1]) * N[1] + (Lp[2] - v0[2]) * N[2];
     const double noiseD = (Delta + eps * sqrt(d2)) * Nn + 16.0 * eps * det3_bound(da[0], da[1], da[2], e1, e2) +
                           1e-12 * fabs(aN);
-    if (!(fabs(aN) > 1.05 * noiseD)) return false;
+    if (!(fabs(aN) > 1.05 * noiseD + rho_l * Nn * (1.0 + 1e-9))) return false;
     return (nN > 0) != (-aN > 0);   // detT and det of opposite signs: t < 0
 }
 
@@ -462,6 +465,18 @@ __device__ static bool sphere_shadow_surely_missed(const RtSphere &S, const doub
     const double r = sqrt((double)S.r2) + 2e-3;
     // wu >= max |w.u| (sum of per-component maxima of |w_k u_k|)
     return w2 - (wu * wu) / n2 * (1.0 + 1e-9) > r * r * (1.0 + 1e-9) + 1e-4;
+}
+
+// The same for every light of a frame's set (each light tested on its own).
+__device__ static bool sphere_shadow_surely_missed_set(const RtSphere &S, const RtFrame &F, const float lo[3],
+                                                       const float hi[3])
+{
+    for (int l = 0; l < F.n_lights; ++l) {
+        const RtLight L = F.lights[l];
+        const double Lp[3] = {(double)L.x, (double)L.y, (double)L.z};
+        if (!sphere_shadow_surely_missed(S, Lp, lo, hi)) return false;
+    }
+    return true;
 }
 
 // Wave-wide min / max (ds_bpermute butterflies; a DPP row version measured
