@@ -503,6 +503,57 @@ constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLat
 
 // Shared pieces of the two lattice kernels.
 //
+// Shading attributes of every object a lattice ray can hit, in LDS: slot k
+// for triangle k (normal, colour), slot kLatSphSlot + q for sphere q
+// (centre, colour).  One table for both kinds keeps these reads LDS reads
+// (separate shade / sphere arrays make the compiler fetch through a flat
+// pointer, which waits for the vector memory counter as well).
+constexpr int kLatMaxSph = 8, kLatSphSlot = 64;
+struct LatObj {
+    float x, y, z, pad0;   // triangle normal, or sphere centre
+    float r, g, b, pad1;   // colour
+};
+__device__ __forceinline__ void lat_load_objs(LatObj *s_obj, const RtShade *__restrict__ shade,
+                                              const RtSphere *__restrict__ sph, int n_tris, int n_sph)
+{
+    const int t = threadIdx.x;
+    if (t < n_tris) {
+        const RtShade h = shade[t];
+        s_obj[t] = LatObj{h.nx, h.ny, h.nz, 0.0f, h.cr, h.cg, h.cb, 0.0f};
+    } else if (t >= kLatSphSlot && t < kLatSphSlot + n_sph) {
+        const RtSphere S = sph[t - kLatSphSlot];
+        s_obj[t] = LatObj{S.cx, S.cy, S.cz, 0.0f, S.cr, S.cg, S.cb, 0.0f};
+    }
+}
+__device__ __forceinline__ int lat_slot(int bi) { return bi >= 0 ? bi : kLatSphSlot - 1 - bi; }
+// object colour (skeleton.cpp:147-148, :378 / :382)
+__device__ __forceinline__ vec3 lat_colour(const LatObj *s_obj, int bi)
+{
+    const LatObj o = s_obj[lat_slot(bi)];
+    return v3(o.r, o.g, o.b);
+}
+// normal at the hit (:377-387): the triangle's, or Sphere::getNormal
+__device__ __forceinline__ vec3 lat_normal(const LatObj *s_obj, int bi, vec3 pos)
+{
+    const LatObj o = s_obj[lat_slot(bi)];
+    if (bi >= 0) return v3(o.x, o.y, o.z);
+    return normalize(pos - v3(o.x, o.y, o.z));
+}
+// DirectLight (skeleton.cpp:366-415) of light Lt for a hit on bi at pos, the
+// shadow ray walking the candidates of smask (as direct_light<true>)
+__device__ __forceinline__ vec3 lat_direct_light(const RtFrame &Fs, const RtTri *__restrict__ tc,
+                                                 const RtSphere *__restrict__ sph, const LatObj *s_obj,
+                                                 const RtLight &Lt, int bi, vec3 pos, unsigned long long smask)
+{
+    const vec3 r = v3(Lt.x, Lt.y, Lt.z) - pos;                          // :370
+    const float rmag = light_rmag(r);                                   // :371
+    const vec3 normal = lat_normal(s_obj, bi, pos);                     // :377-387
+    const vec3 origin = pos + normal * 0.00001f;                        // :394
+    if (shadowed<true>(Fs, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);   // :394-398
+    return direct_light_lit(Lt, r, rmag, normal, lat_colour(s_obj, bi));
+}
+
+//
 // Output of one tile: the pixel value px of (tx, ty) (have = inside the tile),
 // stored as ARGB at row L0 + ty, or in the RGB24 wire format (the pixel's low
 // three bytes, B, G, R; alpha is always 128) inside the output window, full
@@ -644,9 +695,9 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
     // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
     __shared__ float4 s_pt[kLatN];
-    __shared__ RtShade s_shade[64];
+    __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ uint32_t s_px[kLatTileH * kLatTileW];
-    if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
+    lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
     // the needed points, walked row-major at the full pitch kLatW; wave w takes
     // the w-th quarter
     const int npts = kLatW * rows;
@@ -668,12 +719,12 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
         lat_store_black(F, G, o);
         return;                            // the whole workgroup (m0 is uniform)
     }
-    __syncthreads();                       // s_shade
+    __syncthreads();                       // s_obj
     lat_closest(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_pt[p] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
     });
     // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
-    // attributes from the LDS copy
+    // attributes from the LDS table
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
         const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
@@ -684,7 +735,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
                 const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
                 const float t = q.x;
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                const vec3 dl = direct_light<true>(Fs, tc, s_shade, sph, bi, pos, object_colour(s_shade, sph, bi), 0, smask);
+                const vec3 dl = lat_direct_light(Fs, tc, sph, s_obj, F.lights[0], bi, pos, smask);
                 s_pt[idx] = make_float4(dl.x, dl.y, dl.z, q.w);
             }
         }
@@ -706,7 +757,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
             if (bi == INT_MIN) continue;
             valid = true;
             pc = pc + v3(q.x, q.y, q.z);                                                  // :151-153
-            pc = pc + (object_colour(s_shade, sph, bi) * ind);                            // :156
+            pc = pc + (lat_colour(s_obj, bi) * ind);                                      // :156
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
     }
@@ -738,7 +789,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
 // Whether triangle c stays a shadow candidate for hits in [lo, hi] of camera
 // rays (X, [y0, y1], focal) towards the frame's light set: cull_shadow, and
 // when every hit lies on c (own) the own-triangle certificate.
-__device__ __forceinline__ bool lat_unit_keeps(const RtFrame &F, const RtTri &c, const RtShade &sh, bool own, float X,
+__device__ __forceinline__ bool lat_unit_keeps(const RtFrame &F, const RtTri &c, const LatObj &sh, bool own, float X,
                                             float y0, float y1, const float (&lo)[3], const float (&hi)[3])
 {
     if (cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, lo, hi))) return false;
@@ -748,7 +799,7 @@ __device__ __forceinline__ bool lat_unit_keeps(const RtFrame &F, const RtTri &c,
     if (cull_primary(c, X, X, y0, y1, F.focal, &pd) || !primary_t_range(c, pd, tlo, thi)) return true;
     cg_tri T{};
     T.v0.x = c.v0x; T.v0.y = c.v0y; T.v0.z = c.v0z;
-    T.normal.x = sh.nx; T.normal.y = sh.ny; T.normal.z = sh.nz;
+    T.normal.x = sh.x; T.normal.y = sh.y; T.normal.z = sh.z;
     const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};
     return !own_shadow_rejects(T, c, pd, thi, F.cam, X, X, y0, y1, F.focal, Lp, F.lrho, lo, hi);
 }
@@ -756,6 +807,12 @@ __device__ __forceinline__ bool lat_unit_keeps(const RtFrame &F, const RtTri &c,
 constexpr int kLatHalfH = 8;                        // pixel rows per half
 constexpr int kLatHalfRows = 2 * kLatHalfH + 1;     // lattice rows per half
 constexpr int kLatMaxLights = 64;
+// Column-buffer swizzle: light l of (row r, component c) sits at slot
+// l ^ lat_swz(r, c).  The folding lanes read the same light group of 24
+// different (r, c) rows at once; rows 64 floats apart would all hit one LDS
+// bank, the xor spreads them over 16 float4 slots.  It keeps groups of four
+// lights contiguous and in order, so one ds_read_b128 still yields l .. l + 3.
+__device__ __forceinline__ int lat_swz(int r, int c) { return 4 * ((r * 3 + c) & 15); }
 
 __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                           const RtShade *__restrict__ shade,
@@ -775,11 +832,11 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
     const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
     const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
     __shared__ float2 s_hit[kLatN];                                   // (t, hit index bits)
-    __shared__ RtShade s_shade[64];
+    __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ float s_dl[2][kLatHalfRows][3][kLatMaxLights];         // column buffers
     __shared__ float s_pc[kLatTileH][kLatTileW][3];                   // pixel sums
     __shared__ uint8_t s_valid[kLatTileH][kLatTileW];
-    if (threadIdx.x < F.n_tris) s_shade[threadIdx.x] = shade[threadIdx.x];
+    lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
     const int npts = kLatW * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
     if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window
@@ -803,7 +860,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
             s_valid[ty][tx] = 0;
         }
     }
-    __syncthreads();                       // s_shade
+    __syncthreads();                       // s_obj
     lat_closest(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_hit[p] = make_float2(t, __int_as_float(bi));
     });
@@ -859,24 +916,28 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
             const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
             const float X = 0.5f * (float)(ax0 + cx);
             const float y0 = 0.5f * (float)(ay0 + lr0), y1 = 0.5f * (float)(ay0 + lr0 + nlr - 1);
-            if (lat_unit_keeps(F, tc[k], s_shade[k], one == k, X, y0, y1, lo, hi))
+            if (lat_unit_keeps(F, tc[k], s_obj[k], one == k, X, y0, y1, lo, hi))
                 atomicOr(&s_umask[h][cx], 1ull << k);
         }
     }
     __syncthreads();
     const int nL = F.n_lights;
     const float ind = F.indirect;
-    const bool fixed_l = kRtThreads % nL == 0;
-    const int my_l = threadIdx.x % nL, r_first = threadIdx.x / nL, r_stride = kRtThreads / nL;
+    const bool fixed_l = 64 % nL == 0;
+    const int my_l = lane % nL, r_stride = kRtThreads / nL;
     const RtLight my_light = F.lights[my_l];
-    // folding lanes: wave 3, lane = 24 k + 3 pr + comp (k = 0: the pixel whose
-    // first or middle column this is, k = 1: the pixel whose last column it is)
-    const bool folder = wave == 3 && lane < 48;
+    // folding lanes: lane = 24 k + 3 pr + comp (k = 0: the pixel whose first
+    // or middle column this is, k = 1: the pixel whose last column it is)
     const int fk = lane / 24, fpr = (lane % 24) / 3, fcomp = lane % 3;
     for (int h = 0; h * kLatHalfH < G.nv; ++h) {
         const int pr0 = h * kLatHalfH, npr = min(kLatHalfH, G.nv - pr0);
         const int lr0 = 2 * pr0, nlr = 2 * npr + 1, items = nlr * nL;
         for (int step = 0; step <= cols; ++step) {
+            // roles rotate over the waves step by step (logical wave lw): the
+            // wave with lw = 0 takes the odd 17th row, lw = 3 also folds, so
+            // every SIMD of the CU carries the same load over a sweep
+            const int lw = (wave + step) & 3, lt = lw * 64 + lane;
+            const bool folder = lw == 3 && lane < 48;
             if (step < cols) {   // DirectLight of column `step`, every light (:151-153, :366-415)
                 const int cx = step;
                 const unsigned long long um = uniform_u64(s_umask[h][cx]);
@@ -888,22 +949,16 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
                     if (bi == INT_MIN) return;
                     const float Y = 0.5f * (float)(ay0 + cy), t = hq.x;
                     const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                    const vec3 r3 = v3(Lt.x, Lt.y, Lt.z) - pos;                   // :370
-                    const float rmag = light_rmag(r3);                            // :371
-                    const vec3 normal = hit_normal(s_shade, sph, bi, pos);        // :377-387
-                    const vec3 origin = pos + normal * 0.00001f;                  // :394
-                    vec3 dl = v3(0.0f, 0.0f, 0.0f);
-                    if (!shadowed<true>(Fs, tc, sph, origin, r3, rmag, um))       // :394-398
-                        dl = direct_light_lit(Lt, r3, rmag, normal, object_colour(s_shade, sph, bi));
-                    float *b = &s_dl[step & 1][r][0][l];
-                    b[0] = dl.x;
-                    b[kLatMaxLights] = dl.y;
-                    b[2 * kLatMaxLights] = dl.z;
+                    const vec3 dl = lat_direct_light(Fs, tc, sph, s_obj, Lt, bi, pos, um);
+                    float *b = &s_dl[step & 1][r][0][0];
+                    b[l ^ lat_swz(r, 0)] = dl.x;
+                    b[kLatMaxLights + (l ^ lat_swz(r, 1))] = dl.y;
+                    b[2 * kLatMaxLights + (l ^ lat_swz(r, 2))] = dl.z;
                 };
-                if (fixed_l) {   // nL divides 256: each thread keeps one light (in registers)
-                    for (int r = r_first; r < nlr; r += r_stride) item(r, my_l, my_light);
+                if (fixed_l) {   // nL divides 64: each thread keeps one light (in registers)
+                    for (int r = lt / nL; r < nlr; r += r_stride) item(r, my_l, my_light);
                 } else {
-                    for (int it = threadIdx.x; it < items; it += kRtThreads) {
+                    for (int it = lt; it < items; it += kRtThreads) {
                         const int r = it / nL, l = it - r * nL;
                         item(r, l, F.lights[l]);
                     }
@@ -924,16 +979,17 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
                         if (bi == INT_MIN) continue;
                         valid = true;
                         const float *b = buf + (r * 3 + fcomp) * kLatMaxLights;
+                        const int sw = lat_swz(r, fcomp);
                         int l = 0;
-                        for (; l + 4 <= nL; l += 4) {
-                            const float4 v = *(const float4 *)(b + l);
+                        for (; l + 4 <= nL; l += 4) {   // lights l .. l + 3, in order
+                            const float4 v = *(const float4 *)(b + (l ^ sw));
                             pc = pc + v.x;
                             pc = pc + v.y;
                             pc = pc + v.z;
                             pc = pc + v.w;
                         }
-                        for (; l < nL; ++l) pc = pc + b[l];
-                        const vec3 oc = object_colour(s_shade, sph, bi);          // :147-148
+                        for (; l < nL; ++l) pc = pc + b[l ^ sw];
+                        const vec3 oc = lat_colour(s_obj, bi);                    // :147-148
                         const float a = fcomp == 0 ? oc.x : (fcomp == 1 ? oc.y : oc.z);
                         pc = pc + (a * ind);                                      // :156
                     }
@@ -1164,8 +1220,8 @@ static bool rt_lattice_ok(const RtFrame &F)
 // caller has rt_prepare_kernel certify its tiles first).
 bool rt_use_lattice(const RtFrame &F)
 {
-    return F.n_tris > 0 && F.n_tris <= 62 && F.cull_primary && F.n_lights >= 1 && F.n_lights <= kLatMaxLights &&
-           rt_lattice_ok(F);
+    return F.n_tris > 0 && F.n_tris <= 62 && F.n_sph <= kLatMaxSph && F.cull_primary && F.n_lights >= 1 &&
+           F.n_lights <= kLatMaxLights && rt_lattice_ok(F);
 }
 
 size_t rt_lattice_tiles(const RtFrame &F)
