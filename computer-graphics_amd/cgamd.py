@@ -131,6 +131,18 @@ _SIGS = {
     "cg_rast_draw": (C.c_int, [P, C.POINTER(RastParams), P, P, P, C.POINTER(Stats)]),
     "cg_rast_draw_device": (C.c_int, [P, C.POINTER(RastParams), P, P, P, P]),
     "cg_rast_draw_frames_device": (C.c_int, [P, C.POINTER(RastParams), C.c_int, P, P, P, C.c_size_t, P]),
+    "cg_dist_unique_id": (C.c_int, [P]),
+    "cg_dist_create": (C.c_int, [P, C.c_int, C.c_int, P, C.POINTER(P)]),
+    "cg_dist_create_local": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(P)]),
+    "cg_dist_destroy": (None, [P]),
+    "cg_dist_set_bands": (C.c_int, [P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "cg_dist_get_bands": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "cg_dist_set_chunk": (C.c_int, [P, C.c_int]),
+    "cg_dist_rebalance": (C.c_int, [P]),
+    "cg_dist_last_times": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "cg_rt_render_frames_dist": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int, P,
+                                           C.c_size_t, P]),
+    "cg_dist_band_partition": (C.c_int, [P, C.c_int, C.c_int, P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "cg_image_jpeg_info": (C.c_int, [P, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "cg_image_jpeg_check": (C.c_int, [P, C.c_size_t]),
     "cg_image_decode_jpeg": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
@@ -333,6 +345,91 @@ def jpeg_info(data: bytes):
     if lib.cg_image_jpeg_info(buf.ctypes.data_as(P), buf.size, C.byref(w), C.byref(h), C.byref(ch)) != 0:
         raise ValueError("not a supported JPEG")
     return w.value, h.value, ch.value
+
+DIST_ID_BYTES = 128   # cg_dist_id (an RCCL unique id)
+
+
+def dist_unique_id() -> bytes:
+    """cg_dist_unique_id: rank 0 creates the id every rank passes to Dist."""
+    buf = (C.c_char * DIST_ID_BYTES)()
+    rc = load().cg_dist_unique_id(buf)
+    if rc != CG_OK:
+        raise RuntimeError(f"cg_dist_unique_id failed with {rc}")
+    return bytes(buf.raw)
+
+
+def band_partition_native(row_cost, nranks, overhead=None):
+    """cg_dist_band_partition (host-only): [(row0, rows)] per rank."""
+    c = np.ascontiguousarray(row_cost, dtype=np.float64)
+    o = None if overhead is None else np.ascontiguousarray(overhead, dtype=np.float64)
+    r0, rs = (C.c_int * nranks)(), (C.c_int * nranks)()
+    rc = load().cg_dist_band_partition(c.ctypes.data_as(P), len(c), nranks, o.ctypes.data_as(P) if o is not None
+                                       else None, r0, rs)
+    if rc != CG_OK:
+        raise RuntimeError(f"cg_dist_band_partition failed with {rc}")
+    return [(r0[r], rs[r]) for r in range(nranks)]
+
+
+class Dist:
+    """Multi-GPU raytracer frames (cg_dist_*): one rank's handle.  Dist(ctx,
+    nranks, rank, id) joins an RCCL communicator; Dist.local(ctxs) builds an
+    in-process group (tests) and returns one handle per rank."""
+
+    def __init__(self, ctx, nranks=1, rank=0, uid: bytes = None, _handle=None):
+        self.ctx, self.lib, self.nranks, self.rank = ctx, ctx.lib, nranks, rank
+        if _handle is not None:
+            self.h = _handle
+            return
+        h = P()
+        idb = (C.c_char * DIST_ID_BYTES).from_buffer_copy(uid)
+        ctx._check(self.lib.cg_dist_create(ctx.h, nranks, rank, idb, C.byref(h)), "cg_dist_create")
+        self.h = h
+
+    @classmethod
+    def local(cls, ctxs):
+        n = len(ctxs)
+        hs, outs = (P * n)(*[c.h for c in ctxs]), (P * n)()
+        ctxs[0]._check(ctxs[0].lib.cg_dist_create_local(hs, n, outs), "cg_dist_create_local")
+        return [cls(ctxs[r], n, r, _handle=P(outs[r])) for r in range(n)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cg_dist_destroy(self.h)
+            self.h = None
+
+    def set_bands(self, height, bands):
+        r0 = (C.c_int * self.nranks)(*[b[0] for b in bands])
+        rs = (C.c_int * self.nranks)(*[b[1] for b in bands])
+        self.ctx._check(self.lib.cg_dist_set_bands(self.h, height, r0, rs), "cg_dist_set_bands")
+
+    def bands(self):
+        r0, rs = (C.c_int * self.nranks)(), (C.c_int * self.nranks)()
+        rc = self.lib.cg_dist_get_bands(self.h, r0, rs)
+        if rc < 0:
+            return None
+        return [(r0[r], rs[r]) for r in range(self.nranks)]
+
+    def set_chunk(self, frames):
+        self.ctx._check(self.lib.cg_dist_set_chunk(self.h, frames), "cg_dist_set_chunk")
+
+    def rebalance(self):
+        self.ctx._check(self.lib.cg_dist_rebalance(self.h), "cg_dist_rebalance")
+
+    def last_times(self):
+        """(render ms per frame, assembly ms per frame) of this rank's last call."""
+        a, b = C.c_double(), C.c_double()
+        self.ctx._check(self.lib.cg_dist_last_times(self.h, C.byref(a), C.byref(b)), "cg_dist_last_times")
+        return a.value, b.value
+
+    def render_frames(self, cams, d_frames, stream=None, lights=None, frame_stride=0):
+        """cg_rt_render_frames_dist: len(cams) frames, assembled on rank 0 at d_frames."""
+        lights = default_lights() if lights is None else lights
+        arr = (RtCamera * len(cams))(*cams)
+        self.ctx._check(self.lib.cg_rt_render_frames_dist(self.h, lights, len(lights), arr, len(cams),
+                                                          P(d_frames) if d_frames else None, frame_stride,
+                                                          P(stream) if stream else None),
+                        "cg_rt_render_frames_dist")
+
 
 class Context:
     """One GPU context (cg_create/cg_destroy)."""

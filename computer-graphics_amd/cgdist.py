@@ -1,5 +1,9 @@
-"""Multi-GPU raytracer sharding: framebuffer stripes dealt
-round-robin over ranks, one gather to rank 0, one unstripe kernel.
+"""Multi-GPU raytracer sharding.  The product path is native:
+cg_rt_render_frames_dist (csrc/cg_dist.hip: balanced bands, RCCL p2p to rank
+0, in-place assembly); join() below sets it up over a torch.distributed
+world.  This module also keeps the earlier stripe layout (framebuffer
+stripes dealt round-robin over ranks, one gather to rank 0, one unstripe
+kernel) and numpy mirrors of the partition / assembly logic for CPU tests.
 
 Pixels are independent in the reference's Draw (raytracer/Source/
 skeleton.cpp:123-168), so there is no data-path exchange while rendering:
@@ -100,6 +104,27 @@ def rebalance(bands, render_s, overhead_s, height: int):
         if n > 0:
             cost[r0:r0 + n] = max(float(t), 1e-12) / n
     return band_partition(cost, len(bands), overhead_s)
+
+
+def join(ctx, group=None, chunk=None):
+    """This process's cgamd.Dist in the torch.distributed world (one process
+    per GPU): rank 0 creates the RCCL id (cg_dist_unique_id) and it travels
+    over the existing process group; cg_dist_create then joins the library's
+    own RCCL communicator on ctx's device."""
+    import torch
+    import torch.distributed as dist
+
+    import cgamd
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.zeros(cgamd.DIST_ID_BYTES, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        t.copy_(torch.tensor(list(cgamd.dist_unique_id()), dtype=torch.uint8))
+    dist.broadcast(t, src=0, group=group)
+    d = cgamd.Dist(ctx, world, rank, bytes(t.cpu().tolist()))
+    if chunk:
+        d.set_chunk(chunk)
+    return d
 
 
 def pack_rgb24_np(argb: np.ndarray) -> np.ndarray:

@@ -1,0 +1,569 @@
+// cg_dist.hip -- multi-GPU raytracer frames, one process per GPU.
+//
+// The reference's Draw (raytracer/Source/skeleton.cpp:104-169) renders every
+// pixel independently on one CPU thread, so the frame shards by rows with no
+// exchange while rendering.  Rank r renders the contiguous band of frame
+// rows [row0_r, row0_r + rows_r); ranks > 0 render it in the RGB24 wire
+// format (PutPixelSDL's alpha is constant) and only in the columns the camera
+// can see anything in (cg_rt_frame_columns: the rest is certainly black), and
+// send it to rank 0 with one RCCL point-to-point send per chunk of frames --
+// on MI355X every peer has its own xGMI link to rank 0, so the sends run in
+// parallel; rank 0 renders its own band straight into the caller's frames and
+// expands the received bands in place (rt_assemble_kernel).  A call's frames
+// go in chunks through two buffer slots, so the transfer of chunk j (on the
+// transfer stream) overlaps the render of chunk j + 1 (on the caller's
+// stream).  Band boundaries come from measured per-rank times
+// (cg_dist_rebalance): the row cost of the Cornell box is far from uniform
+// (tiles that certainly miss everything exit at once, the floor and boxes
+// cost most).
+//
+// Transports: RCCL (cg_dist_create) or, for tests, an in-process group of
+// contexts whose bands move by device-to-device copies (cg_dist_create_local).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cg_internal.h"
+
+namespace cg {
+int ctx_device(const cg_ctx *c);
+hipStream_t ctx_stream(const cg_ctx *c);
+void ctx_set_error(cg_ctx *c, const std::string &e);
+void ctx_rt_columns(const cg_ctx *c, const cg_rt_camera *cam, int *c0, int *c1);
+}  // namespace cg
+
+using namespace cg;
+
+namespace {
+
+constexpr int kBandAlign = kLatTileH;   // default band boundaries: whole lattice tile rows
+
+struct Mem {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n)
+    {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    ~Mem()
+    {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct TimedPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    int frames = 0;
+};
+
+struct LocalGroup;
+
+}  // namespace
+
+struct cg_dist {
+    cg_ctx *ctx = nullptr;
+    int nranks = 1, rank = 0;
+    ncclComm_t comm = nullptr;        // RCCL transport
+    LocalGroup *group = nullptr;      // in-process transport (tests)
+    hipStream_t xs = nullptr;         // transfer stream
+    int height = 0;                   // frame height the bands are for
+    std::vector<int> row0, rows;      // band of every rank
+    int chunk = 4;                    // frames per chunk
+    Mem sbuf[2], rbuf[2];             // send (ranks > 0) / receive (rank 0) slots
+    Mem sall;                         // local transport: a peer's whole call
+    hipEvent_t ev_rend[2] = {}, ev_sent[2] = {}, ev_recv[2] = {}, ev_asm[2] = {}, ev_done = nullptr;
+    std::vector<hipEvent_t> ev_chunk; // local transport: a peer's chunk j rendered
+    std::vector<TimedPair> t_rend, t_asm;   // timing of the last call (reused event pool)
+    size_t n_rend = 0, n_asm = 0;
+    Mem stats;                        // rebalance: gathered per-rank times (device)
+    int last_pitch = 0;               // local transport: the peer's window pitch of its last call
+    size_t last_frames = 0;
+};
+
+namespace {
+
+struct LocalGroup {
+    std::vector<cg_dist *> members;
+};
+
+int fail(cg_dist *d, int code, const std::string &what)
+{
+    if (d && d->ctx) ctx_set_error(d->ctx, what);
+    return code;
+}
+#define DT(d, call, what)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) return fail((d), CG_E_HIP, std::string(what) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define DN(d, call, what)                                                                              \
+    do {                                                                                               \
+        ncclResult_t r_ = (call);                                                                      \
+        if (r_ != ncclSuccess) return fail((d), CG_E_HIP, std::string(what) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+void equal_bands(int H, int n, std::vector<int> &row0, std::vector<int> &rows)
+{
+    const int units = (H + kBandAlign - 1) / kBandAlign;
+    row0.assign(n, 0);
+    rows.assign(n, 0);
+    for (int r = 0; r < n; ++r) {
+        const int a = std::min(H, (int)((long long)units * r / n) * kBandAlign);
+        const int b = r + 1 == n ? H : std::min(H, (int)((long long)units * (r + 1) / n) * kBandAlign);
+        row0[r] = a;
+        rows[r] = b - a;
+    }
+}
+
+// Bisection on the makespan T with a greedy sweep (cgdist.band_partition).
+void band_partition(const double *cost, int H, int n, const double *ovh, int *row0, int *rows)
+{
+    std::vector<double> C(H + 1, 0.0), o(n, 0.0);
+    for (int i = 0; i < H; ++i) C[i + 1] = C[i] + cost[i];
+    if (ovh)
+        for (int r = 0; r < n; ++r) o[r] = ovh[r];
+    auto sweep = [&](double T, std::vector<int> &b) {
+        b.assign(1, 0);
+        for (int r = 0; r < n - 1; ++r) {
+            const int lo = b.back(), left = n - 1 - r;
+            const int hi_max = H >= n ? std::max(lo + 1, H - left) : lo + (lo < H ? 1 : 0);
+            // largest end with cost <= T (at least one row, leaving one per later rank)
+            const double target = C[lo] + T - o[r];
+            int end = (int)(std::upper_bound(C.begin(), C.end(), target) - C.begin()) - 1;
+            end = std::min(std::max(end, lo < H ? lo + 1 : lo), hi_max);
+            b.push_back(end);
+        }
+        b.push_back(H);
+    };
+    double lo_T = 0.0, hi_T = C[H] + *std::max_element(o.begin(), o.end()) + 1.0;
+    std::vector<int> b;
+    for (int it = 0; it < 60; ++it) {
+        const double T = 0.5 * (lo_T + hi_T);
+        sweep(T, b);
+        const double last = C[b[n]] - C[b[n - 1]] + o[n - 1];
+        if (last <= T) hi_T = T;
+        else lo_T = T;
+    }
+    sweep(hi_T, b);
+    for (int r = 0; r < n; ++r) {
+        row0[r] = b[r];
+        rows[r] = b[r + 1] - b[r];
+    }
+}
+
+int ensure_events(cg_dist *d)
+{
+    if (d->ev_done) return CG_OK;
+    DT(d, hipSetDevice(ctx_device(d->ctx)), "hipSetDevice");
+    DT(d, hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking), "transfer stream");
+    for (int k = 0; k < 2; ++k) {
+        DT(d, hipEventCreateWithFlags(&d->ev_rend[k], hipEventDisableTiming), "event");
+        DT(d, hipEventCreateWithFlags(&d->ev_sent[k], hipEventDisableTiming), "event");
+        DT(d, hipEventCreateWithFlags(&d->ev_recv[k], hipEventDisableTiming), "event");
+        DT(d, hipEventCreateWithFlags(&d->ev_asm[k], hipEventDisableTiming), "event");
+        // recorded once so the first waits on them are satisfied
+        DT(d, hipEventRecord(d->ev_sent[k], d->xs), "event");
+        DT(d, hipEventRecord(d->ev_asm[k], d->xs), "event");
+    }
+    DT(d, hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming), "event");
+    return CG_OK;
+}
+
+// the next timing pair of a pool (events created on first use)
+int timed(cg_dist *d, std::vector<TimedPair> &pool, size_t &n, TimedPair *&out)
+{
+    if (n == pool.size()) {
+        TimedPair t;
+        DT(d, hipEventCreate(&t.a), "event");
+        DT(d, hipEventCreate(&t.b), "event");
+        pool.push_back(t);
+    }
+    out = &pool[n++];
+    return CG_OK;
+}
+
+double pool_ms_per_frame(const std::vector<TimedPair> &pool, size_t n)
+{
+    double ms = 0.0;
+    int f = 0;
+    for (size_t i = 0; i < n; ++i) {
+        float m = 0.f;
+        if (hipEventSynchronize(pool[i].b) == hipSuccess && hipEventElapsedTime(&m, pool[i].a, pool[i].b) == hipSuccess)
+            ms += m;
+        f += pool[i].frames;
+    }
+    return f ? ms / f : 0.0;
+}
+
+// The columns whose pixels ranks > 0 send: the union of every camera's window.
+void call_window(const cg_dist *d, const cg_rt_camera *cams, int n, int &c0, int &cols)
+{
+    const int W = cams[0].width;
+    int a = W, b = 0;
+    for (int f = 0; f < n; ++f) {
+        int x0, x1;
+        ctx_rt_columns(d->ctx, &cams[f], &x0, &x1);
+        a = std::min(a, x0);
+        b = std::max(b, x1);
+    }
+    if (b <= a) {   // nothing visible anywhere: keep a minimal window
+        a = 0;
+        b = std::min(W, 16);
+    }
+    if ((a == 0 && b == W) || (b - a) % 4) {
+        c0 = 0;
+        cols = 0;   // whole rows (the assembly needs a 4-aligned window)
+    } else {
+        c0 = a;
+        cols = b - a;
+    }
+}
+
+int render_band(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int nf, int r0, int nr,
+                int c0, int cols, void *dst, size_t stride, int fmt, hipStream_t st)
+{
+    cg_rt_shard sh{0, 1, kLatTileH, r0, nr, fmt == CG_PIX_RGB24 ? c0 : 0, fmt == CG_PIX_RGB24 ? cols : 0};
+    TimedPair *t;
+    int rc = timed(d, d->t_rend, d->n_rend, t);
+    if (rc) return rc;
+    t->frames = nf;
+    DT(d, hipEventRecord(t->a, st), "event");
+    rc = cg_rt_render_frames_device(d->ctx, lights, n_lights, cams, nf, &sh, dst, stride, fmt, st);
+    if (rc) return rc;
+    DT(d, hipEventRecord(t->b, st), "event");
+    return CG_OK;
+}
+
+}  // namespace
+
+extern "C" int cg_dist_unique_id(cg_dist_id *id)
+{
+    if (!id) return CG_E_INVALID;
+    static_assert(sizeof(cg_dist_id) == sizeof(ncclUniqueId), "cg_dist_id must hold an ncclUniqueId");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return CG_E_HIP;
+    std::memcpy(id->bytes, u.internal, sizeof(u.internal));
+    return CG_OK;
+}
+
+extern "C" int cg_dist_create(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, cg_dist **out)
+{
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return CG_E_INVALID;
+    *out = nullptr;
+    cg_dist *d = new cg_dist;
+    d->ctx = ctx;
+    d->nranks = nranks;
+    d->rank = rank;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id->bytes, sizeof(u.internal));
+    if (hipSetDevice(ctx_device(ctx)) != hipSuccess) {
+        delete d;
+        return fail(nullptr, CG_E_HIP, "hipSetDevice");
+    }
+    const ncclResult_t r = ncclCommInitRank(&d->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        ctx_set_error(ctx, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        delete d;
+        return CG_E_HIP;
+    }
+    *out = d;
+    return CG_OK;
+}
+
+extern "C" int cg_dist_create_local(cg_ctx *const *ctxs, int nranks, cg_dist **outs)
+{
+    if (!ctxs || !outs || nranks < 1) return CG_E_INVALID;
+    for (int r = 0; r < nranks; ++r)
+        if (!ctxs[r]) return CG_E_INVALID;
+    LocalGroup *g = new LocalGroup;
+    for (int r = 0; r < nranks; ++r) {
+        cg_dist *d = new cg_dist;
+        d->ctx = ctxs[r];
+        d->nranks = nranks;
+        d->rank = r;
+        d->group = g;
+        g->members.push_back(d);
+        outs[r] = d;
+    }
+    return CG_OK;
+}
+
+extern "C" void cg_dist_destroy(cg_dist *d)
+{
+    if (!d) return;
+    (void)hipSetDevice(ctx_device(d->ctx));
+    if (d->xs) (void)hipStreamSynchronize(d->xs);
+    if (d->comm) (void)ncclCommDestroy(d->comm);
+    for (int k = 0; k < 2; ++k)
+        for (hipEvent_t e : {d->ev_rend[k], d->ev_sent[k], d->ev_recv[k], d->ev_asm[k]})
+            if (e) (void)hipEventDestroy(e);
+    if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+    for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
+    for (auto *pool : {&d->t_rend, &d->t_asm})
+        for (TimedPair &t : *pool) {
+            (void)hipEventDestroy(t.a);
+            (void)hipEventDestroy(t.b);
+        }
+    if (d->xs) (void)hipStreamDestroy(d->xs);
+    if (d->group) {   // the last member frees the group
+        auto &m = d->group->members;
+        m.erase(std::remove(m.begin(), m.end(), d), m.end());
+        if (m.empty()) delete d->group;
+    }
+    delete d;
+}
+
+extern "C" int cg_dist_set_bands(cg_dist *d, int height, const int *row0, const int *rows)
+{
+    if (!d || height <= 0 || !row0 || !rows) return CG_E_INVALID;
+    int next = 0;
+    for (int r = 0; r < d->nranks; ++r) {
+        if (row0[r] != next || rows[r] < 0) return CG_E_INVALID;
+        next += rows[r];
+    }
+    if (next != height) return CG_E_INVALID;
+    d->height = height;
+    d->row0.assign(row0, row0 + d->nranks);
+    d->rows.assign(rows, rows + d->nranks);
+    return CG_OK;
+}
+
+extern "C" int cg_dist_get_bands(const cg_dist *d, int *row0, int *rows)
+{
+    if (!d || !row0 || !rows) return CG_E_INVALID;
+    if (d->row0.empty()) return CG_E_INVALID;
+    std::copy(d->row0.begin(), d->row0.end(), row0);
+    std::copy(d->rows.begin(), d->rows.end(), rows);
+    return d->height;
+}
+
+extern "C" int cg_dist_set_chunk(cg_dist *d, int frames)
+{
+    if (!d || frames < 1) return CG_E_INVALID;
+    d->chunk = frames;
+    return CG_OK;
+}
+
+extern "C" int cg_dist_last_times(cg_dist *d, double *render_ms_per_frame, double *assemble_ms_per_frame)
+{
+    if (!d) return CG_E_INVALID;
+    if (render_ms_per_frame) *render_ms_per_frame = pool_ms_per_frame(d->t_rend, d->n_rend);
+    if (assemble_ms_per_frame) *assemble_ms_per_frame = pool_ms_per_frame(d->t_asm, d->n_asm);
+    return CG_OK;
+}
+
+extern "C" int cg_dist_band_partition(const double *row_cost, int height, int nranks, const double *overhead,
+                                      int *row0, int *rows)
+{
+    if (!row_cost || height < 0 || nranks < 1 || !row0 || !rows) return CG_E_INVALID;
+    band_partition(row_cost, height, nranks, overhead, row0, rows);
+    return CG_OK;
+}
+
+// New bands from per-rank (render ms/frame, fixed ms/frame) pairs t[2 r], t[2 r + 1].
+static void rebalance_bands(cg_dist *d, const double *t)
+{
+    const int n = d->nranks, H = d->height;
+    std::vector<double> cost(H, 0.0), ovh(n);
+    for (int r = 0; r < n; ++r) {
+        for (int y = d->row0[r]; y < d->row0[r] + d->rows[r]; ++y) cost[y] = std::max(t[2 * r], 1e-12) / d->rows[r];
+        ovh[r] = t[2 * r + 1];
+    }
+    std::vector<int> a(n), b(n);
+    band_partition(cost.data(), H, n, ovh.data(), a.data(), b.data());
+    d->row0 = a;
+    d->rows = b;
+}
+
+extern "C" int cg_dist_rebalance(cg_dist *d)
+{
+    if (!d) return CG_E_INVALID;
+    if (d->height <= 0 || d->nranks == 1) return CG_OK;
+    const int n = d->nranks;
+    if (d->group) {   // every member's last call is enqueued: gather directly
+        if (d->rank != 0) return CG_OK;   // rank 0 rebalances the whole group
+        std::vector<double> t(2 * n);
+        for (cg_dist *m : d->group->members) {
+            t[2 * m->rank] = pool_ms_per_frame(m->t_rend, m->n_rend);
+            t[2 * m->rank + 1] = pool_ms_per_frame(m->t_asm, m->n_asm);
+        }
+        rebalance_bands(d, t.data());
+        for (cg_dist *m : d->group->members) {
+            m->height = d->height;
+            m->row0 = d->row0;
+            m->rows = d->rows;
+        }
+        return CG_OK;
+    }
+    int rc = ensure_events(d);
+    if (rc) return rc;
+    const double mine[2] = {pool_ms_per_frame(d->t_rend, d->n_rend), pool_ms_per_frame(d->t_asm, d->n_asm)};
+    DT(d, d->stats.ensure((size_t)(2 * n + 2) * sizeof(double) + (size_t)2 * n * sizeof(int)), "alloc stats");
+    double *dt = (double *)d->stats.p;
+    int *dband = (int *)(dt + 2 * n + 2);
+    DT(d, hipMemcpyAsync(dt + 2 * n, mine, sizeof(mine), hipMemcpyHostToDevice, d->xs), "stats upload");
+    DN(d, ncclAllGather(dt + 2 * n, dt, 2, ncclFloat64, d->comm, d->xs), "ncclAllGather");
+    std::vector<double> t(2 * n);
+    DT(d, hipMemcpyAsync(t.data(), dt, 2 * n * sizeof(double), hipMemcpyDeviceToHost, d->xs), "stats download");
+    DT(d, hipStreamSynchronize(d->xs), "stats sync");
+    // rank 0 decides; every rank adopts its boundaries
+    std::vector<int> band(2 * n);
+    if (d->rank == 0) {
+        rebalance_bands(d, t.data());
+        for (int r = 0; r < n; ++r) {
+            band[2 * r] = d->row0[r];
+            band[2 * r + 1] = d->rows[r];
+        }
+        DT(d, hipMemcpyAsync(dband, band.data(), band.size() * sizeof(int), hipMemcpyHostToDevice, d->xs), "bands");
+    }
+    DN(d, ncclBroadcast(dband, dband, 2 * n, ncclInt32, 0, d->comm, d->xs), "ncclBroadcast");
+    DT(d, hipMemcpyAsync(band.data(), dband, band.size() * sizeof(int), hipMemcpyDeviceToHost, d->xs), "bands");
+    DT(d, hipStreamSynchronize(d->xs), "bands sync");
+    for (int r = 0; r < n; ++r) {
+        d->row0[r] = band[2 * r];
+        d->rows[r] = band[2 * r + 1];
+    }
+    return CG_OK;
+}
+
+extern "C" int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
+                                        int n_frames, uint32_t *d_frames, size_t frame_stride, void *stream)
+{
+    if (!d || n_frames < 0 || (n_frames && !cams)) return CG_E_INVALID;
+    if (n_frames == 0) return CG_OK;
+    const int W = cams[0].width, H = cams[0].height;
+    if (W <= 0 || H <= 0) return CG_E_INVALID;
+    for (int f = 1; f < n_frames; ++f)
+        if (cams[f].width != W || cams[f].height != H) return CG_E_INVALID;
+    if (d->rank == 0 && !d_frames) return CG_E_INVALID;
+    if (frame_stride == 0) frame_stride = (size_t)W * H;
+    if (frame_stride < (size_t)W * H) return CG_E_INVALID;
+    int rc = ensure_events(d);
+    if (rc) return rc;
+    DT(d, hipSetDevice(ctx_device(d->ctx)), "hipSetDevice");
+    if (d->height != H || (int)d->row0.size() != d->nranks) {
+        d->height = H;
+        equal_bands(H, d->nranks, d->row0, d->rows);
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : ctx_stream(d->ctx);
+    const int n = d->nranks, me = d->rank;
+    int c0, cols;
+    call_window(d, cams, n_frames, c0, cols);
+    const int pitch = cols ? cols : W;
+    const size_t row_bytes = (size_t)pitch * 3;
+    const int C = std::max(1, std::min(d->chunk, n_frames));
+    d->n_rend = d->n_asm = 0;
+    const int r0 = d->row0[me], nr = d->rows[me];
+    if (d->group && me > 0) {
+        // local transport: the whole call's band in one buffer, chunk events
+        // for rank 0's copies (no slot reuse: rank 0's call comes later)
+        const int chunks = (n_frames + C - 1) / C;
+        DT(d, d->sall.ensure(std::max<size_t>(1, (size_t)n_frames * nr * row_bytes)), "alloc band");
+        while ((int)d->ev_chunk.size() < chunks) {
+            hipEvent_t e;
+            DT(d, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+            d->ev_chunk.push_back(e);
+        }
+        for (int j = 0; j < chunks; ++j) {
+            const int f0 = j * C, nf = std::min(C, n_frames - f0);
+            if (nr > 0) {
+                rc = render_band(d, lights, n_lights, cams + f0, nf, r0, nr, c0, cols,
+                                 (uint8_t *)d->sall.p + (size_t)f0 * nr * row_bytes, (size_t)nr * pitch, CG_PIX_RGB24,
+                                 st);
+                if (rc) return rc;
+            }
+            DT(d, hipEventRecord(d->ev_chunk[j], st), "event");
+        }
+        d->last_pitch = pitch;
+        d->last_frames = n_frames;
+        return CG_OK;
+    }
+    for (int f0 = 0, j = 0; f0 < n_frames; f0 += C, ++j) {
+        const int nf = std::min(C, n_frames - f0), s = j & 1;
+        if (me == 0) {
+            // own band straight into the frames (ARGB)
+            if (nr > 0) {
+                rc = render_band(d, lights, n_lights, cams + f0, nf, r0, nr, 0, 0,
+                                 d_frames + (size_t)f0 * frame_stride + (size_t)r0 * W, frame_stride, CG_PIX_ARGB8888,
+                                 st);
+                if (rc) return rc;
+            }
+            if (n == 1) continue;
+            size_t total = 0;
+            for (int p = 1; p < n; ++p) total += (size_t)nf * d->rows[p] * row_bytes;
+            DT(d, d->rbuf[s].ensure(std::max<size_t>(total, 1)), "alloc receive buffer");
+            // the slot was last read by the assembly of chunk j - 2
+            DT(d, hipStreamWaitEvent(d->xs, d->ev_asm[s], 0), "wait");
+            uint8_t *rb = (uint8_t *)d->rbuf[s].p;
+            if (d->group) {
+                size_t off = 0;
+                for (int p = 1; p < n; ++p) {
+                    const cg_dist *m = d->group->members[p];
+                    const size_t bytes = (size_t)nf * d->rows[p] * row_bytes;
+                    if (m->last_frames != (size_t)n_frames || m->last_pitch != pitch || (int)m->ev_chunk.size() <= j)
+                        return fail(d, CG_E_INVALID, "local transport: ranks > 0 must render this call first");
+                    DT(d, hipStreamWaitEvent(d->xs, m->ev_chunk[j], 0), "wait");
+                    if (bytes)
+                        DT(d, hipMemcpyAsync(rb + off, (const uint8_t *)m->sall.p + (size_t)f0 * d->rows[p] * row_bytes,
+                                             bytes, hipMemcpyDeviceToDevice, d->xs), "band copy");
+                    off += bytes;
+                }
+            } else {
+                DN(d, ncclGroupStart(), "ncclGroupStart");
+                size_t off = 0;
+                for (int p = 1; p < n; ++p) {
+                    const size_t bytes = (size_t)nf * d->rows[p] * row_bytes;
+                    if (bytes) DN(d, ncclRecv(rb + off, bytes, ncclUint8, p, d->comm, d->xs), "ncclRecv");
+                    off += bytes;
+                }
+                DN(d, ncclGroupEnd(), "ncclGroupEnd");
+            }
+            DT(d, hipEventRecord(d->ev_recv[s], d->xs), "event");
+            // assembly of the received bands on the render stream
+            DT(d, hipStreamWaitEvent(st, d->ev_recv[s], 0), "wait");
+            std::vector<int> br0(n - 1), brows(n - 1);
+            for (int p = 1; p < n; ++p) {
+                br0[p - 1] = d->row0[p];
+                brows[p - 1] = d->rows[p];
+            }
+            TimedPair *t;
+            rc = timed(d, d->t_asm, d->n_asm, t);
+            if (rc) return rc;
+            t->frames = nf;
+            DT(d, hipEventRecord(t->a, st), "event");
+            rc = cg_rt_assemble_device(d->ctx, rb, CG_PIX_RGB24, br0.data(), brows.data(), n - 1, W, H, nf,
+                                       d_frames + (size_t)f0 * frame_stride, frame_stride, cols ? c0 : 0, cols, st);
+            if (rc) return rc;
+            DT(d, hipEventRecord(t->b, st), "event");
+            DT(d, hipEventRecord(d->ev_asm[s], st), "event");
+        } else {
+            const size_t bytes = (size_t)nf * nr * row_bytes;
+            DT(d, d->sbuf[s].ensure(std::max<size_t>(bytes, 1)), "alloc send buffer");
+            // the slot was last read by the send of chunk j - 2
+            DT(d, hipStreamWaitEvent(st, d->ev_sent[s], 0), "wait");
+            if (nr > 0) {
+                rc = render_band(d, lights, n_lights, cams + f0, nf, r0, nr, c0, cols, d->sbuf[s].p, (size_t)nr * pitch,
+                                 CG_PIX_RGB24, st);
+                if (rc) return rc;
+            }
+            DT(d, hipEventRecord(d->ev_rend[s], st), "event");
+            DT(d, hipStreamWaitEvent(d->xs, d->ev_rend[s], 0), "wait");
+            if (bytes) DN(d, ncclSend(d->sbuf[s].p, bytes, ncclUint8, 0, d->comm, d->xs), "ncclSend");
+            DT(d, hipEventRecord(d->ev_sent[s], d->xs), "event");
+        }
+    }
+    // the caller's stream covers the transfers too
+    DT(d, hipEventRecord(d->ev_done, d->xs), "event");
+    DT(d, hipStreamWaitEvent(st, d->ev_done, 0), "wait");
+    return CG_OK;
+}

@@ -90,6 +90,8 @@ struct cg_ctx {
     int slot = 0;
     DevBuf ptc[2], pshade[2], plat[2], psup[2];
     RtGrid grid{};                      // large scenes only (n_tris > 64)
+    std::vector<cg_tri> tris_host;      // the scene as uploaded (cg_dist's column window)
+    std::vector<cg_sphere> sph_host;
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
@@ -112,6 +114,21 @@ struct cg_ctx {
 };
 
 namespace cg {
+// exposed to cg_dist.hip
+int ctx_device(const cg_ctx *c) { return c->device; }
+hipStream_t ctx_stream(const cg_ctx *c) { return c->stream; }
+void ctx_set_error(cg_ctx *c, const std::string &e) { c->err = e; }
+// cg_rt_frame_columns over the context's scene (the full width without one)
+void ctx_rt_columns(const cg_ctx *c, const cg_rt_camera *cam, int *c0, int *c1)
+{
+    *c0 = 0;
+    *c1 = cam->width;
+    if (c->n_tris < 0 || cg_rt_frame_columns(c->tris_host.data(), (int)c->tris_host.size(), c->sph_host.data(),
+                                             (int)c->sph_host.size(), cam, c0, c1) != CG_OK) {
+        *c0 = 0;
+        *c1 = cam->width;
+    }
+}
 // exposed to cg_rast.hip
 void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
 {
@@ -274,6 +291,8 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     if (n_spheres)
         CG_TRY(c, hipMemcpyAsync(c->sph.p, S.data(), S.size() * sizeof(RtSphere),
                                  hipMemcpyHostToDevice, c->stream), "upload spheres");
+    c->tris_host.assign(tris, tris + n_tris);
+    c->sph_host.assign(spheres, spheres + n_spheres);
     c->grid = RtGrid{};
     if (n_tris > 64) {   // large scene: grid for the shadow-ray blocker search
         std::vector<int> gs, gt;

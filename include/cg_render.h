@@ -201,6 +201,56 @@ int cg_rt_probe_closest(cg_ctx *ctx, const cg_vec4 *starts, const cg_vec4 *dirs,
 int cg_rt_probe_direct_light(cg_ctx *ctx, const cg_isect *isects, const cg_light *light, int n,
                              cg_vec3 *out);
 
+/* ---- multi-GPU raytracer ------------------------------- */
+/* One process per GPU.  The reference renders every pixel of Draw
+ * (raytracer/Source/skeleton.cpp:104-169) on one CPU thread; pixels are
+ * independent, so N GPUs each render one contiguous band of frame rows and
+ * rank 0 assembles the frames: ranks > 0 render their band in CG_PIX_RGB24
+ * (only the columns the camera can see anything in, cg_rt_frame_columns) and
+ * send it to rank 0 with RCCL point-to-point over xGMI (every peer has its own
+ * link to rank 0); rank 0 renders its own band straight into the frames and
+ * expands the received bands in place (cg_rt_assemble_device).  Frames are
+ * processed in chunks: the transfer of chunk j overlaps the render of chunk
+ * j + 1.  A cg_dist is bound to one context and is not thread-safe. */
+typedef struct cg_dist cg_dist;
+typedef struct { char bytes[128]; } cg_dist_id;    /* an RCCL unique id (ncclUniqueId) */
+/* Rank 0 creates the id and hands it to every rank (MPI, sockets, ...). */
+int cg_dist_unique_id(cg_dist_id *id);
+/* Collective over the nranks processes: RCCL communicator on ctx's device. */
+int cg_dist_create(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, cg_dist **out);
+/* In-process transport for tests: nranks contexts (any devices, possibly one)
+ * in one process and thread, one cg_dist per rank in outs[]; bands move by
+ * device-to-device copies.  Each render call must be made on ranks
+ * nranks-1 .. 1 before rank 0 (their work is only enqueued). */
+int cg_dist_create_local(cg_ctx *const *ctxs, int nranks, cg_dist **outs);
+void cg_dist_destroy(cg_dist *d);
+/* Band partition: rank r renders rows row0[r] .. row0[r] + rows[r] - 1; the
+ * bands must tile [0, height) in rank order.  Default (and after a height
+ * change): equal bands on multiples of 15 rows (the lattice tile height). */
+int cg_dist_set_bands(cg_dist *d, int height, const int *row0, const int *rows);
+int cg_dist_get_bands(const cg_dist *d, int *row0, int *rows);
+/* Frames per chunk of the render/transfer pipeline (default 4). */
+int cg_dist_set_chunk(cg_dist *d, int frames);
+/* Collective: new bands from every rank's measured render time per frame in
+ * its last cg_rt_render_frames_dist call (cost density uniform within each
+ * old band; rank 0 also pays the assembly), so the bands take equal time. */
+int cg_dist_rebalance(cg_dist *d);
+/* This rank's device time per frame in its last cg_rt_render_frames_dist
+ * call (waits for it): its band's render and, on rank 0, the assembly. */
+int cg_dist_last_times(cg_dist *d, double *render_ms_per_frame, double *assemble_ms_per_frame);
+/* Collective: n_frames frames (cams as cg_rt_render_frames_device; one size),
+ * assembled on rank 0 into d_frames + f * frame_stride pixels (ARGB8888;
+ * frame_stride 0 = W*H).  d_frames is ignored on ranks > 0.  Enqueued on
+ * `stream` (NULL: the context's); when `stream` has drained, rank 0's frames
+ * are complete. */
+int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
+                             int n_frames, uint32_t *d_frames, size_t frame_stride, void *stream);
+/* Host-only: contiguous bands minimising max_r (sum of row_cost over band r
+ * + overhead[r]) (overhead may be NULL); every rank gets >= 1 row when
+ * height >= nranks. */
+int cg_dist_band_partition(const double *row_cost, int height, int nranks, const double *overhead, int *row0,
+                           int *rows);
+
 /* ---- rasteriser ------------------------------------------------------- */
 /* glibc rand() as colour modes 1-2 consume it (seed 1, never reseeded by the
  * reference): n values starting at call index `offset`.  Host-only probe of

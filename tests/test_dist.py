@@ -162,3 +162,19 @@ def test_rgb24_pack_assemble_roundtrip():
                           for a, n in bands for f in range(nf)])
     got = cgdist.assemble_np(src, 3, bands, Wd, Hd, nf, np.zeros_like(frames_ref))
     assert np.array_equal(got, frames_ref)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_native_band_partition_matches_python(nranks):
+    """cg_dist_band_partition (the library's rebalance) == cgdist.band_partition."""
+    import cgamd
+    rng = np.random.default_rng(nranks)
+    for H in (1, 5, 64, 1080):
+        for _ in range(5):
+            cost = rng.random(H) * rng.choice([0.0, 1.0], H, p=[0.3, 0.7])
+            ovh = rng.random(nranks) * cost.sum() / nranks * 0.3
+            for o in (None, ovh):
+                want = cgdist.band_partition(cost, nranks, o)
+                got = cgamd.band_partition_native(cost, nranks, o)
+                assert got == want, (H, nranks, got, want)
+                assert sum(n for _, n in got) == H and got[0][0] == 0

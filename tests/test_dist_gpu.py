@@ -1,0 +1,138 @@
+"""GPU: the library's multi-GPU raytracer (cg_rt_render_frames_dist,
+csrc/cg_dist.hip) assembles on rank 0 exactly the frames one GPU renders.
+
+Ranks run in one process through the in-process transport
+(cg_dist_create_local: N contexts on cuda:0, bands moved by device copies --
+the same band, window, chunk and assembly logic as the RCCL transport), and
+the RCCL transport itself with one rank.  Frames are compared bit for bit
+with cg_rt_render_frames_device on a single context, itself pinned to the
+oracle by tests/test_rt_gpu.py."""
+import numpy as np
+import pytest
+import torch
+
+import cgamd
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctxs(n, scene=None):
+    out = []
+    for _ in range(n):
+        c = cgamd.Context(0)
+        tris, nt, sph = scene or cgamd.rt_scene()
+        c.rt_set_scene(tris, nt, sph, 1 if sph is not None else 0)
+        out.append(c)
+    return out
+
+
+def _single(ctx, cams, lights):
+    W, H = cams[0].width, cams[0].height
+    buf = torch.zeros(len(cams) * W * H, dtype=torch.int32, device="cuda")
+    ctx.rt_render_frames_device(cams, buf.data_ptr(), lights=lights, frame_stride=W * H)
+    torch.cuda.synchronize()
+    return buf.cpu().numpy().view(np.uint32).reshape(len(cams), H * W)
+
+
+def _dist_render(ds, cams, lights):
+    W, H = cams[0].width, cams[0].height
+    frames = torch.zeros(len(cams) * W * H, dtype=torch.int32, device="cuda")
+    for d in reversed(ds):                 # ranks > 0 enqueue first (local transport)
+        d.render_frames(cams, frames.data_ptr() if d.rank == 0 else None, lights=lights)
+    torch.cuda.synchronize()
+    return frames.cpu().numpy().view(np.uint32).reshape(len(cams), H * W)
+
+
+def _cams(W, H, f, n, R=None):
+    # the camera moves from frame to frame (the reference's Update(), skeleton.cpp:195-252)
+    return [cgamd.rt_camera(W, H, f, (0.01 * k, -0.005 * k, -3.0 + 0.02 * k, 1.0), R) for k in range(n)]
+
+
+@pytest.mark.parametrize("nranks,chunk", [(2, 4), (3, 1), (8, 3)])
+def test_dist_local_matches_single_gpu(nranks, chunk):
+    W, H = 320, 256
+    cams = _cams(W, H, 256.0, 7)
+    lights = cgamd.default_lights()
+    ctxs = _ctxs(nranks)
+    ds = cgamd.Dist.local(ctxs)
+    try:
+        for d in ds:
+            d.set_chunk(chunk)
+        want = _single(ctxs[0], cams, lights)
+        got = _dist_render(ds, cams, lights)
+        assert np.array_equal(got, want)
+        bands = ds[0].bands()
+        assert bands[0][0] == 0 and sum(n for _, n in bands) == H
+        # uneven bands (one rank empty) and a rebalance from the measured times
+        if nranks >= 3:
+            rows = [(H - 100) * (r + 1) // (nranks - 2) - (H - 100) * r // (nranks - 2) for r in range(nranks - 2)]
+            b = [(0, 100), (100, 0)] + [(100 + (H - 100) * r // (nranks - 2), rows[r]) for r in range(nranks - 2)]
+            for d in ds:
+                d.set_bands(H, b)
+            assert np.array_equal(_dist_render(ds, cams, lights), want)
+        ds[0].rebalance()
+        nb = ds[0].bands()
+        assert all(d.bands() == nb for d in ds) and sum(n for _, n in nb) == H
+        assert np.array_equal(_dist_render(ds, cams, lights), want)
+        r, a = ds[0].last_times()
+        assert r > 0 and (a > 0 or nranks == 1)
+    finally:
+        for d in ds:
+            d.close()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("kind", ["c4", "yaw"])
+def test_dist_local_light_set_and_rotated_camera(kind):
+    """The light-set lattice kernel (C4's 8x8 area light) and the general
+    kernel (yawed camera: full-width rows, pack pass) through the bands."""
+    W, H = 240, 120   # whole frames: a multiple of the 8-row tile (no padding rows)
+    if kind == "c4":
+        cams, lights = _cams(W, H, 135.0, 3), cgamd.area_lights(None, 0.1, 8)
+    else:
+        cams, lights = _cams(W, H, 135.0, 3, cgamd.yaw_matrix(0.1745)), cgamd.default_lights()
+    ctxs = _ctxs(4)
+    ds = cgamd.Dist.local(ctxs)
+    try:
+        want = _single(ctxs[0], cams, lights)
+        assert np.array_equal(_dist_render(ds, cams, lights), want)
+    finally:
+        for d in ds:
+            d.close()
+        for c in ctxs:
+            c.close()
+
+
+def test_dist_rccl_one_rank():
+    """The RCCL transport with one rank: own id, communicator, frames."""
+    W, H = 320, 256
+    cams = _cams(W, H, 256.0, 5)
+    (ctx,) = _ctxs(1)
+    d = cgamd.Dist(ctx, 1, 0, cgamd.dist_unique_id())
+    try:
+        want = _single(ctx, cams, cgamd.default_lights())
+        got = _dist_render([d], cams, cgamd.default_lights())
+        assert np.array_equal(got, want)
+        d.rebalance()
+    finally:
+        d.close()
+        ctx.close()
+
+
+def test_dist_errors():
+    ctxs = _ctxs(2)
+    ds = cgamd.Dist.local(ctxs)
+    try:
+        with pytest.raises(RuntimeError):
+            ds[0].set_bands(100, [(0, 60), (50, 50)])      # overlapping
+        with pytest.raises(RuntimeError):
+            ds[0].set_chunk(0)
+        with pytest.raises(RuntimeError):                  # rank 0 before its peer (local transport)
+            ds[0].render_frames(_cams(64, 48, 48.0, 2), torch.zeros(2 * 64 * 48, dtype=torch.int32,
+                                                                    device="cuda").data_ptr())
+    finally:
+        for d in ds:
+            d.close()
+        for c in ctxs:
+            c.close()
