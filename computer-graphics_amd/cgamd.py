@@ -138,6 +138,7 @@ _SIGS = {
     "cg_dist_set_bands": (C.c_int, [P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "cg_dist_get_bands": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "cg_dist_set_chunk": (C.c_int, [P, C.c_int]),
+    "cg_dist_set_pipeline": (C.c_int, [P, C.c_int]),
     "cg_dist_rebalance": (C.c_int, [P]),
     "cg_dist_last_times": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "cg_rt_render_frames_dist": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int, P,
@@ -347,6 +348,7 @@ def jpeg_info(data: bytes):
     return w.value, h.value, ch.value
 
 DIST_ID_BYTES = 128   # cg_dist_id (an RCCL unique id)
+DIST_SIGNALLED, DIST_CHUNKED = 0, 1   # cg_dist_set_pipeline
 
 
 def dist_unique_id() -> bytes:
@@ -411,6 +413,10 @@ class Dist:
 
     def set_chunk(self, frames):
         self.ctx._check(self.lib.cg_dist_set_chunk(self.h, frames), "cg_dist_set_chunk")
+
+    def set_pipeline(self, mode):
+        """DIST_SIGNALLED / DIST_CHUNKED (cg_dist_set_pipeline)."""
+        self.ctx._check(self.lib.cg_dist_set_pipeline(self.h, mode), "cg_dist_set_pipeline")
 
     def rebalance(self):
         self.ctx._check(self.lib.cg_dist_rebalance(self.h), "cg_dist_rebalance")

@@ -9,10 +9,15 @@
 // send it to rank 0 with one RCCL point-to-point send per chunk of frames --
 // on MI355X every peer has its own xGMI link to rank 0, so the sends run in
 // parallel; rank 0 renders its own band straight into the caller's frames and
-// expands the received bands in place (rt_assemble_kernel).  A call's frames
-// go in chunks through two buffer slots, so the transfer of chunk j (on the
-// transfer stream) overlaps the render of chunk j + 1 (on the caller's
-// stream).  Band boundaries come from measured per-rank times
+// expands the received bands in place (rt_assemble_kernel).  The transfer of
+// a chunk of frames (on the transfer stream) overlaps the render of the later
+// frames (on the caller's stream): by default (CG_DIST_SIGNALLED) a call's
+// frames render in full-size lattice launches that count each frame's stored
+// tiles in uncached device memory, and the transfer stream waits on those
+// counts (hipStreamWaitValue32) before sending a chunk -- small per-chunk
+// launches would lose ~15-25 % to launch tails, more so on a 1/8 band;
+// CG_DIST_CHUNKED instead launches chunk by chunk through two buffer slots
+// ordered by events.  Band boundaries come from measured per-rank times
 // (cg_dist_rebalance): the row cost of the Cornell box is far from uniform
 // (tiles that certainly miss everything exit at once, the floor and boxes
 // cost most).
@@ -30,6 +35,9 @@
 #include "cg_internal.h"
 
 namespace cg {
+int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
+                     const cg_rt_shard *shard, void *d_out, size_t frame_stride, int pix_format, void *stream,
+                     uint32_t *d_done, uint32_t *target);
 int ctx_device(const cg_ctx *c);
 hipStream_t ctx_stream(const cg_ctx *c);
 void ctx_set_error(cg_ctx *c, const std::string &e);
@@ -88,6 +96,16 @@ struct cg_dist {
     Mem stats;                        // rebalance: gathered per-rank times (device)
     int last_pitch = 0;               // local transport: the peer's window pitch of its last call
     size_t last_frames = 0;
+    // Signalled pipeline (when the device supports stream waits on memory):
+    // a call renders all its frames in one launch and the transfer stream
+    // waits on per-frame completion counts (rt_render_frames' d_done).
+    bool signals = false;
+    unsigned calls = 0;               // call parity selects the slot below
+    uint32_t *done[2] = {nullptr, nullptr};
+    size_t done_cap[2] = {0, 0};
+    std::vector<uint32_t> target[2];
+    hipEvent_t ev_call[2] = {};       // ranks > 0: slot free again (its sends / copies done)
+    int cur = 0;                      // slot of the last call
 };
 
 namespace {
@@ -176,6 +194,13 @@ int ensure_events(cg_dist *d)
         DT(d, hipEventRecord(d->ev_asm[k], d->xs), "event");
     }
     DT(d, hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming), "event");
+    for (int k = 0; k < 2; ++k) {
+        DT(d, hipEventCreateWithFlags(&d->ev_call[k], hipEventDisableTiming), "event");
+        DT(d, hipEventRecord(d->ev_call[k], d->xs), "event");
+    }
+    int wait_value = 0;
+    d->signals = hipDeviceGetAttribute(&wait_value, hipDeviceAttributeCanUseStreamWaitValue, ctx_device(d->ctx)) ==
+                     hipSuccess && wait_value != 0;
     return CG_OK;
 }
 
@@ -230,7 +255,8 @@ void call_window(const cg_dist *d, const cg_rt_camera *cams, int n, int &c0, int
 }
 
 int render_band(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int nf, int r0, int nr,
-                int c0, int cols, void *dst, size_t stride, int fmt, hipStream_t st)
+                int c0, int cols, void *dst, size_t stride, int fmt, hipStream_t st, uint32_t *d_done = nullptr,
+                uint32_t *target = nullptr)
 {
     cg_rt_shard sh{0, 1, kLatTileH, r0, nr, fmt == CG_PIX_RGB24 ? c0 : 0, fmt == CG_PIX_RGB24 ? cols : 0};
     TimedPair *t;
@@ -238,7 +264,7 @@ int render_band(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_ca
     if (rc) return rc;
     t->frames = nf;
     DT(d, hipEventRecord(t->a, st), "event");
-    rc = cg_rt_render_frames_device(d->ctx, lights, n_lights, cams, nf, &sh, dst, stride, fmt, st);
+    rc = rt_render_frames(d->ctx, lights, n_lights, cams, nf, &sh, dst, stride, fmt, st, d_done, target);
     if (rc) return rc;
     DT(d, hipEventRecord(t->b, st), "event");
     return CG_OK;
@@ -308,6 +334,10 @@ extern "C" void cg_dist_destroy(cg_dist *d)
         for (hipEvent_t e : {d->ev_rend[k], d->ev_sent[k], d->ev_recv[k], d->ev_asm[k]})
             if (e) (void)hipEventDestroy(e);
     if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+    for (int k = 0; k < 2; ++k) {
+        if (d->ev_call[k]) (void)hipEventDestroy(d->ev_call[k]);
+        if (d->done[k]) (void)hipFree(d->done[k]);
+    }
     for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
     for (auto *pool : {&d->t_rend, &d->t_asm})
         for (TimedPair &t : *pool) {
@@ -345,6 +375,16 @@ extern "C" int cg_dist_get_bands(const cg_dist *d, int *row0, int *rows)
     std::copy(d->row0.begin(), d->row0.end(), row0);
     std::copy(d->rows.begin(), d->rows.end(), rows);
     return d->height;
+}
+
+extern "C" int cg_dist_set_pipeline(cg_dist *d, int mode)
+{
+    if (!d || (mode != CG_DIST_SIGNALLED && mode != CG_DIST_CHUNKED)) return CG_E_INVALID;
+    int rc = ensure_events(d);
+    if (rc) return rc;
+    if (mode == CG_DIST_CHUNKED) d->signals = false;
+    else if (!d->signals) return fail(d, CG_E_INVALID, "stream waits on memory are not supported on this device");
+    return CG_OK;
 }
 
 extern "C" int cg_dist_set_chunk(cg_dist *d, int frames)
@@ -436,6 +476,132 @@ extern "C" int cg_dist_rebalance(cg_dist *d)
     return CG_OK;
 }
 
+// One call, signalled: every rank renders its band for all the call's frames
+// in one render call (one lattice launch per 32 frames: full-size launches
+// even for a 1/8 band); ranks > 0 render into the call's send slot and their
+// transfer stream sends each chunk as soon as its frames' tiles are all
+// stored (hipStreamWaitValue32 on the per-frame counts), while later frames
+// are still rendering; rank 0 receives and assembles chunk by chunk on its
+// transfer stream, beside its own band's render.
+static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
+                            uint32_t *d_frames, size_t frame_stride, hipStream_t st, int c0, int cols)
+{
+    const int n = d->nranks, me = d->rank, W = cams[0].width, H = cams[0].height;
+    const int pitch = cols ? cols : W;
+    const size_t row_bytes = (size_t)pitch * 3;
+    const int C = std::max(1, std::min(d->chunk, n_frames));
+    const int r0 = d->row0[me], nr = d->rows[me];
+    const int s = (int)(d->calls++ & 1u);
+    d->cur = s;
+    int rc;
+    if (me > 0) {
+        // the slot's previous reader: this rank's sends (RCCL) or rank 0's
+        // copies (local transport) of the call two calls ago
+        hipEvent_t prev = d->group ? d->group->members[0]->ev_call[s] : d->ev_call[s];
+        if (prev) DT(d, hipStreamWaitEvent(st, prev, 0), "wait");
+        const size_t bytes = (size_t)n_frames * nr * row_bytes;
+        Mem &out = d->sbuf[s];   // the whole call's band (rank 0 pulls from it in the local transport)
+        DT(d, out.ensure(std::max<size_t>(bytes, 1)), "alloc send buffer");
+        if (d->done_cap[s] < (size_t)n_frames) {
+            DT(d, hipStreamSynchronize(st), "sync");
+            if (d->done[s]) DT(d, hipFree(d->done[s]), "free signals");
+            d->done[s] = nullptr;
+            // uncached fine-grained device memory: the kernels' atomics land in
+            // memory, where the command processor's waits poll them
+            DT(d, hipExtMallocWithFlags((void **)&d->done[s], (size_t)n_frames * sizeof(uint32_t),
+                                        hipDeviceMallocUncached), "alloc signals");
+            d->done_cap[s] = n_frames;
+        }
+        d->target[s].assign(n_frames, 0u);
+        DT(d, hipMemsetAsync(d->done[s], 0, (size_t)n_frames * sizeof(uint32_t), st), "zero signals");
+        if (nr > 0) {
+            rc = render_band(d, lights, n_lights, cams, n_frames, r0, nr, c0, cols, out.p, (size_t)nr * pitch,
+                             CG_PIX_RGB24, st, d->done[s], d->target[s].data());
+            if (rc) return rc;
+        } else {
+            for (int f = 0; f < n_frames; ++f) d->target[s][f] = 0u;   // nothing to wait for
+        }
+        d->last_pitch = pitch;
+        d->last_frames = n_frames;
+        if (d->group) return CG_OK;   // rank 0 pulls the chunks
+        for (int f0 = 0; f0 < n_frames; f0 += C) {
+            const int nf = std::min(C, n_frames - f0);
+            for (int f = f0; f < f0 + nf; ++f)
+                if (d->target[s][f])
+                    DT(d, hipStreamWaitValue32(d->xs, d->done[s] + f, d->target[s][f], hipStreamWaitValueGte,
+                                               0xffffffffu), "wait frame");
+            const size_t cb = (size_t)nf * nr * row_bytes;
+            if (cb) DN(d, ncclSend((uint8_t *)out.p + (size_t)f0 * nr * row_bytes, cb, ncclUint8, 0, d->comm, d->xs),
+                       "ncclSend");
+        }
+        DT(d, hipEventRecord(d->ev_call[s], d->xs), "event");
+        return CG_OK;
+    }
+    // rank 0: own band straight into the frames (ARGB), on the caller's stream
+    if (nr > 0) {
+        rc = render_band(d, lights, n_lights, cams, n_frames, r0, nr, 0, 0, d_frames + (size_t)r0 * W, frame_stride,
+                         CG_PIX_ARGB8888, st);
+        if (rc) return rc;
+    }
+    if (n > 1) {
+        size_t per_frame = 0;
+        for (int p = 1; p < n; ++p) per_frame += (size_t)d->rows[p] * row_bytes;
+        DT(d, d->rbuf[0].ensure(std::max<size_t>((size_t)n_frames * per_frame, 1)), "alloc receive buffer");
+        uint8_t *rb = (uint8_t *)d->rbuf[0].p;
+        std::vector<int> br0(n - 1), brows(n - 1);
+        for (int p = 1; p < n; ++p) {
+            br0[p - 1] = d->row0[p];
+            brows[p - 1] = d->rows[p];
+        }
+        for (int f0 = 0; f0 < n_frames; f0 += C) {
+            const int nf = std::min(C, n_frames - f0);
+            uint8_t *cb = rb + (size_t)f0 * per_frame;   // blocks of this chunk, peers in order
+            size_t off = 0;
+            if (d->group) {
+                for (int p = 1; p < n; ++p) {
+                    const cg_dist *m = d->group->members[p];
+                    const size_t bytes = (size_t)nf * d->rows[p] * row_bytes;
+                    if (m->last_frames != (size_t)n_frames || m->last_pitch != pitch || m->cur != s ||
+                        m->calls != d->calls)
+                        return fail(d, CG_E_INVALID, "local transport: ranks > 0 must render this call first");
+                    for (int f = f0; f < f0 + nf; ++f)
+                        if (m->target[s][f])
+                            DT(d, hipStreamWaitValue32(d->xs, m->done[s] + f, m->target[s][f],
+                                                       hipStreamWaitValueGte, 0xffffffffu), "wait frame");
+                    if (bytes)
+                        DT(d, hipMemcpyAsync(cb + off, (const uint8_t *)m->sbuf[s].p + (size_t)f0 * d->rows[p] * row_bytes,
+                                             bytes, hipMemcpyDeviceToDevice, d->xs), "band copy");
+                    off += bytes;
+                }
+            } else {
+                DN(d, ncclGroupStart(), "ncclGroupStart");
+                for (int p = 1; p < n; ++p) {
+                    const size_t bytes = (size_t)nf * d->rows[p] * row_bytes;
+                    if (bytes) DN(d, ncclRecv(cb + off, bytes, ncclUint8, p, d->comm, d->xs), "ncclRecv");
+                    off += bytes;
+                }
+                DN(d, ncclGroupEnd(), "ncclGroupEnd");
+            }
+            // assembly of the chunk on the transfer stream (rows disjoint from
+            // the render's own band)
+            TimedPair *t;
+            rc = timed(d, d->t_asm, d->n_asm, t);
+            if (rc) return rc;
+            t->frames = nf;
+            DT(d, hipEventRecord(t->a, d->xs), "event");
+            rc = cg_rt_assemble_device(d->ctx, cb, CG_PIX_RGB24, br0.data(), brows.data(), n - 1, W, H, nf,
+                                       d_frames + (size_t)f0 * frame_stride, frame_stride, cols ? c0 : 0, cols, d->xs);
+            if (rc) return rc;
+            DT(d, hipEventRecord(t->b, d->xs), "event");
+        }
+        // local transport: the peers' slot s is free once these copies ran
+        DT(d, hipEventRecord(d->ev_call[s], d->xs), "event");
+    }
+    DT(d, hipEventRecord(d->ev_done, d->xs), "event");
+    DT(d, hipStreamWaitEvent(st, d->ev_done, 0), "wait");
+    return CG_OK;
+}
+
 extern "C" int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
                                         int n_frames, uint32_t *d_frames, size_t frame_stride, void *stream)
 {
@@ -464,6 +630,8 @@ extern "C" int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int 
     const int C = std::max(1, std::min(d->chunk, n_frames));
     d->n_rend = d->n_asm = 0;
     const int r0 = d->row0[me], nr = d->rows[me];
+    if (d->signals)
+        return render_signalled(d, lights, n_lights, cams, n_frames, d_frames, frame_stride, st, c0, cols);
     if (d->group && me > 0) {
         // local transport: the whole call's band in one buffer, chunk events
         // for rank 0's copies (no slot reuse: rank 0's call comes later)

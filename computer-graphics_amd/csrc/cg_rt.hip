@@ -675,12 +675,10 @@ __device__ __forceinline__ void lat_store_black(const RtFrame &F, const LatTile 
 // blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
 // tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
 // out + frame * out_stride.
-__global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtFrame F0, const RtTri *__restrict__ tc,
-                                                                  const RtShade *__restrict__ shade,
-                                                                  const RtSphere *__restrict__ sph,
-                                                                  const unsigned long long *__restrict__ lat_masks,
-                                                                  RtFrameCams cams, size_t out_stride,
-                                                                  uint32_t *__restrict__ out)
+__device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__restrict__ tc,
+                                             const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
+                                             const unsigned long long *__restrict__ lat_masks, const RtFrameCams &cams,
+                                             size_t out_stride, uint32_t *__restrict__ out)
 {
     const int frame = blockIdx.z;
     RtFrame F = F0;
@@ -814,12 +812,12 @@ constexpr int kLatMaxLights = 64;
 // lights contiguous and in order, so one ds_read_b128 still yields l .. l + 3.
 __device__ __forceinline__ int lat_swz(int r, int c) { return 4 * ((r * 3 + c) & 15); }
 
-__global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
-                                                                          const RtShade *__restrict__ shade,
-                                                                          const RtSphere *__restrict__ sph,
-                                                                          const unsigned long long *__restrict__ lat_masks,
-                                                                          RtFrameCams cams, size_t out_stride,
-                                                                          uint32_t *__restrict__ out)
+__device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtTri *__restrict__ tc,
+                                                    const RtShade *__restrict__ shade,
+                                                    const RtSphere *__restrict__ sph,
+                                                    const unsigned long long *__restrict__ lat_masks,
+                                                    const RtFrameCams &cams, size_t out_stride,
+                                                    uint32_t *__restrict__ out)
 {
     const int frame = blockIdx.z;
     RtFrame F = F0;
@@ -1007,6 +1005,43 @@ __global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFram
         px = s_valid[ty][tx] ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
     }
     lat_store(F, G, o, px, tx, ty, (uint32_t *)&s_dl[0][0][0][0]);
+}
+
+// The kernels.  frame_done (optional, cg_dist's transfer pipeline): when a
+// workgroup's tile is stored, frame_done[frame] counts it -- every wave first
+// writes its stores back (__threadfence: agent-scope release, L2 write-back
+// across the XCDs), then one lane adds -- so a stream that waits for a
+// frame's count to reach its tile count (hipStreamWaitValue32) may read the
+// frame while the launch is still rendering later frames.
+__device__ __forceinline__ void lat_signal(uint32_t *frame_done, int frame)
+{
+    if (!frame_done) return;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&frame_done[frame], 1u);
+}
+
+__global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+                                                                  const RtShade *__restrict__ shade,
+                                                                  const RtSphere *__restrict__ sph,
+                                                                  const unsigned long long *__restrict__ lat_masks,
+                                                                  RtFrameCams cams, size_t out_stride,
+                                                                  uint32_t *__restrict__ out, uint32_t *frame_done)
+{
+    lattice_body(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
+    lat_signal(frame_done, blockIdx.z);
+}
+
+__global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+                                                                          const RtShade *__restrict__ shade,
+                                                                          const RtSphere *__restrict__ sph,
+                                                                          const unsigned long long *__restrict__ lat_masks,
+                                                                          RtFrameCams cams, size_t out_stride,
+                                                                          uint32_t *__restrict__ out,
+                                                                          uint32_t *frame_done)
+{
+    lattice_lights_body(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
+    lat_signal(frame_done, blockIdx.z);
 }
 
 // ARGB8888 -> RGB24 wire format (kernels without a fused RGB24 store): rows
@@ -1234,15 +1269,15 @@ size_t rt_lattice_tiles(const RtFrame &F)
 hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
                                     const RtSphere *d_sph, const unsigned long long *d_lat_masks,
                                     const RtFrameCams &cams, int nframes, size_t out_stride, uint32_t *d_out,
-                                    hipStream_t st)
+                                    hipStream_t st, uint32_t *d_done)
 {
     const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     if (F.n_lights == 1)
         hipLaunchKernelGGL(rt_lattice_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
-                           cams, out_stride, d_out);
+                           cams, out_stride, d_out, d_done);
     else
         hipLaunchKernelGGL(rt_lattice_lights_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                           d_lat_masks, cams, out_stride, d_out);
+                           d_lat_masks, cams, out_stride, d_out, d_done);
     return hipGetLastError();
 }
 
@@ -1254,7 +1289,7 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
     if (d_lat_masks && rt_use_lattice(F)) {
         RtFrameCams cams{};
         for (int c = 0; c < 4; ++c) cams.c[0][c] = F.cam[c];
-        return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, 0, d_out, st);
+        return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, 0, d_out, st, nullptr);
     } else if (F.n_tris <= 64 && F.cull_primary)
         hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);

@@ -20,7 +20,7 @@ hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTr
 size_t rt_sup_units(const RtFrame &);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                     const unsigned long long *, const RtFrameCams &, int, size_t, uint32_t *,
-                                    hipStream_t);
+                                    hipStream_t, uint32_t *);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             const unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
@@ -488,7 +488,7 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 // Frames f0 .. f0 + nf - 1 of a batch, one prepare + one lattice launch
 // (rt_use_lattice(F) holds for every frame; they differ only in cameraPos).
 static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
-                                    void *d_out, size_t stride, hipStream_t st)
+                                    void *d_out, size_t stride, hipStream_t st, uint32_t *d_done)
 {
     if (!c->aux) {
         CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
@@ -524,7 +524,8 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
     CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
-                                       (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st),
+                                       (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st,
+                                       d_done),
            "rt_lattice launch");
     CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
     return CG_OK;
@@ -532,9 +533,28 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
 
 static size_t pix_bytes(int fmt) { return fmt == CG_PIX_RGB24 ? 3 : 4; }
 
+namespace cg {
+int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
+                     const cg_rt_shard *shard, void *d_out, size_t frame_stride, int pix_format, void *stream,
+                     uint32_t *d_done, uint32_t *target);
+}
+
 extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int n_lights,
                                           const cg_rt_camera *cams, int n_frames, const cg_rt_shard *shard,
                                           void *d_out, size_t frame_stride, int pix_format, void *stream)
+{
+    return rt_render_frames(c, lights, n_lights, cams, n_frames, shard, d_out, frame_stride, pix_format, stream,
+                            nullptr, nullptr);
+}
+
+namespace cg {
+// cg_rt_render_frames_device, plus per-frame completion signals for cg_dist:
+// with d_done (signal memory, zeroed by the caller), frame f is complete once
+// d_done[f] >= target[f] (the lattice kernels count the frame's tiles as they
+// are stored; other paths write 1 after the frame's kernels).
+int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
+                     const cg_rt_shard *shard, void *d_out, size_t frame_stride, int pix_format, void *stream,
+                     uint32_t *d_done, uint32_t *target)
 {
     if (!c || !d_out || n_frames < 0 || (n_frames && !cams)) return CG_E_INVALID;
     if (pix_format != CG_PIX_ARGB8888 && pix_format != CG_PIX_RGB24) return CG_E_INVALID;
@@ -567,16 +587,24 @@ extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int
             }
             rc = rt_enqueue(c, F, out + (size_t)f * fbytes, st);
             if (rc) return rc;
+            if (d_done) {
+                CG_TRY(c, hipStreamWriteValue32(st, d_done + f, 1u, 0), "frame signal");
+                target[f] = 1u;
+            }
         }
         return CG_OK;
     }
     for (int f0 = 0; f0 < n_frames; f0 += kMaxFrameBatch) {
         const int nf = std::min(kMaxFrameBatch, n_frames - f0);
-        rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, out + (size_t)f0 * fbytes, stride, st);
+        rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, out + (size_t)f0 * fbytes, stride, st,
+                                      d_done ? d_done + f0 : nullptr);
         if (rc) return rc;
+        if (d_done)
+            for (int f = f0; f < f0 + nf; ++f) target[f] = (uint32_t)rt_lattice_tiles(F);
     }
     return CG_OK;
 }
+}  // namespace cg
 
 extern "C" int cg_rt_assemble_device(cg_ctx *c, const void *d_src, int pix_format, const int *row0,
                                      const int *rows, int n_blocks, int width, int height, int n_frames,

@@ -231,6 +231,14 @@ int cg_dist_set_bands(cg_dist *d, int height, const int *row0, const int *rows);
 int cg_dist_get_bands(const cg_dist *d, int *row0, int *rows);
 /* Frames per chunk of the render/transfer pipeline (default 4). */
 int cg_dist_set_chunk(cg_dist *d, int frames);
+/* Pipeline: CG_DIST_SIGNALLED (the default where the device supports stream
+ * waits on memory) renders a call's frames in full-size launches and sends
+ * each chunk when its frames' tiles are all stored (per-frame completion
+ * counts); CG_DIST_CHUNKED launches each chunk separately and orders the
+ * transfers with events. */
+#define CG_DIST_SIGNALLED 0
+#define CG_DIST_CHUNKED 1
+int cg_dist_set_pipeline(cg_dist *d, int mode);
 /* Collective: new bands from every rank's measured render time per frame in
  * its last cg_rt_render_frames_dist call (cost density uniform within each
  * old band; rank 0 also pays the assembly), so the bands take equal time. */

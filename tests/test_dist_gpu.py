@@ -48,8 +48,9 @@ def _cams(W, H, f, n, R=None):
     return [cgamd.rt_camera(W, H, f, (0.01 * k, -0.005 * k, -3.0 + 0.02 * k, 1.0), R) for k in range(n)]
 
 
+@pytest.mark.parametrize("pipeline", [cgamd.DIST_SIGNALLED, cgamd.DIST_CHUNKED])
 @pytest.mark.parametrize("nranks,chunk", [(2, 4), (3, 1), (8, 3)])
-def test_dist_local_matches_single_gpu(nranks, chunk):
+def test_dist_local_matches_single_gpu(nranks, chunk, pipeline):
     W, H = 320, 256
     cams = _cams(W, H, 256.0, 7)
     lights = cgamd.default_lights()
@@ -58,6 +59,7 @@ def test_dist_local_matches_single_gpu(nranks, chunk):
     try:
         for d in ds:
             d.set_chunk(chunk)
+            d.set_pipeline(pipeline)
         want = _single(ctxs[0], cams, lights)
         got = _dist_render(ds, cams, lights)
         assert np.array_equal(got, want)
@@ -128,6 +130,8 @@ def test_dist_errors():
             ds[0].set_bands(100, [(0, 60), (50, 50)])      # overlapping
         with pytest.raises(RuntimeError):
             ds[0].set_chunk(0)
+        with pytest.raises(RuntimeError):
+            ds[0].set_pipeline(7)
         with pytest.raises(RuntimeError):                  # rank 0 before its peer (local transport)
             ds[0].render_frames(_cams(64, 48, 48.0, 2), torch.zeros(2 * 64 * 48, dtype=torch.int32,
                                                                     device="cuda").data_ptr())
