@@ -1,12 +1,16 @@
-"""Per-rank render time of each RT sharding on ONE GPU (multi-GPU planning).
+"""Per-rank render time of the multi-GPU band layout, measured on ONE GPU
+(planning for cg_rt_render_frames_dist; the 8-GPU run itself is the driver's).
 
-For N ranks, every rank's shard is rendered in turn on cuda:0 and timed with
-HIP events (median of `reps`); prints max/mean per layout.  Layouts:
-  stripeS  -- S-row stripes dealt round-robin (needs the unstripe kernel)
-  band     -- one contiguous band per rank (stripe_h = ceil(H/N) rounded up to
-              the kernel's tile height): the gather lands in place.
-Also times the batched unstripe kernel per frame.
-usage: python scripts/shard_balance.py [rt|c4|c5] [reps]
+For the C2 frame it measures, in steady state (calls of K frames back to
+back, so each call's certificate kernels overlap the previous lattice launch):
+  * the whole frame's time per frame;
+  * every 15-row band's time per frame (the row-cost profile);
+  * for N = 2, 4, 8: bands partitioned on that profile (cgdist.band_partition,
+    the rule cg_dist_rebalance applies), each rank's band timed on its own ->
+    max over ranks, and the render-only scaling bound whole / max.
+The gap between the sum of the 15-row bands and the whole frame is the fixed
+per-band cost (launch tails, certificates) a small shard pays.
+usage: python scripts/shard_balance.py [rt|c4] [calls]
 """
 import json
 import os
@@ -24,64 +28,46 @@ from bench import RT_WORKLOADS  # noqa: E402
 
 def main():
     wl_name = sys.argv[1] if len(sys.argv) > 1 else "rt"
-    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    calls = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     wl = RT_WORKLOADS[wl_name]
     W, H = wl["W"], wl["H"]
+    K = 32
     st = torch.cuda.Stream()
     torch.cuda.set_stream(st)
     ctx = cgamd.Context(0)
-    if wl["random"]:
-        ctx.rt_set_scene(cgamd.random_scene(wl["random"], 0x5EED), wl["random"], None, 0)
-    else:
-        t, n, s = cgamd.rt_scene()
-        ctx.rt_set_scene(t, n, s, 1)
+    t, n, s = cgamd.rt_scene()
+    ctx.rt_set_scene(t, n, s, 1)
     cam = cgamd.rt_camera(W, H, wl["F"])
     lights = cgamd.area_lights(None, *wl["area"]) if wl["area"] else cgamd.default_lights()
+    buf = torch.zeros(K * W * H, dtype=torch.int32, device="cuda")
+    cams = [cam] * K
 
-    K = int(os.environ.get("CG_BAL_FRAMES", "1"))   # frames per render call (batched launch)
-    buf = torch.zeros(K * (W * H + 64 * W), dtype=torch.int32, device="cuda")
-
-    def time_shard(shard):
-        """Device time per frame of this shard, K frames per call."""
-        def call():
-            if K == 1:
-                ctx.rt_render_device(cam, buf.data_ptr(), shard, st.cuda_stream, lights)
-            else:
-                ctx.rt_render_frames_device([cam] * K, buf.data_ptr(), shard, st.cuda_stream, lights)
-        for _ in range(3):
-            call()
-        ts = []
-        for _ in range(reps):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(st)
-            call()
-            b.record(st)
-            b.synchronize()
-            ts.append(a.elapsed_time(b))
-        return float(np.median(ts)) * 1e3 / K
-
-    tile = wl["stripe"]
-    res = {"workload": wl_name, "frames_per_call": K, "whole_us": time_shard(None)}
-    for N in (2, 4, 8):
-        band = -(-(-(-H // N)) // tile) * tile
-        for name, S in ((f"stripe{tile}", tile), ("band", band)):
-            us = [time_shard(cgamd.RtShard(r, N, S)) for r in range(N)]
-            res[f"N{N}_{name}"] = {"per_rank_us": [round(x, 1) for x in us],
-                                   "max_over_mean": max(us) / float(np.mean(us)), "max_us": max(us)}
-    # the batched unstripe kernel, per frame (K = 8 frames, N = 8)
-    N, KU, S = 8, 8, tile
-    rows = cgdist.shard_rows(H, N, S)
-    g = torch.zeros(N * KU * rows * W, dtype=torch.int32, device="cuda")
-    fr = torch.zeros(KU * H * W, dtype=torch.int32, device="cuda")
-    ts = []
-    for _ in range(reps):
+    def per_frame_us(shard):
+        for _ in range(2):
+            ctx.rt_render_frames_device(cams, buf.data_ptr(), shard, st.cuda_stream, lights)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
-        ctx.rt_unstripe_batch_device(g.data_ptr(), W, H, N, S, KU, fr.data_ptr(), st.cuda_stream)
+        for _ in range(calls):
+            ctx.rt_render_frames_device(cams, buf.data_ptr(), shard, st.cuda_stream, lights)
         b.record(st)
         b.synchronize()
-        ts.append(a.elapsed_time(b))
-    res["unstripe_us_per_frame"] = float(np.median(ts)) * 1e3 / KU
+        return a.elapsed_time(b) * 1e3 / (calls * K)
+
+    whole = per_frame_us(cgamd.RtShard(row0=0, rows=H))
+    step = cgdist.LATTICE_STRIPE
+    bands = [(r0, min(step, H - r0)) for r0 in range(0, H, step)]
+    band_us = [per_frame_us(cgamd.RtShard(row0=r0, rows=nr)) for r0, nr in bands]
+    cost = np.zeros(H)
+    for (r0, nr), u in zip(bands, band_us):
+        cost[r0:r0 + nr] = u / nr
+    res = {"workload": wl_name, "frames_per_call": K, "calls": calls, "whole_us_per_frame": whole,
+           "sum_of_15row_bands_us": float(sum(band_us)),
+           "band15_us": [round(u, 2) for u in band_us]}
+    for N in (2, 4, 8):
+        part = cgdist.band_partition(cost, N)
+        us = [per_frame_us(cgamd.RtShard(row0=r0, rows=nr)) if nr else 0.0 for r0, nr in part]
+        res[f"N{N}"] = {"bands": part, "per_rank_us": [round(x, 2) for x in us], "max_us": max(us),
+                        "render_scaling_bound": whole / max(us)}
     print(json.dumps(res), flush=True)
     ctx.close()
 
