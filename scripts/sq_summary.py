@@ -11,12 +11,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = sys.argv[1] if len(sys.argv) > 1 else "rt_lattice_kernel"
 SRC = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "sq_*", "sq_counter_collection.csv")
 SECTION = sys.argv[3] if len(sys.argv) > 3 else "rt"
+FPL = int(sys.argv[4]) if len(sys.argv) > 4 else 32     # frames per launch of the profiled kernel
 SIMDS = 256 * 4
 
 agg = collections.defaultdict(list)
 for f in sorted(glob.glob(SRC)):
     for r in csv.DictReader(open(f)):
-        if KERNEL in r["Kernel_Name"]:
+        if r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1] == KERNEL:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 c = {k: sum(v) / len(v) for k, v in agg.items()}
 cycles = c["GRBM_GUI_ACTIVE"] / 8.0
@@ -26,6 +27,7 @@ sq = {"kernel": KERNEL, "counters_per_launch": c,
       "valu_lane_ops_per_launch": c["SQ_INSTS_VALU"] * 64,
       "wave_state_frac": {"active": c["SQ_ACTIVE_INST_ANY"] / wave, "issue_stall": c["SQ_WAIT_INST_ANY"] / wave,
                           "waiting": c["SQ_WAIT_ANY"] / wave},
+      "frames_per_launch": FPL,
       "note": "valu_issue_frac = SQ_INSTS_VALU x 2 cyc / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
 path = os.path.join(ROOT, "profiles", "pmc_summary.json")
 out = json.load(open(path))
