@@ -205,32 +205,34 @@ CG_HD int clip_plane(const cg_rtri &in, int plane, const GeomParams &p, cg_rtri 
 template <class Emit>
 CG_HD int clip_dfs(const cg_rtri &root, const GeomParams &p, Emit emit)
 {
-    // Follow the modified child in registers; only extra children are
-    // stacked (with the plane they continue from), popped in LIFO order --
-    // the same pre-order as a full stack, without copying every triangle.
-    cg_rtri stack[8];
-    int plane_of[8];
-    int sp = 0, n = 0;
-    cg_rtri cur = root;
-    int pl = 1;
+    // The leaves of the clip tree in pre-order are its root-to-leaf paths in
+    // lexicographic order of their choices at the splitting planes (0 =
+    // modified child, 1 = extra child).  Bit pl of `path` is the choice at
+    // plane pl; each path is walked from the root, and the next one flips the
+    // deepest untaken split to 1 and clears the choices below it.  No stack:
+    // one triangle in registers (the device kernel runs this per thread).
+    unsigned path = 0u;
+    int n = 0;
     for (;;) {
+        cg_rtri cur = root;
+        unsigned splits = 0u;   // planes of this path where the triangle split
         bool alive = true;
-        for (; pl <= 6; ++pl) {
+        for (int pl = 1; pl <= 6; ++pl) {
             cg_rtri ch[2];
             const int k = clip_plane(cur, pl, p, ch);
             if (k == 0) { alive = false; break; }
-            cur = ch[0];
-            if (k == 2) {                  // stacked planes strictly increase: <= 6 entries
-                stack[sp] = ch[1];
-                plane_of[sp] = pl + 1;
-                ++sp;
+            if (k == 2) {
+                splits |= 1u << pl;
+                cur = (path >> pl) & 1u ? ch[1] : ch[0];
+            } else {
+                cur = ch[0];
             }
         }
         if (alive) emit(n++, cur);
-        if (sp == 0) break;
-        --sp;
-        cur = stack[sp];
-        pl = plane_of[sp];
+        const unsigned open = splits & ~path;   // splits still to take their extra branch
+        if (!open) break;
+        const int d = 31 - __builtin_clz(open);   // the deepest one
+        path = (path & ((1u << d) - 1u)) | (1u << d);
     }
     return n;
 }

@@ -23,136 +23,108 @@ GeomParams geom_params(const cg_rast_params &p)
     return g;
 }
 
-constexpr int kGeomThreads = 512;
-constexpr int kGeomWaves = kGeomThreads / 64;
-constexpr int kGeomLds = 512;      // list entries held in LDS per list (more spill to global)
+// Device geometry in two launches, both spread over the chip.  Triangles
+// never interact while clipping, and the reference's plane-by-plane list (a
+// split inserting [modified, extra] in place, skeleton.cpp:720-1673) is, per
+// input triangle in order, that triangle's own plane-by-plane list -- the
+// depth-first pre-order clip_dfs emits on the host.
+//  rast_clip_kernel     one wave per input triangle (the room, then each box
+//                       triangle and its 6 shadow-volume triangles): the
+//                       triangle's list through planes 1..6 in LDS, children
+//                       placed by a ballot scan, the survivors staged at
+//                       stage[i * kGeomMaxLeaves ..] with their count;
+//  rast_compact_kernel  one wave per input triangle again: its offset is the
+//                       sum of the earlier counts, its survivors are copied
+//                       there, the total goes to out_n.
+// Every descendant carries its input triangle's normal, colour, texture and
+// index (a split's extra triangle copies them, :838-841), so lists hold only
+// vertices.  Planes 1-4 and 6 can split (plane 5 never does): at most 32
+// survivors per input triangle.
+constexpr int kGeomMaxLeaves = 32;
 
-// A list of triangles between clip planes: only the vertices change while
-// clipping -- a split's extra triangle copies normal, colour, texture and index
-// from its parent (skeleton.cpp:838-841) -- so an entry is three vertices plus
-// the input triangle it descends from.  Entries [0, kGeomLds) live in LDS, the
-// rest in a global spill buffer (vertices + `index` = parent).
-struct GeomList {
-    float4 v0[kGeomLds], v1[kGeomLds], v2[kGeomLds];
-    int par[kGeomLds];
-};
-
-__device__ __forceinline__ void glist_put(GeomList &L, cg_rtri *spill, int i, const cg_rtri &t, int parent)
+__global__ __launch_bounds__(64) void rast_clip_kernel(GeomParams p, const cg_rtri *__restrict__ room, int n_room,
+                                                       const cg_rtri *__restrict__ boxes, int n_boxes,
+                                                       cg_rtri *__restrict__ stage, int *__restrict__ counts,
+                                                       cg_vec4 *__restrict__ out_light)
 {
-    if (i < kGeomLds) {
-        L.v0[i] = make_float4(t.v0.x, t.v0.y, t.v0.z, t.v0.w);
-        L.v1[i] = make_float4(t.v1.x, t.v1.y, t.v1.z, t.v1.w);
-        L.v2[i] = make_float4(t.v2.x, t.v2.y, t.v2.z, t.v2.w);
-        L.par[i] = parent;
-    } else {
-        cg_rtri &d = spill[i - kGeomLds];
-        d.v0 = t.v0;
-        d.v1 = t.v1;
-        d.v2 = t.v2;
-        d.index = parent;
-    }
-}
-
-__device__ __forceinline__ cg_rtri glist_get(const GeomList &L, const cg_rtri *spill, int i, int &parent)
-{
-    cg_rtri t{};
-    if (i < kGeomLds) {
-        const float4 a = L.v0[i], b = L.v1[i], c = L.v2[i];
-        t.v0 = cg_vec4{a.x, a.y, a.z, a.w};
-        t.v1 = cg_vec4{b.x, b.y, b.z, b.w};
-        t.v2 = cg_vec4{c.x, c.y, c.z, c.w};
-        parent = L.par[i];
-    } else {
-        const cg_rtri &d = spill[i - kGeomLds];
-        t.v0 = d.v0;
-        t.v1 = d.v1;
-        t.v2 = d.v2;
-        parent = d.index;
-    }
-    return t;
-}
-
-// One workgroup, breadth-first -- the reference's own order (clip() walks the
-// whole list plane by plane, a split inserting [modified, extra] in place):
-// per plane, thread i clips list entry i into 0..2 children, a wave ballot
-// scan plus an 8-entry LDS scan gives each child its slot, and the children
-// land, in order, in the next list.  Plane 1 reads the input triangles built
-// on the fly (room, then each box triangle and its 6 shadow triangles; kept in
-// `inb` for their attributes); the lists ping-pong between the two LDS lists
-// (spilling to scr0/scr1) and plane 6 writes whole triangles to `out`.
-// out_n[0] = final count, out_light = rotated camera-space light (:223).
-__global__ __launch_bounds__(kGeomThreads) void rast_geometry_kernel(
-    GeomParams p, const cg_rtri *__restrict__ room, int n_room, const cg_rtri *__restrict__ boxes,
-    int n_boxes, cg_rtri *__restrict__ out, cg_rtri *scr0, cg_rtri *scr1, cg_rtri *inb, int cap,
-    int *__restrict__ out_n, cg_vec4 *__restrict__ out_light)
-{
-    __shared__ GeomList s_list[2];
-    __shared__ int wsum[kGeomWaves];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ float4 s_v[2][kGeomMaxLeaves][3];
+    const int i = blockIdx.x, lane = threadIdx.x;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    if (threadIdx.x == 0) *out_light = C4(mat4_mul(p.R, geom_light_camera(p)));
-    int len = n_room + 7 * n_boxes;
+    if (i == 0 && lane == 0) *out_light = C4(mat4_mul(p.R, geom_light_camera(p)));
+    const cg_rtri root = geom_input(p, room, n_room, boxes, i);   // uniform over the wave
+    int len = 1;
     for (int pl = 1; pl <= 6; ++pl) {
-        const int si = pl & 1, di = si ^ 1;                 // plane 1 writes list 0
-        const cg_rtri *sspill = si ? scr1 : scr0;
-        cg_rtri *dspill = di ? scr1 : scr0;
-        int carry = 0;
-        for (int base = 0; base < len; base += kGeomThreads) {
-            const int i = base + (int)threadIdx.x;
-            cg_rtri ch[2];
-            int k = 0, parent = i;
-            if (i < len) {
-                cg_rtri t;
-                if (pl == 1) {
-                    t = geom_input(p, room, n_room, boxes, i);
-                    inb[i] = t;
-                } else {
-                    t = glist_get(s_list[si], sspill, i, parent);
-                }
-                k = clip_plane(t, pl, p, ch);
+        const int si = pl & 1, di = si ^ 1;
+        cg_rtri ch[2];
+        int k = 0;
+        if (lane < len) {
+            cg_rtri t = root;
+            if (pl > 1) {
+                const float4 a = s_v[si][lane][0], b = s_v[si][lane][1], c = s_v[si][lane][2];
+                t.v0 = cg_vec4{a.x, a.y, a.z, a.w};
+                t.v1 = cg_vec4{b.x, b.y, b.z, b.w};
+                t.v2 = cg_vec4{c.x, c.y, c.z, c.w};
             }
-            const unsigned long long b0 = __ballot(k & 1), b1 = __ballot(k >> 1);
-            const int pre = __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
-            if (lane == 63) wsum[wid] = pre + k;
-            __syncthreads();
-            int off = carry, tot = 0;
-            for (int w = 0; w < kGeomWaves; ++w) {
-                const int v = wsum[w];
-                off += w < wid ? v : 0;
-                tot += v;
-            }
-            off += pre;
-            if (pl < 6) {
-                if (k > 0 && off < cap) glist_put(s_list[di], dspill, off, ch[0], parent);
-                if (k > 1 && off + 1 < cap) glist_put(s_list[di], dspill, off + 1, ch[1], parent);
-            } else if (k > 0) {
-                cg_rtri o = inb[parent];                      // normal, colour, texture, index
-                if (off < cap) {
-                    o.v0 = ch[0].v0; o.v1 = ch[0].v1; o.v2 = ch[0].v2;
-                    out[off] = o;
-                }
-                if (k > 1 && off + 1 < cap) {
-                    o.v0 = ch[1].v0; o.v1 = ch[1].v1; o.v2 = ch[1].v2;
-                    out[off + 1] = o;
-                }
-            }
-            carry += tot;
-            __syncthreads();                 // wsum reuse
+            k = clip_plane(t, pl, p, ch);
         }
-        len = min(carry, cap);
-        __threadfence_block();
-        __syncthreads();                     // the new list (LDS and spill) visible to the workgroup
+        const unsigned long long b0 = __ballot(k & 1), b1 = __ballot(k >> 1);
+        const int pre = __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+        __syncthreads();   // the source list of the next plane is overwritten below
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            if (c < k) {
+                s_v[di][pre + c][0] = make_float4(ch[c].v0.x, ch[c].v0.y, ch[c].v0.z, ch[c].v0.w);
+                s_v[di][pre + c][1] = make_float4(ch[c].v1.x, ch[c].v1.y, ch[c].v1.z, ch[c].v1.w);
+                s_v[di][pre + c][2] = make_float4(ch[c].v2.x, ch[c].v2.y, ch[c].v2.z, ch[c].v2.w);
+            }
+        len = __popcll(b0) + 2 * __popcll(b1);
+        __syncthreads();
     }
-    if (threadIdx.x == 0) *out_n = len;
+    // plane 6 wrote list 1
+    if (lane < len) {
+        cg_rtri o = root;
+        const float4 a = s_v[1][lane][0], b = s_v[1][lane][1], c = s_v[1][lane][2];
+        o.v0 = cg_vec4{a.x, a.y, a.z, a.w};
+        o.v1 = cg_vec4{b.x, b.y, b.z, b.w};
+        o.v2 = cg_vec4{c.x, c.y, c.z, c.w};
+        stage[(size_t)i * kGeomMaxLeaves + lane] = o;
+    }
+    if (lane == 0) counts[i] = len;
+}
+
+__global__ __launch_bounds__(64) void rast_compact_kernel(const cg_rtri *__restrict__ stage,
+                                                          const int *__restrict__ counts, int n_in,
+                                                          cg_rtri *__restrict__ out, int cap, int *__restrict__ out_n)
+{
+    const int i = blockIdx.x, lane = threadIdx.x;
+    int before = 0, total = 0;
+    for (int j = lane; j < n_in; j += 64) {
+        const int c = counts[j];
+        before += j < i ? c : 0;
+        total += c;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        before += __shfl_xor(before, o, 64);
+        total += __shfl_xor(total, o, 64);
+    }
+    const int n = counts[i];
+    if (lane < n && before + lane < cap) out[before + lane] = stage[(size_t)i * kGeomMaxLeaves + lane];
+    if (i == 0 && lane == 0) *out_n = min(total, cap);
 }
 
 hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
-                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_scr0,
-                                cg_rtri *d_scr1, cg_rtri *d_inb, int cap, int *d_n, cg_vec4 *d_light,
-                                hipStream_t st)
+                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_stage,
+                                int *d_counts, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st)
 {
-    hipLaunchKernelGGL(rast_geometry_kernel, dim3(1), dim3(kGeomThreads), 0, st, geom_params(prm), d_room,
-                       n_room, d_boxes, n_boxes, d_out, d_scr0, d_scr1, d_inb, cap, d_n, d_light);
+    const int n_in = n_room + 7 * n_boxes;
+    if (n_in <= 0) {   // empty scene: no triangles
+        hipLaunchKernelGGL(rast_compact_kernel, dim3(1), dim3(64), 0, st, d_stage, d_counts, 0, d_out, cap, d_n);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(rast_clip_kernel, dim3(n_in), dim3(64), 0, st, geom_params(prm), d_room, n_room, d_boxes,
+                       n_boxes, d_stage, d_counts, d_light);
+    hipLaunchKernelGGL(rast_compact_kernel, dim3(n_in), dim3(64), 0, st, d_stage, d_counts, n_in, d_out, cap, d_n);
     return hipGetLastError();
 }
 

@@ -628,9 +628,8 @@ int rast_colour_fill(cg_ctx *c, const RastArgs &A, const cg_rast_params *p, cons
                      int32_t *shadow, hipStream_t st, long long *n_shaded);
 
 hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
-                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_scr0,
-                                cg_rtri *d_scr1, cg_rtri *d_inb, int cap, int *d_n, cg_vec4 *d_light,
-                                hipStream_t st);
+                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_stage,
+                                int *d_counts, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st);
 
 // The fill + post pipeline.  Either the triangle count is known on the host
 // (n_dev == nullptr, n = count) or it lives on the device (n_dev, n = capacity,
@@ -695,16 +694,16 @@ int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri
     // planes 1-4 and 6 can each split a triangle in two; plane 5 never does
     const int cap = n_in > 0 ? 32 * n_in : 1;
     hipError_t e;
-    // out + 2 spill lists + the input triangles
-    cg_rtri *tris = (cg_rtri *)ctx_buf(c, 0, (3 * (size_t)cap + n_in + 1) * sizeof(cg_rtri), &e);
+    // the clipped list, then each input triangle's staged survivors (32 each)
+    cg_rtri *tris = (cg_rtri *)ctx_buf(c, 0, ((size_t)cap + 32 * (size_t)n_in) * sizeof(cg_rtri), &e);
     if (!tris) return ctx_fail(c, e, "alloc clipped triangles");
-    int *geo = (int *)ctx_buf(c, 9, 64, &e);               // [0] count, [4..7] light
+    int *geo = (int *)ctx_buf(c, 9, 64 + 4 * (size_t)n_in, &e);   // [0] count, [4..7] light, [16..] counts
     if (!geo) return ctx_fail(c, e, "alloc geometry header");
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
     if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
-    if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, tris + 2 * (size_t)cap,
-                                  tris + 3 * (size_t)cap, cap, geo, (cg_vec4 *)(geo + 4), st)) != hipSuccess)
+    if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, geo + 16, cap, geo,
+                                  (cg_vec4 *)(geo + 4), st)) != hipSuccess)
         return ctx_fail(c, e, "rast_geometry launch");
     if (n_out) *n_out = geo;
     return rast_pipeline(c, tris, cap, geo, p, cg_vec4{0, 0, 0, 1}, (const cg_vec4 *)(geo + 4), d_argb, d_depth,
