@@ -917,6 +917,22 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             if (lat_unit_keeps(F, tc[k], s_obj[k], one == k, X, y0, y1, lo, hi))
                 atomicOr(&s_umask[h][cx], 1ull << k);
         }
+        // bit 63: a sphere may block a shadow ray of the unit -- the
+        // sphere-shadow certificate of every light over the unit's hit box
+        // (the tile's flag, rt_tile_cert_kernel, covers the whole tile)
+        const int spairs = Fs.n_sph > 0 ? nhalf * kLatW * F.n_lights : 0;
+        for (int it = threadIdx.x; it < spairs; it += kRtThreads) {
+            const int unit = it / F.n_lights, l = it - unit * F.n_lights;
+            const int h = unit / kLatW, cx = unit - h * kLatW;
+            if (cx >= cols || s_uone[h][cx] == -2) continue;
+            const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
+            const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
+            const RtLight Lt = F.lights[l];
+            const double Lp[3] = {(double)Lt.x, (double)Lt.y, (double)Lt.z};
+            bool may = false;
+            for (int q = 0; q < Fs.n_sph && !may; ++q) may = !sphere_shadow_surely_missed(sph[q], Lp, lo, hi);
+            if (may) atomicOr(&s_umask[h][cx], 1ull << 63);
+        }
     }
     __syncthreads();
     const int nL = F.n_lights;
@@ -938,7 +954,10 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             const bool folder = lw == 3 && lane < 48;
             if (step < cols) {   // DirectLight of column `step`, every light (:151-153, :366-415)
                 const int cx = step;
-                const unsigned long long um = uniform_u64(s_umask[h][cx]);
+                const unsigned long long um0 = uniform_u64(s_umask[h][cx]);
+                const unsigned long long um = um0 & ~(1ull << 63);
+                RtFrame Fu = Fs;                      // spheres only where one may block
+                if (!(um0 >> 63)) Fu.n_sph = 0;
                 const float X = 0.5f * (float)(ax0 + cx);
                 auto item = [&](int r, int l, const RtLight &Lt) {
                     const int cy = lr0 + r;
@@ -947,7 +966,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                     if (bi == INT_MIN) return;
                     const float Y = 0.5f * (float)(ay0 + cy), t = hq.x;
                     const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                    const vec3 dl = lat_direct_light(Fs, tc, sph, s_obj, Lt, bi, pos, um);
+                    const vec3 dl = lat_direct_light(Fu, tc, sph, s_obj, Lt, bi, pos, um);
                     float *b = &s_dl[step & 1][r][0][0];
                     b[l ^ lat_swz(r, 0)] = dl.x;
                     b[kLatMaxLights + (l ^ lat_swz(r, 1))] = dl.y;
