@@ -102,6 +102,7 @@ _SIGS = {
     "cg_rt_area_lights": (C.c_int, [C.POINTER(Light), C.c_float, C.c_int, C.POINTER(Light), C.c_int]),
     "cg_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(Tri)]),
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
+    "cg_rt_set_pending_cap": (C.c_int, [P, C.c_int]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
                                       C.POINTER(RtShard), P, P]),
@@ -475,6 +476,10 @@ class Context:
         sp = C.byref(sph) if sph is not None else None
         self._check(self.lib.cg_rt_set_scene(self.h, tris, n, sp, n_sph if sph is not None else 0),
                     "cg_rt_set_scene")
+
+    def rt_set_pending_cap(self, cap):
+        """Test hook: capacity of the large-scene pending shadow-ray queue (0 = default)."""
+        self._check(self.lib.cg_rt_set_pending_cap(self.h, cap), "cg_rt_set_pending_cap")
 
     def rt_render(self, cam, lights=None, n_lights=None):
         lights = default_lights() if lights is None else lights

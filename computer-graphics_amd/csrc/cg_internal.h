@@ -66,13 +66,16 @@ struct RtSphere {
     float cr, cg, cb, pad;  // color
 };
 
-// Uniform grid over a large scene's triangles (heuristic blocker search for
-// shadow rays; never a culling structure, see cg_rt_big.hip).
+// Uniform grid over a large scene's triangles: each triangle is listed in
+// every cell its bounding box touches (float floor of (x - lo) * inv_h per
+// axis, clamped).  Used by the shadow blocker hints and by the certified lit
+// search (cg_rt_big.hip).
 struct RtGrid {
     float lo[3], inv_h, h;      // cell (i, j, k) spans lo + h * [i, i + 1) x ...
     int res[3];
     const int *start;           // [cells + 1] prefix offsets into tris; null = no grid
     const int *tris;
+    float blo[3], bhi[3];       // box of every possible hit position (triangles and spheres)
 };
 
 // Frame arguments, passed by value (kernarg -> SGPRs).

@@ -42,7 +42,7 @@ constexpr int kBinW = 128, kBinH = 32;        // pixels; multiples of the 8x8 wa
 constexpr int kBinTilesX = kBinW / 8, kBinTilesY = kBinH / 8;
 static_assert(kBinTilesX * kBinTilesY == 64, "one wave tile per lane in rt_bin_boxes");
 constexpr int kBinTris = 1024;                // triangles per workgroup in the bin kernels
-constexpr int kMaxPend = 65536;               // pending shadow rays searched exhaustively in K5
+constexpr int kMaxPend = 65536;               // queue of shadow rays K4 leaves to K5 (the lit search)
 constexpr int kSupBins = 4;                   // a super-bin is 4 x 4 bins (512 x 128 px)
 constexpr int kDepthBuckets = 32;             // per bin: 0 = no key (det's sign uncertain), 1.. by key
 
@@ -54,7 +54,7 @@ struct PendRay {
 };
 
 struct BigBufs {
-    int *bin_list, *bin_n;        // [n_bins][cap], [n_bins]
+    int *bin_n;                   // [n_bins]
     // primary bin lists with keys: key bits << 32 | triangle, unsorted and by bucket
     unsigned long long *bin_ent;                       // [n_bins][cap], unsorted
     unsigned long long *bin_pbox, *bin_pbox2;          // [n_bins][cap]: projected boxes (proj_box16) for the
@@ -75,6 +75,12 @@ struct BigBufs {
     unsigned long long *sh_bits, *pend_bits;
     int *pend_n;                  // shadow rays left unresolved by K4 (counter, after bin_n/sbin_n)
     struct PendRay *pend_ray;     // [kMaxPend]
+    int max_pend;                 // queue capacity used (<= kMaxPend; lowered only by cg_rt_set_pending_cap)
+    // certified lit search (K5): triangles near the light, the walk margin and
+    // the frame's bounds on |r| (componentwise) and on |p|
+    int *near_list, *near_n;      // [n_tris], counter (pend_n[1])
+    float lit_M;
+    double litD[3], lit_pn;
     int cap, bins_x, bins_y, tiles_x, tiles_y;
     int *sup_list, *sup_n;        // [n_sups][cap], [n_sups]: triangles the super-bin's certificate keeps
     int sups_x, sups_y;
@@ -904,11 +910,11 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
                     last = k;
                 } else {
                     const int p = atomicAdd(B.pend_n, 1);
-                    if (p < kMaxPend)
+                    if (p < B.max_pend)
                         B.pend_ray[p] = PendRay{q.origin.x, q.origin.y, q.origin.z, q.nd.x, q.nd.y, q.nd.z,
                                                 q.len, q.rmag, (int)pix, s * F.n_lights + l};
                     else
-                        pending |= bit;       // past kMaxPend: rt_big_shade_kernel searches it
+                        pending |= bit;       // past the queue: rt_big_shade_kernel searches it
                 }
             }
         }
@@ -917,38 +923,240 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
     }
 }
 
-// K5: exhaustive any-hit of the unresolved shadow rays with the reference's
-// own test (cheaper than certifying): each workgroup keeps 1024 triangles in
-// registers and runs every pending ray against them; a hit sets the ray's
-// verdict bit.
-__global__ __launch_bounds__(256) void rt_pending_test_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+// ---------------------------------------------------------------------------
+// K5: certified lit search for the shadow rays K4 left unresolved.
+//
+// A shadow ray (skeleton.cpp:394) starts at S = P + n 1e-5 with direction
+// r = L - P (floats; tri_shadows receives nd = -r) and s = fl(S - v0).  Let D
+// = det[-r, e1, e2] = -r.N, T = det[s, e1, e2] = s.N, U, V (N = e1 x e2) be
+// the exact determinants of these float inputs; the float evaluations D_f,
+// T_f, U_f, V_f differ from them by at most E_D, E_T, E_U, E_V (16 eps times
+// the sum of their |triple products|, as in the certificates).  If the
+// reference's float test accepts the triangle, the real quotients satisfy
+// lambda = T_f / D_f in [-1e-6, 1 + 1e-6] (distance >= 0 and < rmag; rmag /
+// len <= 1 + 4 eps), mu = U_f / D_f >= -tiny, nu = V_f / D_f >= -tiny and
+// mu + nu <= 1 + 4 eps.  Then
+//  (1) |D_f| >= |T_f - D_f| / (1 + 1e-6) and T - D = (s + r).N with s + r =
+//      (L - v0) + p, |p| <= pn (the 1e-5 offset and the roundings): |D_f| >=
+//      delta = (|(lc - v0).N| - (rho + pn) |N| - E_T - E_D) / (1 + 1e-6) for
+//      every light within rho of lc -- delta > 0 unless the triangle's plane
+//      passes near the light;
+//  (2) Cramer's residual: Q = v0 + mu e1 + nu e2 and P = S + lambda r satisfy
+//      |Q - P| <= (|r| E_T + |e1| E_U + |e2| E_V + |s| E_D) / |D_f| + |fl(S -
+//      v0) - (S - v0)|, and Q lies within 1e-6 (|e1| + |e2|) of the closed
+//      triangle.
+// So an accepting triangle has a point within R = (2) / delta + 1e-6 (|e1| +
+// |e2|) of the segment S + [-1e-6, 1 + 1e-6] r.  rt_lit_class_kernel bounds R
+// per triangle over every shadow ray of the frame (hit positions in the
+// scene's hit box, every light): a triangle with delta <= 0 or R > M (a
+// quarter grid cell) is "near the light" and listed.  rt_pending_lit_kernel
+// tests, with the reference's own test, every listed triangle and every
+// triangle of the grid cells within M of the segment: when none accepts, no
+// triangle of the scene can -- the ray is lit, the verdict of the reference's
+// loop over all n triangles.  (Without a grid every triangle is listed.)
+__device__ bool lit_near_light(const RtTri &c, const RtFrame &F, const BigBufs &B)
 {
-    const int np = min(*B.pend_n, kMaxPend);
-    if (np == 0) return;
-    RtTri T[4];
-    bool ok[4];
+    const RtGrid &G = B.grid;
+    if (!G.start) return true;
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double g = 16.0 * eps;
+    const double e1[3] = {c.e1x, c.e1y, c.e1z}, e2[3] = {c.e2x, c.e2y, c.e2z}, v0[3] = {c.v0x, c.v0y, c.v0z};
+    const double N[3] = {e1[1] * e2[2] - e2[1] * e1[2], e1[2] * e2[0] - e2[2] * e1[0], e1[0] * e2[1] - e2[0] * e1[1]};
+    double S[3], a1[3], a2[3];
+    for (int k = 0; k < 3; ++k) {   // |s| over every start in the hit box (+ the 1e-5 offset)
+        S[k] = (fmax(fabs(v0[k] - (double)G.blo[k]), fabs((double)G.bhi[k] - v0[k])) + 1.01e-5 * (double)F.nbound) *
+                   (1.0 + 1e-6) + 1e-12;
+        a1[k] = fabs(e1[k]);
+        a2[k] = fabs(e2[k]);
+    }
+    const double *D = B.litD;
+    auto M3 = [](const double x[3], const double y[3], const double z[3]) {   // sum |triple products|
+        return x[0] * (y[1] * z[2] + y[2] * z[1]) + y[0] * (x[1] * z[2] + x[2] * z[1]) +
+               z[0] * (x[1] * y[2] + x[2] * y[1]);
+    };
+    const double Ed = g * M3(D, a1, a2), Et = g * M3(S, a1, a2), Eu = g * M3(D, S, a2), Ev = g * M3(D, a1, S);
+    const double nN = sqrt_ub(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+    const double n1 = sqrt_ub(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    const double n2 = sqrt_ub(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+    const double sn = sqrt_ub(S[0] * S[0] + S[1] * S[1] + S[2] * S[2]);
+    const double dn = sqrt_ub(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
+    const double ax = (double)F.lc[0] - v0[0], ay = (double)F.lc[1] - v0[1], az = (double)F.lc[2] - v0[2];
+    const double aN = ax * N[0] + ay * N[1] + az * N[2];
+    const double EaN = 1e-12 * (fabs(ax * N[0]) + fabs(ay * N[1]) + fabs(az * N[2]));
+    const double delta = (fabs(aN) - EaN - (F.lrho + B.lit_pn) * nN - Et - Ed) * (1.0 - 2e-6);
+    if (!(delta > 0.0)) return true;
+    const double R = (dn * Et + n1 * Eu + n2 * Ev + sn * Ed) / delta * (1.0 + 1e-9) + 1e-6 * (n1 + n2) +
+                     2.0 * eps * sn + 1e-9;
+    return !(R <= (double)B.lit_M);
+}
+
+__global__ __launch_bounds__(256) void rt_lit_class_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int base = blockIdx.x * kBinTris;
+    bool near[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int i = blockIdx.x * kBinTris + r * 256 + (int)threadIdx.x;
-        ok[r] = i < F.n_tris;
-        T[r] = tc[ok[r] ? i : 0];
+        const int i = base + r * 256 + (int)threadIdx.x;
+        near[r] = i < F.n_tris && lit_near_light(tc[i], F, B);
     }
-    // rays staged through LDS 256 at a time (one coalesced load per thread)
-    __shared__ PendRay s_r[256];
-    for (int p0 = 0; p0 < np; p0 += 256) {
-        if (p0 + (int)threadIdx.x < np) s_r[threadIdx.x] = B.pend_ray[p0 + threadIdx.x];
-        __syncthreads();
-        const int pn = min(256, np - p0);
-        for (int p = 0; p < pn; ++p) {
-            const PendRay R = s_r[p];                          // uniform: LDS broadcast
-            const vec3 o = v3(R.ox, R.oy, R.oz), nd = v3(R.nx, R.ny, R.nz);
-            bool hit = false;
+    bin_append(near, base, B.near_list, B.near_n);
+}
+
+// The cells of the walk: slabs of cells along r's major axis a; in slab i the
+// part of the segment whose a-coordinate lies within Ms of the slab, and the
+// rectangle of cells (axes b, c) within Ms of that part.  Ms = M plus a slack
+// for the float evaluation of all of this and of the grid's own cell
+// assignment (relative errors ~1e-7 of coordinates).
+struct FatWalk {
+    float o[3], d[3], Ms, tlo, thi;
+    int a, b, c, ia0, ia1;
+};
+
+__device__ __forceinline__ int grid_cell(const RtGrid &G, int k, float x)
+{
+    const float q = fminf(fmaxf((x - G.lo[k]) * G.inv_h, -1.0f), (float)G.res[k]);
+    return min(max((int)floorf(q), 0), G.res[k] - 1);
+}
+
+__device__ __forceinline__ FatWalk fat_walk_init(const RtGrid &G, vec3 S, vec3 r, float M)
+{
+    FatWalk w;
+    w.o[0] = S.x; w.o[1] = S.y; w.o[2] = S.z;
+    w.d[0] = r.x; w.d[1] = r.y; w.d[2] = r.z;
+    const float ad[3] = {fabsf(r.x), fabsf(r.y), fabsf(r.z)};
+    w.a = ad[0] >= ad[1] ? (ad[0] >= ad[2] ? 0 : 2) : (ad[1] >= ad[2] ? 1 : 2);
+    w.b = (w.a + 1) % 3;
+    w.c = (w.a + 2) % 3;
+    const float big = fmaxf(fmaxf(fabsf(S.x), fabsf(S.y)), fabsf(S.z)) + fmaxf(fmaxf(ad[0], ad[1]), ad[2]);
+    w.Ms = M * 1.00001f + 1e-5f * (1.0f + big);
+    w.tlo = -1e-6f;
+    w.thi = 1.000001f;
+    const float p0 = w.o[w.a] + w.tlo * w.d[w.a], p1 = w.o[w.a] + w.thi * w.d[w.a];
+    w.ia0 = grid_cell(G, w.a, fminf(p0, p1) - w.Ms);
+    w.ia1 = grid_cell(G, w.a, fmaxf(p0, p1) + w.Ms);
+    return w;
+}
+
+// Cell rectangle of slab i: false when the segment has no part there.
+__device__ __forceinline__ bool fat_walk_slab(const RtGrid &G, const FatWalk &w, int i, int &jb0, int &jb1, int &jc0,
+                                              int &jc1)
+{
+    const float xl = G.lo[w.a] + (float)i * G.h - w.Ms, xh = G.lo[w.a] + (float)(i + 1) * G.h + w.Ms;
+    float t0 = (xl - w.o[w.a]) / w.d[w.a], t1 = (xh - w.o[w.a]) / w.d[w.a];
+    if (!(w.d[w.a] != 0.0f)) {   // r = 0: a point
+        t0 = w.tlo;
+        t1 = w.thi;
+    }
+    if (t0 > t1) { const float x = t0; t0 = t1; t1 = x; }
+    t0 = fmaxf(t0, w.tlo);
+    t1 = fminf(t1, w.thi);
+    if (!(t0 <= t1)) return false;
+    const float b0 = w.o[w.b] + t0 * w.d[w.b], b1 = w.o[w.b] + t1 * w.d[w.b];
+    const float c0 = w.o[w.c] + t0 * w.d[w.c], c1 = w.o[w.c] + t1 * w.d[w.c];
+    jb0 = grid_cell(G, w.b, fminf(b0, b1) - w.Ms);
+    jb1 = grid_cell(G, w.b, fmaxf(b0, b1) + w.Ms);
+    jc0 = grid_cell(G, w.c, fminf(c0, c1) - w.Ms);
+    jc1 = grid_cell(G, w.c, fmaxf(c0, c1) + w.Ms);
+    return true;
+}
+
+__device__ __forceinline__ int fat_walk_cell(const RtGrid &G, const FatWalk &w, int i, int jb, int jc)
+{
+    int x[3];
+    x[w.a] = i;
+    x[w.b] = jb;
+    x[w.c] = jc;
+    return (x[2] * G.res[1] + x[1]) * G.res[0] + x[0];
+}
+
+// Whole wave, one (uniform) ray: true when a near-light triangle or a
+// triangle of a cell within M of the segment accepts it.
+__device__ bool lit_blocked_wave(const RtTri *__restrict__ tc, const BigBufs &B, const PendRay &R, int lane)
+{
+    const vec3 o = v3(R.ox, R.oy, R.oz), nd = v3(R.nx, R.ny, R.nz);
+    const int nn = *B.near_n;
+    for (int i0 = 0; i0 < nn; i0 += 64) {
+        const int i = i0 + lane;
+        const bool hit = i < nn && tri_shadows(tc[B.near_list[i]], o, nd, R.len, R.rmag);
+        if (__ballot(hit)) return true;
+    }
+    const RtGrid &G = B.grid;
+    if (!G.start) return false;
+    const FatWalk w = fat_walk_init(G, o, -nd, B.lit_M);
+    for (int i = w.ia0; i <= w.ia1; ++i) {
+        int jb0, jb1, jc0, jc1;
+        if (!fat_walk_slab(G, w, i, jb0, jb1, jc0, jc1)) continue;
+        const int nb = jb1 - jb0 + 1, ncell = nb * (jc1 - jc0 + 1);
+        for (int q0 = 0; q0 < ncell; q0 += 64) {
+            // lane q: one cell of the rectangle; its triangles are flattened
+            // across the wave by an exclusive scan of the cell sizes
+            const int q = q0 + lane, m = min(64, ncell - q0);
+            int st = 0, cnt = 0;
+            if (q < ncell) {
+                const int cell = fat_walk_cell(G, w, i, jb0 + q % nb, jc0 + q / nb);
+                st = G.start[cell];
+                cnt = G.start[cell + 1] - st;
+            }
+            int x = cnt;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hit |= ok[r] && tri_shadows(T[r], o, nd, R.len, R.rmag);
-            const unsigned long long hm = __ballot(hit);
-            if (hm != 0ull && (threadIdx.x & 63) == __builtin_ctzll(hm)) atomicOr(&B.sh_bits[R.pix], 1ull << R.bit);
+            for (int s = 1; s < 64; s <<= 1) {
+                const int y = __shfl_up(x, s);
+                if (lane >= s) x += y;
+            }
+            const int excl = x - cnt, total = __shfl(x, 63);
+            for (int j0 = 0; j0 < total; j0 += 64) {
+                const int j = min(j0 + lane, total - 1);
+                // the last cell whose prefix is <= j holds entry j (every lane
+                // takes part in the shuffles)
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step; step >>= 1) {
+                    const int mid = lo + step;
+                    const int pm = __shfl(excl, min(mid, 63));
+                    if (mid < m && pm <= j) lo = mid;
+                }
+                const int e = __shfl(st, lo) + j - __shfl(excl, lo);
+                const bool hit = j0 + lane < total && tri_shadows(tc[G.tris[e]], o, nd, R.len, R.rmag);
+                if (__ballot(hit)) return true;
+            }
         }
-        __syncthreads();
+    }
+    return false;
+}
+
+// The same for one lane's own ray (the shade kernel's overflow path).
+__device__ bool lit_blocked_lane(const RtTri *__restrict__ tc, const BigBufs &B, vec3 o, vec3 nd, float len,
+                                 float rmag)
+{
+    const int nn = *B.near_n;
+    for (int i = 0; i < nn; ++i)
+        if (tri_shadows(tc[B.near_list[i]], o, nd, len, rmag)) return true;
+    const RtGrid &G = B.grid;
+    if (!G.start) return false;
+    const FatWalk w = fat_walk_init(G, o, -nd, B.lit_M);
+    for (int i = w.ia0; i <= w.ia1; ++i) {
+        int jb0, jb1, jc0, jc1;
+        if (!fat_walk_slab(G, w, i, jb0, jb1, jc0, jc1)) continue;
+        for (int jc = jc0; jc <= jc1; ++jc)
+            for (int jb = jb0; jb <= jb1; ++jb) {
+                const int cell = fat_walk_cell(G, w, i, jb, jc);
+                for (int e = G.start[cell], ee = G.start[cell + 1]; e < ee; ++e)
+                    if (tri_shadows(tc[G.tris[e]], o, nd, len, rmag)) return true;
+            }
+    }
+    return false;
+}
+
+// One wave per unresolved shadow ray (grid-stride); a blocked ray sets its
+// verdict bit.
+__global__ __launch_bounds__(256) void rt_pending_lit_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int np = min(*B.pend_n, B.max_pend);
+    const int lane = threadIdx.x & 63;
+    for (int p = blockIdx.x * 4 + (int)(threadIdx.x >> 6); p < np; p += gridDim.x * 4) {
+        const int pu = __builtin_amdgcn_readfirstlane(p);
+        const PendRay R = B.pend_ray[pu];
+        if (lit_blocked_wave(tc, B, R, lane) && lane == 0) atomicOr(&B.sh_bits[R.pix], 1ull << R.bit);
     }
 }
 
@@ -974,7 +1182,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
         const vec4 dir = pixel_dir(F, u, v);
         const bool flags_fit = 9 * F.n_lights <= 64;
         const unsigned long long shadowed = flags_fit && F.n_lights > 0 ? B.sh_bits[pix] : 0ull;
-        // pixels past kMaxPend still carry pending bits: exhaustive search here
+        // rays past the queue still carry pending bits: the lit search per lane
         const unsigned long long left = flags_fit && F.n_lights > 0 ? B.pend_bits[pix] : 0ull;
         const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
         const int *slist = B.sbin_list + (size_t)bin * B.cap;
@@ -996,8 +1204,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
                 const int bit = s * F.n_lights + l;
                 if (flags_fit) {
                     ts = ((shadowed >> bit) & 1ull) != 0;
-                    if (!ts && ((left >> bit) & 1ull))
-                        for (int k = 0; k < F.n_tris && !ts; ++k) ts = tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag);
+                    if (!ts && ((left >> bit) & 1ull)) ts = lit_blocked_lane(tc, B, q.origin, q.nd, q.len, q.rmag);
                 } else {
                     ts = grid_blocker(B.grid, tc, q) >= 0 || any_hit(tc, slist, sn, q) >= 0;
                 }
@@ -1037,7 +1244,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return big_counter_bytes(B) + 2 * bins * B.cap * 4 + 7 * bins * (size_t)B.cap * 8 +
+    return big_counter_bytes(B) + bins * B.cap * 4 + (size_t)F.n_tris * 4 + 7 * bins * (size_t)B.cap * 8 +
            (size_t)B.sups_x * B.sups_y * B.cap * 4 +
            2 * bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
            2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
@@ -1066,7 +1273,8 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.sh_bits = (unsigned long long *)p;   p += npix * 8;
     B.pend_bits = (unsigned long long *)p; p += npix * 8;
     B.pend_ray = (PendRay *)p;             p += (size_t)kMaxPend * sizeof(PendRay);
-    B.bin_list = (int *)p; p += bins * B.cap * 4;
+    B.near_n = B.pend_n + 1;
+    B.near_list = (int *)p; p += (size_t)F.n_tris * 4;
     B.sbin_list = (int *)p; p += bins * B.cap * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
     B.bin_ent = (unsigned long long *)p;    p += bins * (size_t)B.cap * 8;
@@ -1077,12 +1285,35 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.sup_list = (int *)p;
 }
 
+// Frame bounds of the lit search (K5): |r_k| = |fl(L - P)_k| over every
+// light and hit position, |p| (see lit_near_light), the walk margin.
+static void lit_bounds(BigBufs &B, const RtFrame &F, const RtGrid &G)
+{
+    const double eps = 5.9604644775390625e-8;
+    double pmax = 0.0, dmax = 0.0, smax = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        B.litD[k] = std::max(std::fabs((double)F.lmax[k] - G.blo[k]), std::fabs((double)G.bhi[k] - F.lmin[k])) *
+                        (1.0 + 1e-6) + 1e-12;
+        pmax = std::max(pmax, std::max(std::fabs((double)G.blo[k]), std::fabs((double)G.bhi[k])));
+        dmax = std::max(dmax, B.litD[k]);
+        smax = std::max(smax, (double)G.bhi[k] - G.blo[k]);
+    }
+    smax += 1.01e-5 * F.nbound + 1e-6 * pmax;
+    // p = (S - P - n 1e-5) + n 1e-5 + (fl(L - P) - (L - P)) + (fl(S - v0) - (S - v0))
+    B.lit_pn = std::sqrt(3.0) * (1.01e-5 * F.nbound + eps * (pmax + 1e-4) + eps * dmax + eps * smax) * (1.0 + 1e-6) +
+               1e-12;
+    B.lit_M = 0.25f * G.h;
+}
+
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
-                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const cg_tri *d_tris)
+                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const cg_tri *d_tris,
+                         int pend_cap)
 {
     BigBufs B = big_layout(F, F.n_tris);
     big_carve(B, F, scratch);
     B.grid = grid;
+    B.max_pend = pend_cap > 0 ? std::min(pend_cap, kMaxPend) : kMaxPend;
+    lit_bounds(B, F, grid);
     const int bins = B.bins_x * B.bins_y;
     hipError_t e = hipMemsetAsync(B.bin_n, 0, big_counter_bytes(B), st);
     if (e != hipSuccess) return e;
@@ -1101,8 +1332,9 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
     } else if (F.n_lights > 0) {
+        hipLaunchKernelGGL(rt_lit_class_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
         hipLaunchKernelGGL(rt_shadow_hints_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-        hipLaunchKernelGGL(rt_pending_test_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
+        hipLaunchKernelGGL(rt_pending_lit_kernel, dim3(1024), dim3(256), 0, st, F, d_tc, B);
     }
     hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     return hipGetLastError();

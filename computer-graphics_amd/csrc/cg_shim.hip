@@ -26,7 +26,7 @@ hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, con
 bool rt_use_lattice(const RtFrame &);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
-                         uint32_t *, hipStream_t, const cg_tri *);
+                         uint32_t *, hipStream_t, const cg_tri *, int);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
@@ -90,6 +90,7 @@ struct cg_ctx {
     int slot = 0;
     DevBuf ptc[2], pshade[2], plat[2], psup[2];
     RtGrid grid{};                      // large scenes only (n_tris > 64)
+    int pend_cap = 0;                   // cg_rt_set_pending_cap (0 = default)
     std::vector<cg_tri> tris_host;      // the scene as uploaded (cg_dist's column window)
     std::vector<cg_sphere> sph_host;
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
@@ -305,8 +306,35 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
                 CG_TRY(c, hipMemcpy(c->gtris.p, gt.data(), gt.size() * 4, hipMemcpyHostToDevice), "upload grid");
             g.start = (const int *)c->gstart.p;
             g.tris = (const int *)c->gtris.p;
-            c->grid = g;
         }
+        // hit positions lie on a triangle or a sphere: the box of both
+        for (int k = 0; k < 3; ++k) {
+            g.blo[k] = FLT_MAX;
+            g.bhi[k] = -FLT_MAX;
+        }
+        auto grow = [&](int k, float lo, float hi) {
+            g.blo[k] = std::min(g.blo[k], lo);
+            g.bhi[k] = std::max(g.bhi[k], hi);
+        };
+        for (int i = 0; i < n_tris; ++i) {
+            const cg_vec4 *v[3] = {&tris[i].v0, &tris[i].v1, &tris[i].v2};
+            for (const cg_vec4 *p : v) {
+                grow(0, p->x, p->x);
+                grow(1, p->y, p->y);
+                grow(2, p->z, p->z);
+            }
+        }
+        for (int i = 0; i < n_spheres; ++i) {   // radius from radiusSquared, rounded up
+            const float r = (float)(std::sqrt((double)spheres[i].radiusSquared) * (1.0 + 1e-6));
+            grow(0, spheres[i].centre.x - r, spheres[i].centre.x + r);
+            grow(1, spheres[i].centre.y - r, spheres[i].centre.y + r);
+            grow(2, spheres[i].centre.z - r, spheres[i].centre.z + r);
+        }
+        for (int k = 0; k < 3; ++k) {   // float hit positions stray by rounding: widen
+            g.blo[k] -= 1e-4f + 1e-5f * std::fabs(g.blo[k]);
+            g.bhi[k] += 1e-4f + 1e-5f * std::fabs(g.bhi[k]);
+        }
+        c->grid = g;
     }
     CG_TRY(c, hipStreamSynchronize(c->stream), "scene upload");
     // Hit normals: the triangles' own (skeleton.cpp:378) and normalize(pos -
@@ -411,6 +439,13 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     return set_lights(c, lights, n_lights, st, F);
 }
 
+extern "C" int cg_rt_set_pending_cap(cg_ctx *c, int cap)
+{
+    if (!c || cap < 0) return CG_E_INVALID;
+    c->pend_cap = cap;
+    return CG_OK;
+}
+
 extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
 {
     cg_rt_shard one{0, 1, kRtTileH, 0, 0, 0, 0};
@@ -464,7 +499,8 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
         // large scene: binned certificates (cg_rt_big.hip)
         CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
         CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
-                                c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p), "rt_big launch");
+                                c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap),
+               "rt_big launch");
         return CG_OK;
     }
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,

@@ -200,6 +200,11 @@ int cg_rt_probe_closest(cg_ctx *ctx, const cg_vec4 *starts, const cg_vec4 *dirs,
                         cg_isect *out, int *hit);
 int cg_rt_probe_direct_light(cg_ctx *ctx, const cg_isect *isects, const cg_light *light, int n,
                              cg_vec3 *out);
+/* Test hook for large scenes (n_tris > 64): capacity of the device queue of
+ * shadow rays the blocker hints leave to the certified lit search (0 = the
+ * default, 65536).  Rays past the queue are searched per pixel by the shading
+ * kernel instead; the image is the same either way. */
+int cg_rt_set_pending_cap(cg_ctx *ctx, int cap);
 
 /* ---- multi-GPU raytracer ------------------------------- */
 /* One process per GPU.  The reference renders every pixel of Draw

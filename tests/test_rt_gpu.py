@@ -396,6 +396,28 @@ def test_rt_c5_1m_triangles_sampled(rt):
     assert (got != 0x80000000).sum() > 100      # the sample does see the cloud
 
 
+@pytest.mark.parametrize("cap", [1, 64])
+def test_rt_c5_pending_queue_overflow(rt, golden, cap):
+    """Shadow rays past the pending queue take the shading kernel's per-lane
+    certified lit search instead of the wave-per-ray one: the C5 golden frame
+    (2000 triangles) and a 100k-triangle frame are unchanged."""
+    cfg = mg.rt_configs()["rt_c5_256x144_rand2000"]
+    big = dict(C5_FULL, width=320, height=180, focal=180.0, scene=dict(random=100_000, seed=0x5EED))
+    try:
+        _set_scene(rt, big)
+        want, _ = rt.rt_render(_cam(big), _lights(big))
+        _set_scene(rt, cfg)
+        rt.rt_set_pending_cap(cap)
+        argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+        assert mg.sha(argb) == golden["rt"]["rt_c5_256x144_rand2000"]["argb_sha256"]
+        _set_scene(rt, big)
+        got, _ = rt.rt_render(_cam(big), _lights(big))
+        assert np.array_equal(got, want)
+    finally:
+        rt.rt_set_pending_cap(0)
+        _set_scene(rt, {})
+
+
 def test_rt_c5_sharded_matches_whole(rt):
     """C5's multi-GPU form (32-row stripes over 4 ranks) == the whole frame."""
     torch = pytest.importorskip("torch")
