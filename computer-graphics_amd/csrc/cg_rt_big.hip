@@ -82,6 +82,7 @@ struct BigBufs {
     float lit_M;
     double litD[3], lit_pn;
     int cap, bins_x, bins_y, tiles_x, tiles_y;
+    int lat_w, lat_h;             // lattice mode: (2 W + 1) x (2 rows + 1) points; 0 = per-pixel mode
     int *sup_list, *sup_n;        // [n_sups][cap], [n_sups]: triangles the super-bin's certificate keeps
     int sups_x, sups_y;
 };
@@ -547,23 +548,92 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs 
     }
 }
 
-// K1: closest hits of the 9 sub-rays of every pixel.
+// Ray slots of one wave tile (K1, K4 and the shading kernel read them):
+//  * per-pixel mode: the tile's 8x8 pixels, lane = pixel, slot s = its
+//    sub-ray s (skeleton.cpp:134-140), stored at s * npix + pixel;
+//  * lattice mode (unrotated camera, rows contiguous, <= 64 lights): with R =
+//    identity pixel (u, v)'s sub-ray (i, j) has the exact direction ((u - W/2)
+//    + i/2, (v - H/2) + j/2, f) (cg_rt.hip), the half-pixel lattice point
+//    (2u + i, 2v + j) its neighbours share.  Its closest hit and its shadow
+//    verdicts depend only on the ray, so each point is traced once: the tile
+//    owns lattice columns Xi = 2u + i + 1 in [16 tx, 16 tx + 16) and rows Yi
+//    = 2 (v - row0) + j + 1 in [16 ty, 16 ty + 16) (the last tile of a row or
+//    column also the one beyond), slot s of a lane is owned point s * 64 +
+//    lane, stored at Yi * lat_w + Xi: 4 rays per lane instead of 9.
+struct LatOwn {
+    int xi0, nx, yi0, ny;
+};
+__device__ __forceinline__ LatOwn lat_own(const RtFrame &F, const BigBufs &B, int tx, int ty)
+{
+    LatOwn o;
+    const int rows = min(F.rows_out, F.H - F.row0);    // rows with v < H
+    o.xi0 = 16 * tx;
+    o.yi0 = 16 * ty;
+    const int xe = tx == (F.W - 1) / 8 ? B.lat_w : min(16 * tx + 16, B.lat_w);
+    const int ye = ty == (rows - 1) / 8 ? B.lat_h : min(16 * ty + 16, B.lat_h);
+    o.nx = max(0, xe - o.xi0);
+    o.ny = ty > (rows - 1) / 8 ? 0 : max(0, ye - o.yi0);
+    return o;
+}
+__device__ __forceinline__ float lat_x(const RtFrame &F, int Xi) { return 0.5f * (float)(Xi - 1 - 2 * (F.W / 2)); }
+__device__ __forceinline__ float lat_y(const RtFrame &F, int Yi)
+{
+    return 0.5f * (float)(Yi - 1 + 2 * F.row0 - 2 * (F.H / 2));
+}
+
+// K1: closest hits of every ray slot of the tile.
+template <bool kLat>
 __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                     const RtShade *__restrict__ shade,
                                                                     const RtSphere *__restrict__ sph, BigBufs B)
 {
+    constexpr int NS = kLat ? 5 : 9;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
-    if (tx >= B.tiles_x) return;                                   // whole wave beyond W
-    const int u = tx * 8 + (lane & 7), L = ty * 8 + (lane >> 3);
-    const bool inside = u < F.W && L < F.rows_out;
-    const int v = inside ? shard_row(F, L) : 0;
-    const bool active = inside && v < F.H;
-    vec4 dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
-    dir = mat4_mul(F.R, dir);                                                         // :128
-    float x0 = wave_min(active ? dir.x : FLT_MAX), x1 = wave_max(active ? dir.x : -FLT_MAX);
-    float y0 = wave_min(active ? dir.y : FLT_MAX), y1 = wave_max(active ? dir.y : -FLT_MAX);
-    x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    if (tx >= B.tiles_x) return;
+    const float m = 0.5f;
+    // slot directions: per-pixel mode dir +- m (i, j); lattice mode rx / ry
+    float rx[kLat ? NS : 1], ry[kLat ? NS : 1];
+    bool on[NS];
+    vec4 dir = v4(0.0f, 0.0f, 0.0f, 0.0f);
+    int u = 0, L = 0, nsu = NS;
+    float x0, x1, y0, y1;
+    if constexpr (kLat) {
+        const LatOwn o = lat_own(F, B, tx, ty);
+        const int n = o.nx * o.ny;
+        nsu = __builtin_amdgcn_readfirstlane((n + 63) >> 6);
+        float a0 = FLT_MAX, a1 = -FLT_MAX, b0 = FLT_MAX, b1 = -FLT_MAX;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int k = s * 64 + lane;
+            on[s] = k < n;
+            const int kk = on[s] ? k : 0;
+            rx[s] = lat_x(F, o.xi0 + kk % max(o.nx, 1));
+            ry[s] = lat_y(F, o.yi0 + kk / max(o.nx, 1));
+            if (on[s]) {
+                a0 = fminf(a0, rx[s]); a1 = fmaxf(a1, rx[s]);
+                b0 = fminf(b0, ry[s]); b1 = fmaxf(b1, ry[s]);
+            }
+        }
+        x0 = wave_min(a0); x1 = wave_max(a1); y0 = wave_min(b0); y1 = wave_max(b1);
+    } else {
+        u = tx * 8 + (lane & 7);
+        L = ty * 8 + (lane >> 3);
+        const bool inside = u < F.W && L < F.rows_out;
+        const int v = inside ? shard_row(F, L) : 0;
+        const bool active = inside && v < F.H;
+        dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
+        dir = mat4_mul(F.R, dir);                                                    // :128
+#pragma unroll
+        for (int s = 0; s < NS; ++s) on[s] = active;
+        x0 = wave_min(active ? dir.x : FLT_MAX); x1 = wave_max(active ? dir.x : -FLT_MAX);
+        y0 = wave_min(active ? dir.y : FLT_MAX); y1 = wave_max(active ? dir.y : -FLT_MAX);
+        x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    }
+    auto slot_nd = [&](int s) -> vec3 {                                              // :137
+        if constexpr (kLat) return v3(rx[s], ry[s], F.focal);
+        else return v3(dir.x + (m * (float)(s / 3 - 1)), dir.y + (m * (float)(s % 3 - 1)), F.focal);
+    };
     const bool any = x0 <= x1;
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
     const int sub = 2 * bin + ((tx % kBinTilesX) < kBinTilesX / 2 ? 0 : 1);          // the wave's half-bin
@@ -571,21 +641,18 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     const unsigned long long *pboxes = B.bin_spbox + (size_t)sub * B.cap;
     const int *boff = B.bkt_off + sub * (kDepthBuckets + 1);
     const unsigned *bmin_inv = B.bkt_min_inv + sub * kDepthBuckets;
-    const float m = 0.5f;
-    float best[9], bt[9], len[9];
-    int bi[9];
+    float best[NS], bt[NS], len[NS];
+    int bi[NS];
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-        const int i = s / 3 - 1, j = s % 3 - 1;
-        vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);       // :137
-        len[s] = length(nd);                                                          // :307
+    for (int s = 0; s < NS; ++s) {
+        len[s] = length(slot_nd(s));                                                 // :307
         best[s] = FLT_MAX;
         bt[s] = 0.0f;
         bi[s] = INT_MIN;
     }
-    // buckets nearest first; tb = the largest best distance of any active
-    // lane's sub-ray (FLT_MAX while one has no hit): a candidate whose key
-    // exceeds it cannot win or tie for any of them
+    // buckets nearest first; tb = the largest best distance of any slot's ray
+    // (FLT_MAX while one has no hit): a candidate whose key exceeds it cannot
+    // win or tie for any of them
     float tb = FLT_MAX;
     // Entries passing the box and key tests are queued in LDS and certified
     // 64 at a time (full lanes for the FP64 certificate), the queue flushed
@@ -602,20 +669,14 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
             mask &= mask - 1ull;
             const int k = __builtin_amdgcn_readlane(cand, b);
             const RtTri T = tc[k];                                            // scalar loads
-            if (active) {
 #pragma unroll
-                for (int s = 0; s < 9; ++s) {
-                    const int i = s / 3 - 1, j = s % 3 - 1;
-                    vec3 nd = -v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
-                    tri_closest(T, k, nd, len[s], best[s], bt[s], bi[s]);
-                }
-            }
+            for (int s = 0; s < NS; ++s)
+                if (s < nsu && on[s]) tri_closest(T, k, -slot_nd(s), len[s], best[s], bt[s], bi[s]);
         }
         float lm = -FLT_MAX;
-        if (active) {
 #pragma unroll
-            for (int s = 0; s < 9; ++s) lm = fmaxf(lm, best[s]);
-        }
+        for (int s = 0; s < NS; ++s)
+            if (on[s]) lm = fmaxf(lm, best[s]);
         tb = wave_max(lm);
     };
     for (int q = 0; any && q < kDepthBuckets; ++q) {
@@ -655,39 +716,48 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     LaneShadowBox sb;
     sb.init();
     const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
-    if (active) {
-        const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
-        const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
+    const vec3 s3 = v3(F.cam[0], F.cam[1], F.cam[2]);
+    const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
+    LatOwn o{};
+    if constexpr (kLat) o = lat_own(F, B, tx, ty);
 #pragma unroll
-        for (int s = 0; s < 9; ++s) {
-            const int i = s / 3 - 1, j = s % 3 - 1;
-            vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);
-            for (int q = 0; q < F.n_sph; ++q) {                                       // :341-355
-                float t;
-                if (sphere_intersect(sph[q], s3, nd, t) && t < best[s]) {
-                    best[s] = t;
-                    bt[s] = t;
-                    bi[s] = -1 - q;
-                }
-            }
-            const int hit = best[s] < FLT_MAX ? bi[s] : INT_MIN;                     // :357
-            B.hit_bi[s * npix + pix] = hit;
-            B.hit_t[s * npix + pix] = bt[s];
-            if (hit != INT_MIN && F.n_lights > 0) {
-                const float t = bt[s];
-                vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
-                shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, hit, pos));
+    for (int s = 0; s < NS; ++s) {
+        if (!(s < nsu && on[s])) continue;
+        const vec3 nd = slot_nd(s);
+        for (int q = 0; q < F.n_sph; ++q) {                                           // :341-355
+            float t;
+            if (sphere_intersect(sph[q], s3, nd, t) && t < best[s]) {
+                best[s] = t;
+                bt[s] = t;
+                bi[s] = -1 - q;
             }
         }
+        const int hit = best[s] < FLT_MAX ? bi[s] : INT_MIN;                         // :357
+        size_t id;
+        if constexpr (kLat) {
+            const int k = s * 64 + lane;
+            id = (size_t)(o.yi0 + k / o.nx) * B.lat_w + o.xi0 + k % o.nx;
+        } else {
+            id = s * npix + pix;
+        }
+        B.hit_bi[id] = hit;
+        B.hit_t[id] = bt[s];
+        if (!kLat && hit != INT_MIN && F.n_lights > 0) {
+            const float t = bt[s];
+            vec3 pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);
+            shadow_box_add(sb, lmin, lmax, pos, hit_normal(shade, sph, hit, pos));
+        }
     }
-    ShadowBox W;
+    if constexpr (!kLat) {   // the many-light path's boxes (per-pixel mode only)
+        ShadowBox W;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        W.lo[q] = wave_min(sb.lo[q]);
-        W.hi[q] = wave_max(sb.hi[q]);
+        for (int q = 0; q < 3; ++q) {
+            W.lo[q] = wave_min(sb.lo[q]);
+            W.hi[q] = wave_max(sb.hi[q]);
+        }
+        W.pn = wave_max(sb.pn);
+        if (lane == 0) B.wave_box[(size_t)ty * B.tiles_x + tx] = W;
     }
-    W.pn = wave_max(sb.pn);
-    if (lane == 0) B.wave_box[(size_t)ty * B.tiles_x + tx] = W;
 }
 
 // K2: union of the wave boxes of each bin (one wave tile per lane).
@@ -834,7 +904,8 @@ __device__ int grid_blocker(const RtGrid &G, const RtTri *__restrict__ tc, const
 }
 
 // Shadow verdicts for 9 * n_lights <= 64 (one bit per (sub-ray s, light l)
-// and pixel), in two parallel steps:
+// and pixel; lattice mode: n_lights <= 64, one bit per light and point), in
+// two parallel steps:
 //  K4 rt_shadow_hints   each shadow ray tries likely blockers: the triangle it
 //                       starts on (the 1e-5 normal offset puts the origin
 //                       behind it when the normal faces away from the light),
@@ -842,18 +913,14 @@ __device__ int grid_blocker(const RtGrid &G, const RtTri *__restrict__ tc, const
 //                       triangle the exact test accepts blocks the ray -- an
 //                       any-hit verdict does not depend on the order.  Rays
 //                       still unresolved are queued;
-//  K5 rt_pending_test   the exhaustive search for the queued rays: every
-//                       triangle, the reference's own test.
+//  K5 rt_pending_lit    the certified lit search for the queued rays (below).
 __device__ __forceinline__ void hit_geometry(const RtFrame &F, const BigBufs &B, const RtShade *__restrict__ shade,
-                                             const RtSphere *__restrict__ sph, vec4 dir, int s, size_t pix,
-                                             size_t npix, int &bi, vec3 &pos, vec3 &normal)
+                                             const RtSphere *__restrict__ sph, vec3 nd, size_t id, int &bi,
+                                             vec3 &pos, vec3 &normal)
 {
-    const float m = 0.5f;
-    bi = B.hit_bi[s * npix + pix];
+    bi = B.hit_bi[id];
     if (bi == INT_MIN) return;
-    const int i = s / 3 - 1, j = s % 3 - 1;
-    const float t = B.hit_t[s * npix + pix];
-    vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);           // :137
+    const float t = B.hit_t[id];
     pos = v3(F.cam[0] + t * nd.x, F.cam[1] + t * nd.y, F.cam[2] + t * nd.z);         // :326/:345
     normal = hit_normal(shade, sph, bi, pos);
 }
@@ -863,61 +930,99 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
     return mat4_mul(F.R, v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f));   // :126-128
 }
 
+// K4 over the tile's ray slots (see K1): per-pixel mode keeps pixel bits s *
+// n_lights + l, lattice mode point bits l.  Every lane walks the same (slot,
+// light) sequence, so the wave's lanes meet at each step of the neighbour
+// exchange.
+template <bool kLat>
 __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
 {
+    constexpr int NS = kLat ? 5 : 9;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
-    const int u = tx * 8 + (lane & 7), L = ty * 8 + (lane >> 3);
-    const bool inside = u < F.W && L < F.rows_out;
-    const int v = inside ? shard_row(F, L) : 0;
-    const bool active = inside && v < F.H;
+    const float m = 0.5f;
+    int u = 0, L = 0, nsu = NS, n = 0;
+    bool active = false;
+    vec4 dir = v4(0.0f, 0.0f, 0.0f, 0.0f);
+    LatOwn o{};
+    if constexpr (kLat) {
+        o = lat_own(F, B, tx, ty);
+        n = o.nx * o.ny;
+        nsu = __builtin_amdgcn_readfirstlane((n + 63) >> 6);
+    } else {
+        u = tx * 8 + (lane & 7);
+        L = ty * 8 + (lane >> 3);
+        const bool inside = u < F.W && L < F.rows_out;
+        const int v = inside ? shard_row(F, L) : 0;
+        active = inside && v < F.H;
+        dir = pixel_dir(F, u, v);
+    }
     const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
-    const vec4 dir = pixel_dir(F, u, v);
     unsigned long long shadowed = 0ull, pending = 0ull;
-    int gtests = 0;
-    if (active) {
-        int last = -1;
-        for (int s = 0; s < 9; ++s) {
-            int bi;
-            vec3 pos, normal;
-            hit_geometry(F, B, shade, sph, dir, s, pix, npix, bi, pos, normal);
-            if (bi == INT_MIN) continue;
-            for (int l = 0; l < F.n_lights; ++l) {
-                const RtLight Lt = F.lights[l];
-                const ShadowRay q = shadow_ray(Lt, pos, normal);
-                int k = -1;
+    int last = -1, gtests = 0;
+    for (int s = 0; s < nsu; ++s) {
+        bool on;
+        vec3 nd;
+        size_t id;
+        if constexpr (kLat) {
+            const int k = s * 64 + lane;
+            on = k < n;
+            const int kk = on ? k : 0, Xi = o.xi0 + kk % max(o.nx, 1), Yi = o.yi0 + kk / max(o.nx, 1);
+            nd = v3(lat_x(F, Xi), lat_y(F, Yi), F.focal);
+            id = (size_t)Yi * B.lat_w + Xi;
+            shadowed = pending = 0ull;
+        } else {
+            on = active;
+            nd = v3(dir.x + (m * (float)(s / 3 - 1)), dir.y + (m * (float)(s % 3 - 1)), F.focal);   // :137
+            id = s * npix + pix;
+        }
+        int bi = INT_MIN;
+        vec3 pos = v3(0.0f, 0.0f, 0.0f), normal = pos;
+        if (on) hit_geometry(F, B, shade, sph, nd, id, bi, pos, normal);
+        const bool ray = bi != INT_MIN;
+        for (int l = 0; l < F.n_lights; ++l) {
+            const RtLight Lt = F.lights[l];
+            const ShadowRay q = shadow_ray(Lt, pos, normal);
+            int k = -1;
+            if (ray) {
                 if (bi >= 0 && tri_shadows(tc[bi], q.origin, q.nd, q.len, q.rmag)) k = bi;
                 else if (last >= 0 && tri_shadows(tc[last], q.origin, q.nd, q.len, q.rmag)) k = last;
-                {
-                    // unresolved rays try up to sixteen distinct blockers other rays of
-                    // the wave found.  They are only hints: each is re-tested with the
-                    // exact tri_shadows, so the verdict does not depend on which lanes
-                    // (pixels, sub-rays) contributed them
-                    unsigned long long have = __ballot(k >= 0);
-                    for (int rep = 0; rep < 16 && have != 0ull && __ballot(k < 0) != 0ull; ++rep) {
-                        const int kn = __shfl(k, __builtin_ctzll(have));
-                        have &= ~__ballot(k == kn);
-                        if (k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
-                    }
-                }
-                if (k < 0) k = grid_blocker(B.grid, tc, q, &gtests);
-                const unsigned long long bit = 1ull << (s * F.n_lights + l);
-                if (k >= 0) {
-                    shadowed |= bit;
-                    last = k;
-                } else {
-                    const int p = atomicAdd(B.pend_n, 1);
-                    if (p < B.max_pend)
-                        B.pend_ray[p] = PendRay{q.origin.x, q.origin.y, q.origin.z, q.nd.x, q.nd.y, q.nd.z,
-                                                q.len, q.rmag, (int)pix, s * F.n_lights + l};
-                    else
-                        pending |= bit;       // past the queue: rt_big_shade_kernel searches it
-                }
+            }
+            // unresolved rays try up to sixteen distinct blockers other rays of the
+            // wave found.  They are only hints: each is re-tested with the exact
+            // tri_shadows, so the verdict does not depend on which lanes
+            // contributed them
+            unsigned long long have = __ballot(k >= 0);
+            for (int rep = 0; rep < 16 && have != 0ull && __ballot(ray && k < 0) != 0ull; ++rep) {
+                const int kn = __shfl(k, __builtin_ctzll(have));
+                have &= ~__ballot(k == kn);
+                if (ray && k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
+            }
+            if (!ray) continue;
+            if (k < 0) k = grid_blocker(B.grid, tc, q, &gtests);
+            const int bitno = kLat ? l : s * F.n_lights + l;
+            const unsigned long long bit = 1ull << bitno;
+            if (k >= 0) {
+                shadowed |= bit;
+                last = k;
+            } else {
+                const int p = atomicAdd(B.pend_n, 1);
+                if (p < B.max_pend)
+                    B.pend_ray[p] = PendRay{q.origin.x, q.origin.y, q.origin.z, q.nd.x, q.nd.y, q.nd.z,
+                                            q.len, q.rmag, (int)(kLat ? id : pix), bitno};
+                else
+                    pending |= bit;       // past the queue: rt_big_shade_kernel searches it
             }
         }
+        if (kLat && on) {
+            B.sh_bits[id] = shadowed;
+            B.pend_bits[id] = pending;
+        }
+    }
+    if (!kLat && active) {
         B.sh_bits[pix] = shadowed;
         B.pend_bits[pix] = pending;
     }
@@ -1160,9 +1265,11 @@ __global__ __launch_bounds__(256) void rt_pending_lit_kernel(RtFrame F, const Rt
     }
 }
 
-// K7: shading in the reference's order (:143-166) from the shadow verdicts;
-// with more than 7 lights each (s, l) is resolved here (grid, then the
-// bin's certified shadow list).
+// K7: shading in the reference's order (:143-166) from the shadow verdicts
+// (per sub-ray in per-pixel mode, per lattice point in lattice mode); with
+// more than 7 lights in per-pixel mode each (s, l) is resolved here (grid,
+// then the bin's certified shadow list).
+template <bool kLat>
 __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph, BigBufs B,
@@ -1180,28 +1287,37 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
     if (active) {
         const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
         const vec4 dir = pixel_dir(F, u, v);
-        const bool flags_fit = 9 * F.n_lights <= 64;
-        const unsigned long long shadowed = flags_fit && F.n_lights > 0 ? B.sh_bits[pix] : 0ull;
+        const bool flags_fit = kLat || 9 * F.n_lights <= 64;
+        const unsigned long long pshadowed = !kLat && flags_fit && F.n_lights > 0 ? B.sh_bits[pix] : 0ull;
         // rays past the queue still carry pending bits: the lit search per lane
-        const unsigned long long left = flags_fit && F.n_lights > 0 ? B.pend_bits[pix] : 0ull;
+        const unsigned long long pleft = !kLat && flags_fit && F.n_lights > 0 ? B.pend_bits[pix] : 0ull;
         const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
         const int *slist = B.sbin_list + (size_t)bin * B.cap;
         const int sn = flags_fit ? 0 : B.sbin_n[bin];
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
+        const float m = 0.5f;
         for (int s = 0; s < 9; ++s) {
+            const int i = s / 3 - 1, j = s % 3 - 1;
+            const vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);   // :137
+            const size_t id = kLat ? (size_t)(2 * L + j + 1) * B.lat_w + (2 * u + i + 1) : s * npix + pix;
             int bi;
             vec3 pos, normal;
-            hit_geometry(F, B, shade, sph, dir, s, pix, npix, bi, pos, normal);
+            hit_geometry(F, B, shade, sph, nd, id, bi, pos, normal);
             if (bi == INT_MIN) continue;
             valid = true;
+            unsigned long long shadowed = pshadowed, left = pleft;
+            if (kLat && F.n_lights > 0) {
+                shadowed = B.sh_bits[id];
+                left = B.pend_bits[id];
+            }
             vec3 oc = object_colour(shade, sph, bi);
             for (int l = 0; l < F.n_lights; ++l) {                                    // :151-153
                 const RtLight Lt = F.lights[l];
                 const ShadowRay q = shadow_ray(Lt, pos, normal);
                 bool ts;
-                const int bit = s * F.n_lights + l;
+                const int bit = kLat ? l : s * F.n_lights + l;
                 if (flags_fit) {
                     ts = ((shadowed >> bit) & 1ull) != 0;
                     if (!ts && ((left >> bit) & 1ull)) ts = lit_blocked_lane(tc, B, q.origin, q.nd, q.len, q.rmag);
@@ -1218,6 +1334,16 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
 }
 
 // ---------------------------------------------------------------------------
+// Lattice mode (K1): unrotated camera, contiguous rows (whole frame or band),
+// verdict bits for every light in one word per point.
+static bool rt_big_lattice(const RtFrame &F)
+{
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            if (F.R[4 * c + r] != (r == c ? 1.0f : 0.0f)) return false;
+    return F.nranks == 1 && F.n_lights <= 64 && F.W < (1 << 20) && F.H < (1 << 20);
+}
+
 BigBufs big_layout(const RtFrame &F, int cap)
 {
     BigBufs B{};
@@ -1228,6 +1354,11 @@ BigBufs big_layout(const RtFrame &F, int cap)
     B.tiles_y = (F.rows_out + 7) / 8;
     B.sups_x = (B.bins_x + kSupBins - 1) / kSupBins;
     B.sups_y = (B.bins_y + kSupBins - 1) / kSupBins;
+    const int rows = std::min(F.rows_out, F.H - F.row0);
+    if (rt_big_lattice(F) && rows > 0) {
+        B.lat_w = 2 * F.W + 1;
+        B.lat_h = 2 * rows + 1;
+    }
     return B;
 }
 
@@ -1239,19 +1370,29 @@ size_t big_counter_bytes(const BigBufs &B)
     return 2 * bins * 4 + 16 + 4 * bins * kDepthBuckets * 4 + 2 * bins * 4 + sups * 4;
 }
 
+// Ray slots (hits) and verdict words of the mode.
+static size_t big_slots(const BigBufs &B, const RtFrame &F)
+{
+    return B.lat_w ? (size_t)B.lat_w * B.lat_h : 9 * (size_t)F.rows_out * F.W;
+}
+static size_t big_words(const BigBufs &B, const RtFrame &F)
+{
+    return B.lat_w ? (size_t)B.lat_w * B.lat_h : (size_t)F.rows_out * F.W;
+}
+
 // Bytes of device scratch for big_layout(F, cap), and its carving.
 size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
-    const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
+    const size_t bins = (size_t)B.bins_x * B.bins_y;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
     return big_counter_bytes(B) + bins * B.cap * 4 + (size_t)F.n_tris * 4 + 7 * bins * (size_t)B.cap * 8 +
            (size_t)B.sups_x * B.sups_y * B.cap * 4 +
-           2 * bins * (kDepthBuckets + 1) * 4 + 9 * npix * 8 + (tiles + bins) * sizeof(ShadowBox) +
-           2 * npix * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
+           2 * bins * (kDepthBuckets + 1) * 4 + big_slots(B, F) * 8 + (tiles + bins) * sizeof(ShadowBox) +
+           2 * big_words(B, F) * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
 {
-    const size_t bins = (size_t)B.bins_x * B.bins_y, npix = (size_t)F.rows_out * F.W;
+    const size_t bins = (size_t)B.bins_x * B.bins_y, slots = big_slots(B, F), words = big_words(B, F);
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
     char *p = (char *)base;
     B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears them
@@ -1267,11 +1408,11 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    B.hit_bi = (int *)p;   p += 9 * npix * 4;
-    B.hit_t = (float *)p;  p += 9 * npix * 4;
+    B.hit_bi = (int *)p;   p += slots * 4;
+    B.hit_t = (float *)p;  p += slots * 4;
     p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    B.sh_bits = (unsigned long long *)p;   p += npix * 8;
-    B.pend_bits = (unsigned long long *)p; p += npix * 8;
+    B.sh_bits = (unsigned long long *)p;   p += words * 8;
+    B.pend_bits = (unsigned long long *)p; p += words * 8;
     B.pend_ray = (PendRay *)p;             p += (size_t)kMaxPend * sizeof(PendRay);
     B.near_n = B.pend_n + 1;
     B.near_list = (int *)p; p += (size_t)F.n_tris * 4;
@@ -1317,7 +1458,8 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const int bins = B.bins_x * B.bins_y;
     hipError_t e = hipMemsetAsync(B.bin_n, 0, big_counter_bytes(B), st);
     if (e != hipSuccess) return e;
-    const bool flags_fit = 9 * F.n_lights <= 64;
+    const bool lat = B.lat_w != 0;
+    const bool flags_fit = lat || 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, B.sups_x * B.sups_y), dim3(256), 0, st, F, d_tc, B);
@@ -1327,16 +1469,19 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((2 * bins + 255) / 256), dim3(256), 0, st, B, 2 * bins);
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
-    hipLaunchKernelGGL(rt_big_primary_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+    if (lat) hipLaunchKernelGGL(rt_big_primary_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+    else hipLaunchKernelGGL(rt_big_primary_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     if (!flags_fit) {
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
     } else if (F.n_lights > 0) {
         hipLaunchKernelGGL(rt_lit_class_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
-        hipLaunchKernelGGL(rt_shadow_hints_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        if (lat) hipLaunchKernelGGL(rt_shadow_hints_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        else hipLaunchKernelGGL(rt_shadow_hints_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         hipLaunchKernelGGL(rt_pending_lit_kernel, dim3(1024), dim3(256), 0, st, F, d_tc, B);
     }
-    hipLaunchKernelGGL(rt_big_shade_kernel, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    if (lat) hipLaunchKernelGGL(rt_big_shade_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    else hipLaunchKernelGGL(rt_big_shade_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     return hipGetLastError();
 }
 
