@@ -103,6 +103,8 @@ _SIGS = {
     "cg_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(Tri)]),
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
     "cg_rt_set_pending_cap": (C.c_int, [P, C.c_int]),
+    "cg_rt_scratch_info": (C.c_int, [P, C.POINTER(C.c_uint64)]),
+    "cg_rt_set_pool_caps": (C.c_int, [P, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
                                       C.POINTER(RtShard), P, P]),
@@ -480,6 +482,16 @@ class Context:
     def rt_set_pending_cap(self, cap):
         """Test hook: capacity of the large-scene pending shadow-ray queue (0 = default)."""
         self._check(self.lib.cg_rt_set_pending_cap(self.h, cap), "cg_rt_set_pending_cap")
+
+    def rt_set_pool_caps(self, sup=0, bin=0, sbin=0, sorted=0):
+        """Test hook: pin the large-scene pool capacities (all 0 = automatic)."""
+        self._check(self.lib.cg_rt_set_pool_caps(self.h, sup, bin, sbin, sorted), "cg_rt_set_pool_caps")
+
+    def rt_scratch_info(self):
+        """Large-scene scratch after the latest frame: dict(bytes, listed, capacity, overflows)."""
+        out = (C.c_uint64 * 4)()
+        self._check(self.lib.cg_rt_scratch_info(self.h, out), "cg_rt_scratch_info")
+        return dict(bytes=out[0], listed=out[1], capacity=out[2], overflows=out[3])
 
     def rt_render(self, cam, lights=None, n_lights=None):
         lights = default_lights() if lights is None else lights

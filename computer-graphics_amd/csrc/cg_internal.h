@@ -78,6 +78,13 @@ struct RtGrid {
     float blo[3], bhi[3];       // box of every possible hit position (triangles and spheres)
 };
 
+// Pool capacities (entries) of the large-scene path (cg_rt_big.hip): the
+// super-bin lists, the bin lists, the many-light shadow lists, the bin
+// lists' bucketed half-bin copies.
+struct BigCaps {
+    long long sup, bin, sbin, sorted;
+};
+
 // Frame arguments, passed by value (kernarg -> SGPRs).
 struct RtFrame {
     int W, H;

@@ -53,27 +53,47 @@ struct PendRay {
     int pix, bit;
 };
 
+// Pooled lists.  A list (the triangles a super-bin keeps, a bin's entries, a
+// bin's shadow candidates) is a sequence of chunks in one pool per kind, a
+// chunk being the survivors of one workgroup pass over <= 1024 candidates
+// (one pool reservation); chunk c of list k is chunk[k * nch + c].  Pool
+// capacities come from the host (cg_shim.hip: sized on a scene's first
+// frame, grown from the demand each later frame reports); a reservation past
+// the capacity marks the list overflowed and its consumers fall back to
+// every triangle -- slower, the same image -- while the full demand is still
+// counted for the host.
+struct Chunk {
+    int off, n;
+};
+enum { kPoolSup = 0, kPoolBin = 1, kPoolSbin = 2, kPoolSorted = 3 };
+
 struct BigBufs {
-    int *bin_n;                   // [n_bins]
-    // primary bin lists with keys: key bits << 32 | triangle, unsorted and by bucket
-    unsigned long long *bin_ent;                       // [n_bins][cap], unsorted
-    unsigned long long *bin_pbox, *bin_pbox2;          // [n_bins][cap]: projected boxes (proj_box16) for the
+    // primary bin lists with keys: key bits << 32 | triangle, unsorted (pool) and by bucket
+    unsigned long long *bin_ent;                       // [cap_bin]
+    unsigned long long *bin_pbox, *bin_pbox2;          // [cap_bin]: projected boxes (proj_box16) for the
                                                        // bin's left / right half, same order
-    // per half-bin (sub = 2 bin + half): the entries whose box meets the half, by bucket
-    unsigned long long *bin_sorted, *bin_spbox;        // [2 n_bins][cap]
+    Chunk *bin_chunk;             // [n_bins][nch]
+    int *bin_nch;                 // [n_bins]: chunks in use
+    int *bin_pre, *bin_tot;       // [n_bins][nch]: entries before each chunk; [n_bins]: list sizes
+    // the bin lists compacted (rt_bin_count_kernel): bin b at [bin_base[b], + bin_tot[b])
+    unsigned long long *flat_ent, *flat_pbox, *flat_pbox2;   // [cap_bin]
+    int *bin_base;                // [n_bins]
+    // per half-bin (sub = 2 bin + half): the entries whose box meets the half, by bucket (global offsets)
+    unsigned long long *bin_sorted, *bin_spbox;        // [cap_sorted]
     int *bkt_cnt;                 // [2 n_bins][kDepthBuckets]: counts, then scatter cursors
     int *bkt_off;                 // [2 n_bins][kDepthBuckets + 1]
     unsigned *bkt_min_inv;        // [2 n_bins][kDepthBuckets]: ~(smallest key bits) (0 = empty)
     unsigned *key_lo_inv, *key_hi;                     // [n_bins]: ~min / max bits of the positive keys
-    int *sbin_list, *sbin_n;
-    int *hit_bi;                  // [9][rows_out * W]
+    int *sbin_pool;               // [cap_sbin] shadow candidates of the many-light path
+    Chunk *sbin_chunk;            // [n_bins][nch]
+    int *hit_bi;                  // ray slots (K1): closest hit index
     float *hit_t;
     ShadowBox *wave_box;          // [tiles_y][tiles_x]
     ShadowBox *bin_box;           // [n_bins]
     RtGrid grid;
     // shadow verdicts (9 * n_lights <= 64): per pixel, bit s * n_lights + l
     unsigned long long *sh_bits, *pend_bits;
-    int *pend_n;                  // shadow rays left unresolved by K4 (counter, after bin_n/sbin_n)
+    int *pend_n;                  // shadow rays left unresolved by K4 (counter)
     struct PendRay *pend_ray;     // [kMaxPend]
     int max_pend;                 // queue capacity used (<= kMaxPend; lowered only by cg_rt_set_pending_cap)
     // certified lit search (K5): triangles near the light, the walk margin and
@@ -81,10 +101,17 @@ struct BigBufs {
     int *near_list, *near_n;      // [n_tris], counter (pend_n[1])
     float lit_M;
     double litD[3], lit_pn;
-    int cap, bins_x, bins_y, tiles_x, tiles_y;
+    int bins_x, bins_y, tiles_x, tiles_y;
     int lat_w, lat_h;             // lattice mode: (2 W + 1) x (2 rows + 1) points; 0 = per-pixel mode
-    int *sup_list, *sup_n;        // [n_sups][cap], [n_sups]: triangles the super-bin's certificate keeps
+    int *sup_pool;                // [cap_sup] triangles the super-bins' certificates keep
+    Chunk *sup_chunk;             // [n_sups][nch]
+    int *sup_pre, *sup_tot;       // [n_sups][nch], [n_sups] (as bin_pre / bin_tot)
+    int *sup_flat, *sup_base;     // [cap_sup]: the super lists compacted, super-bin s at sup_base[s]
     int sups_x, sups_y;
+    int nch;                      // chunks per list: ceil(n_tris / kBinTris)
+    unsigned long long *pool_n;   // [4] demand per pool (kPool*; the sorted pool's is its total)
+    long long cap_sup, cap_bin, cap_sbin, cap_sorted;  // pool capacities (entries)
+    int *sup_over, *bin_over, *sbin_over;              // [n_sups], [n_bins], [n_bins]: list overflowed
 };
 
 // ---------------------------------------------------------------------------
@@ -213,7 +240,130 @@ __device__ bool bin_half_bundle(const RtFrame &F, int bx, int by, int part, floa
     return true;
 }
 
-// Append the kept triangles of this workgroup to a bin list (one atomic per
+// Reserve tot pool entries (thread 0): the offset, or -1 past the capacity
+// (the list is then marked overflowed).  The demand is counted either way.
+__device__ __forceinline__ int pool_reserve(unsigned long long *pool_n, long long cap, int tot, int *over)
+{
+    if (!tot) return 0;
+    const unsigned long long g = atomicAdd(pool_n, (unsigned long long)tot);
+    if ((long long)g + tot > cap) {
+        *over = 1;
+        return -1;
+    }
+    return (int)g;
+}
+
+// Append this workgroup's kept triangles (kept[r]: triangle base + r*256 +
+// tid) to a pooled list as one chunk, recorded in *slot.
+__device__ __forceinline__ void pooled_append(const bool kept[4], int base, int *pool, unsigned long long *pool_n,
+                                              long long cap, Chunk *slot, int *over)
+{
+    __shared__ int s_w[4][4];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long m[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = __ballot(kept[r]);
+        if (lane == 0) s_w[r][w] = __popcll(m[r]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < 4; ++q) tot += s_w[r][q];
+        const int g = pool_reserve(pool_n, cap, tot, over);
+        *slot = Chunk{g < 0 ? 0 : g, g < 0 ? 0 : tot};
+        s_base = g;
+    }
+    __syncthreads();
+    if (s_base < 0) return;
+    int off = s_base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        int before = 0;
+        for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
+        if (kept[r]) pool[off + before + __popcll(m[r] & lt)] = base + r * 256 + (int)threadIdx.x;
+        for (int q = 0; q < 4; ++q) off += s_w[r][q];
+    }
+}
+
+// Prefix sums of the chunk tables (one workgroup per list): pre[c] = entries
+// of the list before chunk c, tot = the list's size.  Consumers then walk a
+// list by flat index in full 1024-entry passes, whatever its chunks' sizes.
+__global__ __launch_bounds__(1024) void rt_chunk_scan_kernel(const Chunk *__restrict__ tab, const int *__restrict__ ncs,
+                                                             int nch, int *__restrict__ pre, int *__restrict__ tot)
+{
+    const int list = blockIdx.x, nc = ncs ? ncs[list] : nch;
+    const Chunk *t = tab + (size_t)list * nch;
+    int *p = pre + (size_t)list * nch;
+    __shared__ int s_wave[16];
+    __shared__ int s_carry;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < nc; c0 += 1024) {
+        const int c = c0 + (int)threadIdx.x;
+        const int n = c < nc ? t[c].n : 0;
+        int x = n;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wave[w] = x;
+        __syncthreads();
+        int before = s_carry;
+        for (int q = 0; q < w; ++q) before += s_wave[q];
+        if (c < nc) p[c] = before + x - n;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[list] = s_carry;
+}
+
+// Exclusive prefix of n list sizes (one workgroup): where each list starts
+// in its compacted array.
+__global__ __launch_bounds__(1024) void rt_list_base_kernel(const int *__restrict__ tot, int n, int *__restrict__ base)
+{
+    __shared__ int s_wave[16];
+    __shared__ int s_carry;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += 1024) {
+        const int i = i0 + (int)threadIdx.x;
+        const int v = i < n ? tot[i] : 0;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wave[w] = x;
+        __syncthreads();
+        int before = s_carry;
+        for (int q = 0; q < w; ++q) before += s_wave[q];
+        if (i < n) base[i] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = before + x;
+        __syncthreads();
+    }
+}
+
+// The super lists' chunks copied into one contiguous array per super-bin.
+__global__ __launch_bounds__(256) void rt_sup_compact_kernel(BigBufs B)
+{
+    const int sup = blockIdx.y, c = blockIdx.x;
+    if (B.sup_over[sup]) return;
+    const Chunk ch = B.sup_chunk[(size_t)sup * B.nch + c];
+    int *dst = B.sup_flat + B.sup_base[sup] + B.sup_pre[(size_t)sup * B.nch + c];
+    for (int e = (int)threadIdx.x; e < ch.n; e += 256) dst[e] = B.sup_pool[ch.off + e];
+}
+
+// Append the kept triangles of this workgroup to a plain list (one atomic per
 // workgroup); kept[r] is this thread's verdict on triangle base + r*256 + tid.
 __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *list, int *count)
 {
@@ -312,20 +462,22 @@ __global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const Rt
 {
     const int sup = blockIdx.y;
     float x0, x1, y0, y1;
-    if (!sup_bundle(F, sup % B.sups_x, sup / B.sups_x, x0, x1, y0, y1)) return;
+    const bool ok = sup_bundle(F, sup % B.sups_x, sup / B.sups_x, x0, x1, y0, y1);
     const int base = blockIdx.x * kBinTris;
     bool kept[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = base + r * 256 + (int)threadIdx.x;
-        kept[r] = i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal);
+        kept[r] = ok && i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal);
     }
-    bin_append(kept, base, B.sup_list + (size_t)sup * B.cap, B.sup_n + sup);
+    pooled_append(kept, base, B.sup_pool, B.pool_n + kPoolSup, B.cap_sup, B.sup_chunk + (size_t)sup * B.nch + blockIdx.x,
+                  B.sup_over + sup);
 }
 
-// K0: camera-ray certificate per (bin, triangle), with the key: every float
-// distance fl(t |nd|) a ray of the bin computes for the triangle is >= key
-// (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23) since nd.z = f, :137).
+// K0: camera-ray certificate per (bin, triangle of its super list), with the
+// key: every float distance fl(t |nd|) a ray of the bin computes for the
+// triangle is >= key (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23)
+// since nd.z = f, :137).  One chunk of the bin list per super-list chunk.
 __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                              const cg_tri *__restrict__ tris, BigBufs B)
 {
@@ -334,8 +486,9 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
     if (!bin_bundle(F, bin % B.bins_x, bin / B.bins_x, x0, x1, y0, y1)) return;
     const int bx = bin % B.bins_x, by = bin / B.bins_x;
     const int sup = (bx / kSupBins) + (by / kSupBins) * B.sups_x;
-    const int ns = B.sup_n[sup];
-    const int *slist = B.sup_list + (size_t)sup * B.cap;
+    const bool all = B.sup_over[sup] != 0;               // overflowed super list: every triangle
+    const int ns = all ? F.n_tris : B.sup_tot[sup];
+    const int *slist = B.sup_flat + (all ? 0 : B.sup_base[sup]);
     __shared__ int s_w[4][4];
     __shared__ int s_base;
     __shared__ unsigned s_lo, s_hi;
@@ -351,7 +504,7 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int e = base + r * 256 + (int)threadIdx.x;
-        const int i = e < ns ? slist[e] : 0;
+        const int i = e < ns ? (all ? e : slist[e]) : 0;
         tri[r] = i;
         kept[r] = false;
         kbits[r] = 0u;
@@ -370,7 +523,7 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
         }
     }
     __syncthreads();
-    // append (one atomic per workgroup), and the bin's positive key range
+    // append (one reservation per pass), and the bin's positive key range
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned long long m[4];
@@ -397,25 +550,29 @@ __global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const Rt
         int tot = 0;
         for (int r = 0; r < 4; ++r)
             for (int q = 0; q < 4; ++q) tot += s_w[r][q];
-        s_base = tot ? atomicAdd(B.bin_n + bin, tot) : 0;
-        if (tot) {
+        const int g = pool_reserve(B.pool_n + kPoolBin, B.cap_bin, tot, B.bin_over + bin);
+        s_base = tot ? g : -1;
+        if (tot && g >= 0) {
+            B.bin_chunk[(size_t)bin * B.nch + atomicAdd(B.bin_nch + bin, 1)] = Chunk{g, tot};
             atomicMax(B.key_lo_inv + bin, s_lo);
             atomicMax(B.key_hi + bin, s_hi);
         }
     }
     __syncthreads();
-    int off = s_base;
+    if (s_base >= 0) {
+        int off = s_base;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        int before = 0;
-        for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
-        if (kept[r]) {
-            const size_t at = (size_t)bin * B.cap + off + before + __popcll(m[r] & lt);
-            B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)tri[r];
-            B.bin_pbox[at] = pbox[r];
-            B.bin_pbox2[at] = pbox2[r];
+        for (int r = 0; r < 4; ++r) {
+            int before = 0;
+            for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
+            if (kept[r]) {
+                const size_t at = (size_t)off + before + __popcll(m[r] & lt);
+                B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)tri[r];
+                B.bin_pbox[at] = pbox[r];
+                B.bin_pbox2[at] = pbox2[r];
+            }
+            for (int q = 0; q < 4; ++q) off += s_w[r][q];
         }
-        for (int q = 0; q < 4; ++q) off += s_w[r][q];
     }
     __syncthreads();                                        // s_w / s_base / s_lo reused by the next chunk
     }
@@ -433,12 +590,15 @@ __device__ __forceinline__ int depth_bucket(unsigned kbits, const BigBufs &B, in
 }
 
 // Per bin: bucket sizes and each bucket's smallest key (workgroups stride
-// over the list 1024 entries at a time).
+// over the bin's chunks).
 __global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                            const cg_tri *__restrict__ tris, BigBufs B)
 {
-    const int bin = blockIdx.y, n = B.bin_n[bin];
-    if ((int)blockIdx.x * 1024 >= n) return;
+    const int bin = blockIdx.y, nc = B.bin_nch[bin];
+    if ((int)blockIdx.x >= nc) return;
+    const Chunk *tab = B.bin_chunk + (size_t)bin * B.nch;
+    const int *pre = B.bin_pre + (size_t)bin * B.nch;
+    const size_t base = B.bin_base[bin];
     // an entry without a box for the whole bin (det's sign uncertain there)
     // gets one per half of the bin where the half's own certificate allows,
     // and none at all where it culls the triangle
@@ -453,28 +613,37 @@ __global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTr
         (&s_min[0][0])[threadIdx.x] = 0u;
     }
     __syncthreads();
-    const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
-    for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024)
-        for (int e = e0 + (int)threadIdx.x; e < min(n, e0 + 1024); e += 256) {
-            const size_t at = (size_t)bin * B.cap + e;
-            if (B.bin_pbox[at] == kProjAll) {
-                const int i = (int)(unsigned)(list[e] & 0xffffffffull);
+    // chunk by chunk, each entry also copied to its place in the compacted list
+    for (int c = blockIdx.x; c < nc; c += gridDim.x) {
+        const Chunk ch = tab[c];
+        const size_t dst = base + pre[c];
+        for (int e = (int)threadIdx.x; e < ch.n; e += 256) {
+            const size_t at = (size_t)ch.off + e;
+            const unsigned long long ent = B.bin_ent[at];
+            unsigned long long pb[2];
+            pb[0] = B.bin_pbox[at];
+            pb[1] = B.bin_pbox2[at];
+            if (pb[0] == kProjAll) {
+                const int i = (int)(unsigned)(ent & 0xffffffffull);
                 for (int h = 0; h < 2; ++h) {
                     PrimDet ph;
-                    unsigned long long b = kProjNone;
+                    pb[h] = kProjNone;
                     if (hv[h] && !cull_primary(tc[i], hx0[h], hx1[h], hy0[h], hy1[h], F.focal, &ph))
-                        b = proj_box16(tc[i], ph, tris[i], F.cam, F.focal);
-                    (h ? B.bin_pbox2 : B.bin_pbox)[at] = b;
+                        pb[h] = proj_box16(tc[i], ph, tris[i], F.cam, F.focal);
                 }
             }
-            const unsigned kb = (unsigned)(list[e] >> 32);
+            B.flat_ent[dst + e] = ent;
+            B.flat_pbox[dst + e] = pb[0];
+            B.flat_pbox2[dst + e] = pb[1];
+            const unsigned kb = (unsigned)(ent >> 32);
             const int b = depth_bucket(kb, B, bin);
             for (int h = 0; h < 2; ++h)
-                if (hv[h] && proj_meets((h ? B.bin_pbox2 : B.bin_pbox)[at], hx0[h], hx1[h], hy0[h], hy1[h])) {
+                if (hv[h] && proj_meets(pb[h], hx0[h], hx1[h], hy0[h], hy1[h])) {
                     atomicAdd(&s_cnt[h][b], 1);
                     atomicMax(&s_min[h][b], ~kb);
                 }
         }
+    }
     __syncthreads();
     if (threadIdx.x < 2 * kDepthBuckets && (&s_cnt[0][0])[threadIdx.x]) {   // [h][b] -> sub 2 bin + h
         atomicAdd(&B.bkt_cnt[2 * bin * kDepthBuckets + threadIdx.x], (&s_cnt[0][0])[threadIdx.x]);
@@ -482,33 +651,80 @@ __global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTr
     }
 }
 
-// Per half-bin: bucket offsets; the counts become the scatter cursors.
-__global__ void rt_bin_scan_kernel(BigBufs B, int subs)
+// Bucket offsets in the sorted pool, over every half-bin and bucket in order
+// (one workgroup; a half-wave per half-bin, a lane per bucket); the counts
+// become the scatter cursors, the total is the sorted pool's demand.  A
+// half-bin reaching past the pool's capacity marks its bin overflowed (K1
+// then walks every triangle; the scatter skips it).
+constexpr int kMaxSubs = 16384;               // half-bins of one frame (8192 x 4096 pixels)
+__global__ __launch_bounds__(1024) void rt_bin_scan_kernel(BigBufs B, int subs)
 {
-    const int bin = blockIdx.x * blockDim.x + threadIdx.x;   // sub-bin
-    if (bin >= subs) return;
-    int *cnt = B.bkt_cnt + bin * kDepthBuckets, *off = B.bkt_off + bin * (kDepthBuckets + 1);
-    int acc = 0;
-    for (int b = 0; b < kDepthBuckets; ++b) {
-        off[b] = acc;
-        const int c = cnt[b];
-        cnt[b] = acc;
-        acc += c;
+    static_assert(kDepthBuckets == 32, "one half-wave lane per bucket");
+    __shared__ int s_tot[kMaxSubs];
+    __shared__ int s_wave[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane & 31, hw = threadIdx.x >> 5;
+    // half-bin totals
+    for (int sub = hw; sub < subs; sub += 32) {
+        int x = B.bkt_cnt[sub * kDepthBuckets + hl];
+#pragma unroll
+        for (int o = 16; o; o >>= 1) x += __shfl_xor(x, o, 32);
+        if (hl == 0) s_tot[sub] = x;
     }
-    off[kDepthBuckets] = acc;
+    __syncthreads();
+    // exclusive prefix of the totals: thread t owns a run of `per` half-bins
+    const int per = (subs + 1023) / 1024;
+    const int s0 = min(subs, (int)threadIdx.x * per), s1 = min(subs, s0 + per);
+    int run = 0;
+    for (int sub = s0; sub < s1; ++sub) run += s_tot[sub];
+    int x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[w] = x;
+    __syncthreads();
+    int acc = x - run;
+    for (int q = 0; q < w; ++q) acc += s_wave[q];
+    if (threadIdx.x == 1023) B.pool_n[kPoolSorted] = (unsigned long long)(acc + run);
+    __syncthreads();                                 // every thread has read s_tot: overwrite with the bases
+    for (int sub = s0; sub < s1; ++sub) {
+        const int t = s_tot[sub];
+        s_tot[sub] = acc;
+        acc += t;
+    }
+    __syncthreads();
+    // per half-bin: bucket offsets = its base + exclusive prefix of its counts
+    for (int sub = hw; sub < subs; sub += 32) {
+        int *cnt = B.bkt_cnt + sub * kDepthBuckets, *off = B.bkt_off + sub * (kDepthBuckets + 1);
+        const int c = cnt[hl];
+        int y = c;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const int z = __shfl_up(y, o, 32);
+            if (hl >= o) y += z;
+        }
+        const int o0 = s_tot[sub] + y - c;
+        off[hl] = o0;
+        cnt[hl] = o0;
+        if (hl == 31) {
+            off[kDepthBuckets] = o0 + c;
+            if ((long long)(o0 + c) > B.cap_sorted) B.bin_over[sub >> 1] = 1;
+        }
+    }
 }
 
 // Per bin: each entry into the bucket lists of the half-bins its box meets
-// (one global reservation per half, bucket and 1024-entry chunk).
+// (one global reservation per half, bucket and chunk).
 __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs B)
 {
-    const int bin = blockIdx.y, n = B.bin_n[bin];
+    const int bin = blockIdx.y, n = B.bin_over[bin] ? 0 : B.bin_tot[bin];
+    const size_t base = B.bin_base[bin];
     float hx0[2], hx1[2], hy0[2], hy1[2];
     bool hv[2];
     for (int h = 0; h < 2; ++h)
         hv[h] = bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, h, hx0[h], hx1[h], hy0[h], hy1[h]);
     __shared__ int s_cnt[2][kDepthBuckets], s_base[2][kDepthBuckets];
-    const unsigned long long *list = B.bin_ent + (size_t)bin * B.cap;
     for (int e0 = (int)blockIdx.x * 1024; e0 < n; e0 += (int)gridDim.x * 1024) {
         if (threadIdx.x < 2 * kDepthBuckets) (&s_cnt[0][0])[threadIdx.x] = 0;
         __syncthreads();
@@ -522,9 +738,10 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs 
             ent[r] = 0ull;
             pb[r][0] = pb[r][1] = kProjNone;
             if (e < n) {
-                ent[r] = list[e];
-                pb[r][0] = B.bin_pbox[(size_t)bin * B.cap + e];
-                pb[r][1] = B.bin_pbox2[(size_t)bin * B.cap + e];
+                const size_t at = base + e;
+                ent[r] = B.flat_ent[at];
+                pb[r][0] = B.flat_pbox[at];
+                pb[r][1] = B.flat_pbox2[at];
                 bk[r] = depth_bucket((unsigned)(ent[r] >> 32), B, bin);
                 for (int h = 0; h < 2; ++h)
                     if (hv[h] && proj_meets(pb[r][h], hx0[h], hx1[h], hy0[h], hy1[h]))
@@ -540,7 +757,7 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs 
         for (int r = 0; r < 4; ++r)
             for (int h = 0; h < 2; ++h)
                 if (loc[r][h] >= 0) {
-                    const size_t at = (size_t)(2 * bin + h) * B.cap + s_base[h][bk[r]] + loc[r][h];
+                    const size_t at = (size_t)s_base[h][bk[r]] + loc[r][h];
                     B.bin_sorted[at] = ent[r];
                     B.bin_spbox[at] = pb[r][h];
                 }
@@ -637,8 +854,8 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
     const bool any = x0 <= x1;
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
     const int sub = 2 * bin + ((tx % kBinTilesX) < kBinTilesX / 2 ? 0 : 1);          // the wave's half-bin
-    const unsigned long long *list = B.bin_sorted + (size_t)sub * B.cap;
-    const unsigned long long *pboxes = B.bin_spbox + (size_t)sub * B.cap;
+    const unsigned long long *list = B.bin_sorted;   // global offsets (rt_bin_scan_kernel)
+    const unsigned long long *pboxes = B.bin_spbox;
     const int *boff = B.bkt_off + sub * (kDepthBuckets + 1);
     const unsigned *bmin_inv = B.bkt_min_inv + sub * kDepthBuckets;
     float best[NS], bt[NS], len[NS];
@@ -679,7 +896,15 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
             if (on[s]) lm = fmaxf(lm, best[s]);
         tb = wave_max(lm);
     };
-    for (int q = 0; any && q < kDepthBuckets; ++q) {
+    if (B.bin_over[bin]) {   // overflowed bin list: every triangle through the wave's certificate
+        for (int c0 = 0; any && c0 < F.n_tris; c0 += 64) {
+            q_w[lane] = c0 + lane;
+            __builtin_amdgcn_wave_barrier();
+            certify_walk(min(64, F.n_tris - c0));
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    for (int q = 0; any && !B.bin_over[bin] && q < kDepthBuckets; ++q) {
         const int b0 = boff[q], b1 = boff[q + 1];
         if (b0 == b1 || __uint_as_float(~bmin_inv[q]) > tb) continue;
         // the next chunk's entries are loaded while this one is scanned
@@ -786,16 +1011,17 @@ __global__ __launch_bounds__(256) void rt_bin_shadow_kernel(RtFrame F, const RtT
 {
     const int bin = blockIdx.y;
     const ShadowBox box = B.bin_box[bin];
-    if (!(box.lo[0] <= box.hi[0])) return;                         // no hits in this bin
+    const bool ok = box.lo[0] <= box.hi[0];                        // hits in this bin
     const vec3 lc = v3(F.lc[0], F.lc[1], F.lc[2]);
     const int base = blockIdx.x * kBinTris;
     bool kept[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = base + r * 256 + (int)threadIdx.x;
-        kept[r] = i < F.n_tris && !cull_shadow(tc[i], lc, F.lrho, box);
+        kept[r] = ok && i < F.n_tris && !cull_shadow(tc[i], lc, F.lrho, box);
     }
-    bin_append(kept, base, B.sbin_list + (size_t)bin * B.cap, B.sbin_n + bin);
+    pooled_append(kept, base, B.sbin_pool, B.pool_n + kPoolSbin, B.cap_sbin,
+                  B.sbin_chunk + (size_t)bin * B.nch + blockIdx.x, B.sbin_over + bin);
 }
 
 // Shadow ray of DirectLight (skeleton.cpp:370-394) for hit `pos` and light l.
@@ -837,15 +1063,24 @@ __device__ __forceinline__ vec3 big_direct_light(const RtFrame &F, const RtSpher
     return ((objColor * lc) * a) / area;                                 // :412
 }
 
-// any-hit of one shadow ray over a uniform list of triangle indices: the
-// blocking triangle, or -1.
-__device__ __forceinline__ int any_hit(const RtTri *__restrict__ tc, const int *list, int n, const ShadowRay &q)
+// any-hit of one shadow ray over a bin's certified shadow list (uniform per
+// wave; every triangle when the list overflowed).
+__device__ __forceinline__ bool any_hit_bin(const RtTri *__restrict__ tc, const BigBufs &B, int n_tris, int bin,
+                                            const ShadowRay &q)
 {
-    for (int i = 0; i < n; ++i) {
-        const int k = __builtin_amdgcn_readfirstlane(list[i]);
-        if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) return k;
+    if (B.sbin_over[bin]) {
+        for (int k = 0; k < n_tris; ++k)
+            if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) return true;
+        return false;
     }
-    return -1;
+    for (int c = 0; c < B.nch; ++c) {
+        const Chunk ch = B.sbin_chunk[(size_t)bin * B.nch + c];
+        for (int e = 0; e < ch.n; ++e) {
+            const int k = __builtin_amdgcn_readfirstlane(B.sbin_pool[ch.off + e]);
+            if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) return true;
+        }
+    }
+    return false;
 }
 
 // Blocker search along the shadow segment S + t (L - P), t in [0, 1], through
@@ -1292,8 +1527,6 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
         // rays past the queue still carry pending bits: the lit search per lane
         const unsigned long long pleft = !kLat && flags_fit && F.n_lights > 0 ? B.pend_bits[pix] : 0ull;
         const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
-        const int *slist = B.sbin_list + (size_t)bin * B.cap;
-        const int sn = flags_fit ? 0 : B.sbin_n[bin];
         vec3 pc = v3(0.0f, 0.0f, 0.0f);
         bool valid = false;
         const vec3 ind = v3(F.indirect, F.indirect, F.indirect);
@@ -1322,7 +1555,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
                     ts = ((shadowed >> bit) & 1ull) != 0;
                     if (!ts && ((left >> bit) & 1ull)) ts = lit_blocked_lane(tc, B, q.origin, q.nd, q.len, q.rmag);
                 } else {
-                    ts = grid_blocker(B.grid, tc, q) >= 0 || any_hit(tc, slist, sn, q) >= 0;
+                    ts = grid_blocker(B.grid, tc, q) >= 0 || any_hit_bin(tc, B, F.n_tris, bin, q);
                 }
                 pc = pc + big_direct_light(F, sph, Lt, q, normal, oc, ts);
             }
@@ -1344,16 +1577,20 @@ static bool rt_big_lattice(const RtFrame &F)
     return F.nranks == 1 && F.n_lights <= 64 && F.W < (1 << 20) && F.H < (1 << 20);
 }
 
-BigBufs big_layout(const RtFrame &F, int cap)
+BigBufs big_layout(const RtFrame &F, const BigCaps &caps)
 {
     BigBufs B{};
-    B.cap = cap;
     B.bins_x = (F.W + kBinW - 1) / kBinW;
     B.bins_y = (F.rows_out + kBinH - 1) / kBinH;
     B.tiles_x = (F.W + 7) / 8;
     B.tiles_y = (F.rows_out + 7) / 8;
     B.sups_x = (B.bins_x + kSupBins - 1) / kSupBins;
     B.sups_y = (B.bins_y + kSupBins - 1) / kSupBins;
+    B.nch = std::max(1, (F.n_tris + kBinTris - 1) / kBinTris);
+    B.cap_sup = caps.sup;
+    B.cap_bin = caps.bin;
+    B.cap_sbin = caps.sbin;
+    B.cap_sorted = caps.sorted;
     const int rows = std::min(F.rows_out, F.H - F.row0);
     if (rt_big_lattice(F) && rows > 0) {
         B.lat_w = 2 * F.W + 1;
@@ -1367,7 +1604,7 @@ size_t big_counter_bytes(const BigBufs &B)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y;
     const size_t sups = (size_t)B.sups_x * B.sups_y;
-    return 2 * bins * 4 + 16 + 4 * bins * kDepthBuckets * 4 + 2 * bins * 4 + sups * 4;
+    return 4 * 8 + 16 + 4 * bins * kDepthBuckets * 4 + 2 * bins * 4 + bins * 4 + (sups + 2 * bins) * 4;
 }
 
 // Ray slots (hits) and verdict words of the mode.
@@ -1380,50 +1617,70 @@ static size_t big_words(const BigBufs &B, const RtFrame &F)
     return B.lat_w ? (size_t)B.lat_w * B.lat_h : (size_t)F.rows_out * F.W;
 }
 
-// Bytes of device scratch for big_layout(F, cap), and its carving.
+// Bytes of device scratch for big_layout(F, caps), and its carving: the
+// frame-sized arrays, the chunk tables, then the pools.
 size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
-    const size_t bins = (size_t)B.bins_x * B.bins_y;
+    const size_t bins = (size_t)B.bins_x * B.bins_y, sups = (size_t)B.sups_x * B.sups_y;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return big_counter_bytes(B) + bins * B.cap * 4 + (size_t)F.n_tris * 4 + 7 * bins * (size_t)B.cap * 8 +
-           (size_t)B.sups_x * B.sups_y * B.cap * 4 +
-           2 * bins * (kDepthBuckets + 1) * 4 + big_slots(B, F) * 8 + (tiles + bins) * sizeof(ShadowBox) +
-           2 * big_words(B, F) * 8 + (size_t)kMaxPend * sizeof(PendRay) + 1024;
+    return big_counter_bytes(B) + 2 * bins * (kDepthBuckets + 1) * 4 + (tiles + bins) * sizeof(ShadowBox) +
+           big_slots(B, F) * 8 + 2 * big_words(B, F) * 8 + (size_t)kMaxPend * sizeof(PendRay) +
+           (size_t)F.n_tris * 4 + (sups + 2 * bins) * B.nch * sizeof(Chunk) + (sups + bins) * (B.nch + 2) * 4 +
+           (size_t)B.cap_sup * 2 * 4 + (size_t)B.cap_sbin * 4 + (size_t)B.cap_bin * 6 * 8 + (size_t)B.cap_sorted * 2 * 8 +
+           8 * 64;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
 {
-    const size_t bins = (size_t)B.bins_x * B.bins_y, slots = big_slots(B, F), words = big_words(B, F);
+    const size_t bins = (size_t)B.bins_x * B.bins_y, sups = (size_t)B.sups_x * B.sups_y;
+    const size_t slots = big_slots(B, F), words = big_words(B, F);
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
     char *p = (char *)base;
-    B.bin_n = (int *)p;  p += bins * 4;          // counters first: one memset clears them
-    B.sbin_n = (int *)p; p += bins * 4;
-    B.pend_n = (int *)p; p += 16;
+    auto align = [&] { p = (char *)(((uintptr_t)p + 63) & ~(uintptr_t)63); };
+    B.pool_n = (unsigned long long *)p; p += 4 * 8;   // counters first: one memset clears them
+    B.pend_n = (int *)p;            p += 16;
+    B.near_n = B.pend_n + 1;
     B.bkt_cnt = (int *)p;           p += 2 * bins * kDepthBuckets * 4;
     B.bkt_min_inv = (unsigned *)p;  p += 2 * bins * kDepthBuckets * 4;
     B.key_lo_inv = (unsigned *)p;   p += bins * 4;
     B.key_hi = (unsigned *)p;       p += bins * 4;
-    B.sup_n = (int *)p;             p += (size_t)B.sups_x * B.sups_y * 4;
+    B.bin_nch = (int *)p;           p += bins * 4;
+    B.sup_over = (int *)p;          p += sups * 4;
+    B.bin_over = (int *)p;          p += bins * 4;
+    B.sbin_over = (int *)p;         p += bins * 4;
     B.bkt_off = (int *)p;           p += 2 * bins * (kDepthBuckets + 1) * 4;
-    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    align();
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
-    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    align();
     B.hit_bi = (int *)p;   p += slots * 4;
     B.hit_t = (float *)p;  p += slots * 4;
-    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    align();
     B.sh_bits = (unsigned long long *)p;   p += words * 8;
     B.pend_bits = (unsigned long long *)p; p += words * 8;
     B.pend_ray = (PendRay *)p;             p += (size_t)kMaxPend * sizeof(PendRay);
-    B.near_n = B.pend_n + 1;
-    B.near_list = (int *)p; p += (size_t)F.n_tris * 4;
-    B.sbin_list = (int *)p; p += bins * B.cap * 4;
-    p = (char *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    B.bin_ent = (unsigned long long *)p;    p += bins * (size_t)B.cap * 8;
-    B.bin_pbox = (unsigned long long *)p;   p += bins * (size_t)B.cap * 8;
-    B.bin_pbox2 = (unsigned long long *)p;  p += bins * (size_t)B.cap * 8;
-    B.bin_sorted = (unsigned long long *)p; p += 2 * bins * (size_t)B.cap * 8;
-    B.bin_spbox = (unsigned long long *)p;  p += 2 * bins * (size_t)B.cap * 8;
-    B.sup_list = (int *)p;
+    B.near_list = (int *)p;                p += (size_t)F.n_tris * 4;
+    align();
+    B.sup_chunk = (Chunk *)p;   p += sups * B.nch * sizeof(Chunk);
+    B.bin_chunk = (Chunk *)p;   p += bins * B.nch * sizeof(Chunk);
+    B.sbin_chunk = (Chunk *)p;  p += bins * B.nch * sizeof(Chunk);
+    B.sup_pre = (int *)p;       p += sups * B.nch * 4;
+    B.bin_pre = (int *)p;       p += bins * B.nch * 4;
+    B.sup_tot = (int *)p;       p += sups * 4;
+    B.bin_tot = (int *)p;       p += bins * 4;
+    B.sup_base = (int *)p;      p += sups * 4;
+    B.bin_base = (int *)p;      p += bins * 4;
+    align();
+    B.bin_ent = (unsigned long long *)p;    p += (size_t)B.cap_bin * 8;
+    B.bin_pbox = (unsigned long long *)p;   p += (size_t)B.cap_bin * 8;
+    B.bin_pbox2 = (unsigned long long *)p;  p += (size_t)B.cap_bin * 8;
+    B.bin_sorted = (unsigned long long *)p; p += (size_t)B.cap_sorted * 8;
+    B.bin_spbox = (unsigned long long *)p;  p += (size_t)B.cap_sorted * 8;
+    B.flat_ent = (unsigned long long *)p;   p += (size_t)B.cap_bin * 8;
+    B.flat_pbox = (unsigned long long *)p;  p += (size_t)B.cap_bin * 8;
+    B.flat_pbox2 = (unsigned long long *)p; p += (size_t)B.cap_bin * 8;
+    B.sup_pool = (int *)p;                  p += (size_t)B.cap_sup * 4;
+    B.sup_flat = (int *)p;                  p += (size_t)B.cap_sup * 4;
+    B.sbin_pool = (int *)p;
 }
 
 // Frame bounds of the lit search (K5): |r_k| = |fl(L - P)_k| over every
@@ -1448,26 +1705,40 @@ static void lit_bounds(BigBufs &B, const RtFrame &F, const RtGrid &G)
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
                          const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const cg_tri *d_tris,
-                         int pend_cap)
+                         int pend_cap, const BigCaps &caps, unsigned long long *h_demand, bool dry)
 {
-    BigBufs B = big_layout(F, F.n_tris);
+    BigBufs B = big_layout(F, caps);
+    if (2 * B.bins_x * B.bins_y > kMaxSubs) return hipErrorInvalidValue;   // rt_bin_scan_kernel's LDS table
     big_carve(B, F, scratch);
     B.grid = grid;
     B.max_pend = pend_cap > 0 ? std::min(pend_cap, kMaxPend) : kMaxPend;
     lit_bounds(B, F, grid);
     const int bins = B.bins_x * B.bins_y;
-    hipError_t e = hipMemsetAsync(B.bin_n, 0, big_counter_bytes(B), st);
+    hipError_t e = hipMemsetAsync(B.pool_n, 0, big_counter_bytes(B), st);
     if (e != hipSuccess) return e;
     const bool lat = B.lat_w != 0;
     const bool flags_fit = lat || 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, B.sups_x * B.sups_y), dim3(256), 0, st, F, d_tc, B);
+    const int sups = B.sups_x * B.sups_y;
+    hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(sups), dim3(1024), 0, st, B.sup_chunk, nullptr, B.nch, B.sup_pre,
+                       B.sup_tot);
+    hipLaunchKernelGGL(rt_list_base_kernel, dim3(1), dim3(1024), 0, st, B.sup_tot, sups, B.sup_base);
+    hipLaunchKernelGGL(rt_sup_compact_kernel, dim3(B.nch, sups), dim3(256), 0, st, B);
     hipLaunchKernelGGL(rt_bin_primary_kernel, dim3(std::min(64, (int)bgrid.x), bins), dim3(256), 0, st, F, d_tc,
                        d_tris, B);
+    hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(bins), dim3(1024), 0, st, B.bin_chunk, B.bin_nch, B.nch, B.bin_pre,
+                       B.bin_tot);
+    hipLaunchKernelGGL(rt_list_base_kernel, dim3(1), dim3(1024), 0, st, B.bin_tot, bins, B.bin_base);
     const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
-    hipLaunchKernelGGL(rt_bin_scan_kernel, dim3((2 * bins + 255) / 256), dim3(256), 0, st, B, 2 * bins);
+    hipLaunchKernelGGL(rt_bin_scan_kernel, dim3(1), dim3(1024), 0, st, B, 2 * bins);
+    if (dry) {   // sizing pass (cg_shim.hip): only the lists, for their demand
+        if (h_demand)
+            e = hipMemcpyAsync(h_demand, B.pool_n, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+        return e != hipSuccess ? e : hipGetLastError();
+    }
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
     if (lat) hipLaunchKernelGGL(rt_big_primary_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     else hipLaunchKernelGGL(rt_big_primary_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
@@ -1482,6 +1753,10 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     }
     if (lat) hipLaunchKernelGGL(rt_big_shade_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     else hipLaunchKernelGGL(rt_big_shade_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    if (h_demand) {   // the pools' demand, for the host's sizing (cg_shim.hip)
+        e = hipMemcpyAsync(h_demand, B.pool_n, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
@@ -1556,9 +1831,9 @@ bool rt_grid_build(const cg_tri *t, int n, RtGrid &g, std::vector<int> &start, s
     return true;
 }
 
-size_t rt_big_scratch_bytes(const RtFrame &F)
+size_t rt_big_scratch_bytes(const RtFrame &F, const BigCaps &caps)
 {
-    BigBufs B = big_layout(F, F.n_tris);
+    BigBufs B = big_layout(F, caps);
     return big_scratch_bytes(B, F);
 }
 

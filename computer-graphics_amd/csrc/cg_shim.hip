@@ -26,9 +26,9 @@ hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, con
 bool rt_use_lattice(const RtFrame &);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
-                         uint32_t *, hipStream_t, const cg_tri *, int);
+                         uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, bool);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
-size_t rt_big_scratch_bytes(const RtFrame &);
+size_t rt_big_scratch_bytes(const RtFrame &, const BigCaps &);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
 hipError_t launch_rt_pack_rgb24(const uint32_t *, int, int, int, int, uint8_t *, hipStream_t);
 hipError_t launch_rt_assemble(const uint8_t *, const RtBlocks &, int, uint32_t *, size_t, hipStream_t);
@@ -91,6 +91,17 @@ struct cg_ctx {
     DevBuf ptc[2], pshade[2], plat[2], psup[2];
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     int pend_cap = 0;                   // cg_rt_set_pending_cap (0 = default)
+    // large-scene pools (cg_rt_big.hip): capacities in entries, sized on the
+    // scene's first frame, then grown from the demand later frames report
+    BigCaps big_caps{};
+    bool big_sized = false;
+    long long big_key = -1;                     // frame shape / path the pools were sized for
+    bool big_fixed = false;                     // cg_rt_set_pool_caps: capacities pinned (test hook)
+    unsigned long long *big_demand = nullptr;   // pinned [4]: the latest frame's demand
+    hipEvent_t big_ev = nullptr;
+    bool big_ev_live = false;
+    unsigned long long big_last[4] = {};
+    long long big_overflows = 0;
     std::vector<cg_tri> tris_host;      // the scene as uploaded (cg_dist's column window)
     std::vector<cg_sphere> sph_host;
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
@@ -244,7 +255,12 @@ extern "C" void cg_destroy(cg_ctx *c)
     DevBuf *bufs[] = {&c->tris, &c->tc, &c->shade, &c->sph, &c->frame,
                       &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights, &c->big,
                       &c->gstart, &c->gtris};
+    if (c->big_ev) {
+        (void)hipEventSynchronize(c->big_ev);
+        (void)hipEventDestroy(c->big_ev);
+    }
     for (DevBuf *b : bufs) b->release();
+    if (c->big_demand) (void)hipHostFree(c->big_demand);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
     for (int k = 0; k < cg_ctx::kRastLanes; ++k) {
         if (c->lanes[k]) cg_destroy(c->lanes[k]);
@@ -295,6 +311,7 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     c->tris_host.assign(tris, tris + n_tris);
     c->sph_host.assign(spheres, spheres + n_spheres);
     c->grid = RtGrid{};
+    c->big_sized = false;   // the next large-scene frame sizes the pools
     if (n_tris > 64) {   // large scene: grid for the shadow-ray blocker search
         std::vector<int> gs, gt;
         RtGrid g{};
@@ -439,6 +456,35 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     return set_lights(c, lights, n_lights, st, F);
 }
 
+static bool big_observe(cg_ctx *c, bool sizing);
+
+extern "C" int cg_rt_scratch_info(cg_ctx *c, uint64_t *out)
+{
+    if (!c || !out) return CG_E_INVALID;
+    if (c->big_ev_live) {
+        CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
+        big_observe(c, false);
+    }
+    const unsigned long long *d = c->big_last;
+    out[0] = c->big.bytes;
+    out[1] = d[0] + d[1] + d[2] + d[3];
+    out[2] = (uint64_t)(c->big_caps.sup + c->big_caps.bin + c->big_caps.sbin + c->big_caps.sorted);
+    out[3] = (uint64_t)c->big_overflows;
+    return CG_OK;
+}
+
+extern "C" int cg_rt_set_pool_caps(cg_ctx *c, long long sup, long long bin, long long sbin, long long sorted)
+{
+    if (!c || sup < 0 || bin < 0 || sbin < 0 || sorted < 0) return CG_E_INVALID;
+    if (c->stream) CG_TRY(c, hipDeviceSynchronize(), "drain before resizing pools");
+    c->big_fixed = sup > 0 || bin > 0 || sbin > 0 || sorted > 0;
+    c->big_caps = c->big_fixed ? BigCaps{sup, bin, sbin, sorted} : BigCaps{};
+    c->big_sized = false;
+    c->big_key = -1;
+    c->big_overflows = 0;
+    return CG_OK;
+}
+
 extern "C" int cg_rt_set_pending_cap(cg_ctx *c, int cap)
 {
     if (!c || cap < 0) return CG_E_INVALID;
@@ -479,6 +525,78 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t 
     return CG_OK;
 }
 
+// The large-scene pools' demand of the latest finished frame: capacities grow
+// to 1.25x a demand that came within 80 % of them (so steady frames neither
+// overflow nor hold more than ~1.6x what they list); a sizing frame sets them
+// to 1.25x its demand either way.  True when the frame overflowed a pool (it
+// was still right: the consumers fell back to every triangle).
+static bool big_observe(cg_ctx *c, bool sizing = false)
+{
+    std::memcpy(c->big_last, c->big_demand, sizeof(c->big_last));
+    const unsigned long long *d = c->big_last;
+    long long *cap[4] = {&c->big_caps.sup, &c->big_caps.bin, &c->big_caps.sbin, &c->big_caps.sorted};
+    bool over = false;
+    for (int k = 0; k < 4; ++k) {
+        const long long need = (long long)d[k];
+        over |= need > *cap[k];
+        if (!c->big_fixed && (sizing || need * 5 > *cap[k] * 4))
+            *cap[k] = std::min<long long>(need + need / 4 + 4096, (1ll << 31) - 1);
+    }
+    if (!sizing) c->big_overflows += over;
+    c->big_ev_live = false;
+    return over;
+}
+
+// Large scene: binned certificates (cg_rt_big.hip).  The first frame of a
+// scene (or of a new frame shape / path) is sized first: dry passes of the
+// list kernels alone report the pools' demand until it fits (a pass in which
+// a list overflowed under-counts what depends on it).  Later frames stay
+// asynchronous and grow the pools for the next ones from their reported
+// demand; a frame that still overflows renders through the fallback.
+static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
+{
+    if (!c->big_demand) {
+        CG_TRY(c, hipHostMalloc((void **)&c->big_demand, 4 * sizeof(unsigned long long), hipHostMallocDefault),
+               "alloc pool demand");
+        std::memset(c->big_demand, 0, 4 * sizeof(unsigned long long));
+        CG_TRY(c, hipEventCreateWithFlags(&c->big_ev, hipEventDisableTiming), "pool event");
+    }
+    if (c->big_caps.sup == 0) {   // first guess; the first frame corrects it
+        const long long g = 2ll * F.n_tris + 65536;
+        c->big_caps = BigCaps{g, g, 4096, 2 * g};
+    }
+    // a new frame shape or path (lattice / per-pixel, many lights) is sized again
+    bool ident = true;
+    for (int k = 0; k < 16; ++k) ident &= F.R[k] == ((k % 5 == 0) ? 1.0f : 0.0f);
+    const int lclass = F.n_lights == 0 ? 0 : F.n_lights <= 7 ? 1 : F.n_lights <= 64 ? 2 : 3;
+    const long long key = ((((long long)F.W * 65536 + F.rows_out) * 4 + lclass) * 2 + ident) * 2 + (F.nranks == 1);
+    if (key != c->big_key) {
+        c->big_key = key;
+        c->big_sized = false;
+    }
+    if (c->big_fixed) c->big_sized = true;
+    if (c->big_ev_live && hipEventQuery(c->big_ev) == hipSuccess) big_observe(c);
+    for (int pass = 0; pass < 6; ++pass) {
+        const bool dry = !c->big_sized && pass < 5;
+        const size_t need = rt_big_scratch_bytes(F, c->big_caps);
+        if ((need > c->big.bytes || need < c->big.bytes / 2) && c->big.p) {   // grow, or give back a sized-down half
+            CG_TRY(c, hipDeviceSynchronize(), "drain before resizing scratch");
+            c->big.release();
+        }
+        CG_TRY(c, c->big.ensure(need), "alloc large-scene scratch");
+        CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
+                                c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap, c->big_caps,
+                                c->big_demand, dry),
+               "rt_big launch");
+        CG_TRY(c, hipEventRecord(c->big_ev, st), "pool event");
+        c->big_ev_live = true;
+        if (!dry) break;
+        CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
+        if (!big_observe(c, true)) c->big_sized = true;   // fits: the next pass renders
+    }
+    return CG_OK;
+}
+
 static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
 {
     unsigned long long *lat = nullptr;
@@ -495,14 +613,7 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
     }
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)c->tc.p,
                                 (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
-    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) {
-        // large scene: binned certificates (cg_rt_big.hip)
-        CG_TRY(c, c->big.ensure(rt_big_scratch_bytes(F)), "alloc large-scene scratch");
-        CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
-                                c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap),
-               "rt_big launch");
-        return CG_OK;
-    }
+    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st);
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                (const RtSphere *)c->sph.p, lat, d_out, st), "rt_pixel launch");
     return CG_OK;

@@ -205,6 +205,15 @@ int cg_rt_probe_direct_light(cg_ctx *ctx, const cg_isect *isects, const cg_light
  * default, 65536).  Rays past the queue are searched per pixel by the shading
  * kernel instead; the image is the same either way. */
 int cg_rt_set_pending_cap(cg_ctx *ctx, int cap);
+/* Large-scene scratch after the latest frame (waits for it): out[0] device
+ * bytes held, out[1] entries the frame listed in the pools (super-bin, bin,
+ * bucketed and shadow lists), out[2] the pools' capacity in entries, out[3]
+ * frames that overflowed a pool (rendered correctly through the fallback). */
+int cg_rt_scratch_info(cg_ctx *ctx, uint64_t *out);
+/* Test hook: pin the large-scene pool capacities (entries: super-bin, bin,
+ * many-light shadow and bucketed lists; all 0 = automatic sizing).  Lists past a capacity take the fallback over every triangle; the
+ * image is the same. */
+int cg_rt_set_pool_caps(cg_ctx *ctx, long long sup, long long bin, long long sbin, long long sorted);
 
 /* ---- multi-GPU raytracer ------------------------------- */
 /* One process per GPU.  The reference renders every pixel of Draw

@@ -43,7 +43,7 @@ typedef struct { cgo_v4 position; float distance; int triangleIndex; int sphereI
 /* raytracer/Source/skeleton.cpp:47-50 */
 typedef struct { cgo_v4 position; cgo_v3 colour; } cgo_light;
 
-#define CGO_MAX_LIGHTS 64   /* C4's 8x8 area light */
+#define CGO_MAX_LIGHTS 128  /* C4: 8x8 area light; the large-scene tests: 9x9 */
 
 /* Frame parameters = the reference's RT globals (skeleton.cpp:56-60). */
 typedef struct {

@@ -45,7 +45,7 @@ class Light(C.Structure):
 class RtParams(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("focal", C.c_float), ("camera", V4),
                 ("R", C.c_float * 16), ("indirect", C.c_float), ("n_lights", C.c_int),
-                ("lights", Light * 64)]   # CGO_MAX_LIGHTS
+                ("lights", Light * 128)]   # CGO_MAX_LIGHTS
 
 
 class RtCounters(C.Structure):

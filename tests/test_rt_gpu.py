@@ -383,14 +383,21 @@ def test_rt_c5_1m_triangles_sampled(rt):
     _set_scene(rt, cfg)
     try:
         argb, st = rt.rt_render(_cam(cfg), _lights(cfg))
+        again, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+        scratch = rt.rt_scratch_info()
     finally:
         _set_scene(rt, {})
+    assert np.array_equal(again, argb)
     xy = _sample_xy(W, H, 768, 5)
     xy[-128:] = np.stack([np.random.default_rng(6).integers(W // 2 - 300, W // 2 + 300, 128),
                           np.random.default_rng(7).integers(H // 2 - 300, H // 2 + 300, 128)], 1)   # in the cloud
     ref = oracle.rt_draw_pixels(mg.rt_params_of(cfg), xy, scene=mg.rt_oracle_scene(cfg),
                                 threads=min(16, os.cpu_count() or 8))
     got = argb.reshape(H, W)[xy[:, 1], xy[:, 0]]
+    # the pools were sized on this first frame: capacity within 2x of what it listed
+    info = scratch
+    assert info["capacity"] <= 2 * info["listed"], info
+    assert info["bytes"] < (4 << 30), info
     bad = np.flatnonzero(got != ref)
     assert bad.size == 0, f"{bad.size} differ, first at {xy[bad[:4]]}: gpu {got[bad[:4]]} ref {ref[bad[:4]]}"
     assert (got != 0x80000000).sum() > 100      # the sample does see the cloud
