@@ -802,8 +802,9 @@ __device__ __forceinline__ bool lat_unit_keeps(const RtFrame &F, const RtTri &c,
     return !own_shadow_rejects(T, c, pd, thi, F.cam, X, X, y0, y1, F.focal, Lp, F.lrho, lo, hi);
 }
 
-constexpr int kLatHalfH = 8;                        // pixel rows per half
-constexpr int kLatHalfRows = 2 * kLatHalfH + 1;     // lattice rows per half
+constexpr int kLatHalfH = 5;                        // pixel rows per part (sweep)
+constexpr int kLatHalfRows = 2 * kLatHalfH + 1;     // lattice rows per part
+constexpr int kLatParts = (kLatTileH + kLatHalfH - 1) / kLatHalfH;
 constexpr int kLatMaxLights = 64;
 // Column-buffer swizzle: light l of (row r, component c) sits at slot
 // l ^ lat_swz(r, c).  The folding lanes read the same light group of 24
@@ -868,14 +869,14 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     // forms it below), plus the own-triangle certificate when every hit of the
     // unit lies on one triangle -- the same exact functions as
     // rt_tile_cert_kernel, over a box of up to 17 points instead of the tile's.
-    __shared__ unsigned long long s_umask[2][kLatW];
+    __shared__ unsigned long long s_umask[kLatParts][kLatW];
     // the units' boxes and sole hit triangles (-1: several, -2: no hit) live
     // in the column buffers, which the sweep below has not started using yet
-    static_assert(sizeof(s_dl) >= 2 * kLatW * 7 * sizeof(float), "unit scratch");
+    static_assert(sizeof(s_dl) / 2 >= kLatParts * kLatW * 6 * sizeof(float), "unit scratch");
     float(*s_ubox)[kLatW][6] = (float(*)[kLatW][6]) & s_dl[0][0][0][0];
     int(*s_uone)[kLatW] = (int(*)[kLatW]) & s_dl[1][0][0][0];
     const int nhalf = (G.nv + kLatHalfH - 1) / kLatHalfH;
-    if (threadIdx.x < 2 * kLatW) {
+    if (threadIdx.x < kLatParts * kLatW) {
         const int h = threadIdx.x / kLatW, cx = threadIdx.x - h * kLatW;
         if (h < nhalf && cx < cols) {
             const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
@@ -1051,7 +1052,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
     lat_signal(frame_done, blockIdx.z);
 }
 
-__global__ __launch_bounds__(kRtThreads, 4) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, 5) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                           const RtShade *__restrict__ shade,
                                                                           const RtSphere *__restrict__ sph,
                                                                           const unsigned long long *__restrict__ lat_masks,
