@@ -329,7 +329,8 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
 }
 
 // Colour mode 0: fill -> post state, 4 bytes per pixel: 1 + the row record of
-// the last shading fragment (0 none) | the shadow mark << 31.  The post-pass
+// the last shading fragment (0 none) | the shadow mark << 31; 2 bytes (the
+// mark in bit 15) when a row holds fewer than 32768 records (A.state16).  The post-pass
 // rebuilds that fragment from the record -- zinv = lz + sz * i (:543) and the
 // pos3d numerators with the same float ops, the normal, the texels -- and
 // evaluates calculateIllumination there, so the fill keeps only what its
@@ -422,7 +423,8 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
     }
     if (x < A.W) {
         const size_t o = (size_t)y * A.W + x;
-        state[o] = (uint32_t)(win + 1) | (shadow ? kStShadow : 0u);
+        if (A.state16) ((uint16_t *)state)[o] = (uint16_t)((win + 1) | (shadow ? 0x8000 : 0));
+        else state[o] = (uint32_t)(win + 1) | (shadow ? kStShadow : 0u);
         if (depth_out) depth_out[o] = depth;
         if (shadow_out) shadow_out[o] = shadow;
     }
@@ -546,6 +548,12 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
     if (g < 0) return;
     const int gx0 = m * kPostTW, gy0 = g * kPostTH;
     const uint32_t *st4 = static_cast<const uint32_t *>(state_v);
+    const uint16_t *st2 = static_cast<const uint16_t *>(state_v);
+    auto state_at = [&](size_t o) -> uint32_t {   // the 4-byte form
+        if (!A.state16) return st4[o];
+        const uint32_t v = st2[o];
+        return (v & 0x7fffu) | ((v >> 15) << 31);
+    };
     const float4 *st16 = static_cast<const float4 *>(state_v);
     // all global loads first (shadow marks, shade state), so each thread has them in flight together
     constexpr int kShR = (kPostSH * kPostSW + 255) / 256, kStR = (kPostHH * kPostHW + 255) / 256;
@@ -557,7 +565,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         const int gx = gx0 - 2 + cx, gy = gy0 - 2 + cy;
         const bool in = i < kPostSH * kPostSW && gx >= 0 && gy >= 0 && gx < W && gy < H;
         if (DIRECT) shv[r] = in ? sh[(size_t)gy * W + gx] : 0;
-        else shv[r] = in ? (int)(st4[(size_t)gy * W + gx] >> 31) : 0;
+        else shv[r] = in ? (int)(state_at((size_t)gy * W + gx) >> 31) : 0;
     }
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
@@ -581,7 +589,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
                 const bool tri = tb >= 0 && !(tb & kStateDirect);
                 shade3c(A, s4, tri ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f}, sc, lo, hi);
             } else {
-                shade_from_record<TEX>(tris, A, recs + (size_t)gy * A.n, st4[o], gx, gy, sc, lo, hi);
+                shade_from_record<TEX>(tris, A, recs + (size_t)gy * A.n, state_at(o), gx, gy, sc, lo, hi);
             }
             if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
         }
@@ -755,6 +763,7 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
         return ctx_invalid(c, "marble: normalMap_marble[y * 2000 + x] would index past the map");
     A.textured = (tex_mask & 0xe) != 0;
     A.use_inv = p->yaw != 0.0f;
+    A.state16 = p->colour_mode == 0 && nn < 32768;
     A.cam[0] = p->camera.x; A.cam[1] = p->camera.y; A.cam[2] = p->camera.z; A.cam[3] = p->camera.w;
     mat4_inverse_glm(p->R, A.Rinv);
     hipEvent_t e0, e1;

@@ -36,6 +36,7 @@ struct RastArgs {
     float cam[4];           // cameraPos
     float Rinv[16];         // glm::inverse(R), column-major
     RastTexMaps tx;
+    int state16;            // colour mode 0: fill -> post state in 2 bytes per pixel (n < 32768)
 };
 
 struct RastHdr {
