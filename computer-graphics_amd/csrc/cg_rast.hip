@@ -316,10 +316,8 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
             RowRec r;
             r.lx = sp.lx; r.rx = sp.rx;
             r.lz = sp.lz; r.sz = sp.sz; r.lX = sp.lX; r.sX = sp.sX; r.lY = sp.lY; r.sY = sp.sY;
-            r.t = t;
+            r.t_sh = (unsigned)t | (T.color.x >= 0 ? 0u : 0x80000000u);
             r.first_x = (t == ft && h.fy == y) ? h.fx : -1;
-            r.shadow = T.color.x >= 0 ? 0 : 1;
-            r.nx = T.normal.x; r.ny = T.normal.y; r.nz = T.normal.z;
             r.tex = T.texture; r.index = T.index;
             recs[(size_t)y * A.n + c + __popcll(below)] = r;
         }
@@ -376,7 +374,7 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
         bool ov = false;
         if (q < cnt) {
             const RowRec &mr = rr[q];
-            mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = mr.shadow;
+            mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = rec_shadow(mr);
             if (TEX) {
                 mtex = mr.tex; midx = mr.index;
                 mlX = mr.lX; msX = mr.sX; mlY = mr.lY; msY = mr.sY;
@@ -514,7 +512,9 @@ __device__ __forceinline__ void shade_from_record(const cg_rtri *__restrict__ tr
     const float fi = (float)(x - r.lx);
     const float z = r.lz + (r.sz * fi);                                    // :543, as the fill evaluated it
     const float X = r.lX + (r.sX * fi), Y = r.lY + (r.sY * fi);            // :547-548 numerators
-    vec3 N = v3(r.nx, r.ny, r.nz);
+    const int t = rec_t(r);
+    const cg_vec4 tn = tris[t].normal;
+    vec3 N = v3(tn.x, tn.y, tn.z);
     int tex = 0;
     uint32_t texel = 0u;
     if (TEX && r.tex != 0 && rast_tex_present(A, r.tex)) {
@@ -522,8 +522,8 @@ __device__ __forceinline__ void shade_from_record(const cg_rtri *__restrict__ tr
         N = rast_tex_normal(A, tex, r.index, z, X, Y, x, y, N, texel);
     }
     const vec3 D = illum_D(A, z, X, Y, N);                                 // :580-585 (:590-645)
-    const float4 s4 = make_float4(__int_as_float(r.t | (x == r.first_x ? (1 << 30) : 0)), D.x, D.y, D.z);
-    shade3c(A, s4, tris[r.t].color, sc, lo, hi, tex, texel);
+    const float4 s4 = make_float4(__int_as_float(t | (x == r.first_x ? (1 << 30) : 0)), D.x, D.y, D.z);
+    shade3c(A, s4, tris[t].color, sc, lo, hi, tex, texel);
 }
 
 template <bool DIRECT, bool TEX>
@@ -764,6 +764,7 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     A.textured = (tex_mask & 0xe) != 0;
     A.use_inv = p->yaw != 0.0f;
     A.state16 = p->colour_mode == 0 && nn < 32768;
+    A.tris = d_tris;
     A.cam[0] = p->camera.x; A.cam[1] = p->camera.y; A.cam[2] = p->camera.z; A.cam[3] = p->camera.w;
     mat4_inverse_glm(p->R, A.Rinv);
     hipEvent_t e0, e1;

@@ -46,7 +46,7 @@ __device__ __forceinline__ RecLane rec_lane(const RowRec *rr, int q, int cnt, in
     RecLane r{0, 0, 0, 0.f, 0.f, false};
     if (q < cnt) {
         const RowRec &m = rr[q];
-        r.lx = m.lx; r.rx = m.rx; r.lz = m.lz; r.sz = m.sz; r.shd = m.shadow;
+        r.lx = m.lx; r.rx = m.rx; r.lz = m.lz; r.sz = m.sz; r.shd = rec_shadow(m);
         r.ov = !(r.rx - 1 < x0 || r.lx > x0 + 63);
     }
     return r;
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(64) void rast_count_kernel(RastArgs A, const RowRec
         }
     }
     __syncthreads();
-    for (int i = lane; i < cnt; i += 64) pc[(size_t)rr[i].t * A.H + y] = s_cnt[i];
+    for (int i = lane; i < cnt; i += 64) pc[(size_t)rec_t(rr[i]) * A.H + y] = s_cnt[i];
 }
 
 // block-wide inclusive scan of v (256 threads); `total` = the block's sum
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(64) void rast_fill_rand_kernel(RastArgs A0, const R
     const RowRec *rr = recs + (size_t)y * A.n;
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int i = lane; i < cnt; i += 64) {
-        const int t = rr[i].t;
+        const int t = rec_t(rr[i]);
         s_run[i] = tbase[t] + pc[(size_t)t * A.H + y];
     }
     __syncthreads();
@@ -254,7 +254,8 @@ __global__ __launch_bounds__(64) void rast_fill_rand_kernel(RastArgs A0, const R
                 const int i = x - r.lx;
                 const float X = r.lX + (r.sX * (float)i);                // :547-548 numerators
                 const float Y = r.lY + (r.sY * (float)i);
-                const vec3 D = illum_D(A, depth, X, Y, v3(r.nx, r.ny, r.nz));
+                const cg_vec4 tn = A.tris[rec_t(r)].normal;
+                const vec3 D = illum_D(A, depth, X, Y, v3(tn.x, tn.y, tn.z));
                 const float r0 = rand_unit(rnd[3 * widx]), r1 = rand_unit(rnd[3 * widx + 1]),
                             r2 = rand_unit(rnd[3 * widx + 2]);
                 const vec3 rc = mode == 1 ? v3(r0, r1, r2) : v3(r0 - 0.2f, 1.0f, r2 - 0.2f);   // :652 / :660

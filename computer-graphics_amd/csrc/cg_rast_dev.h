@@ -37,6 +37,7 @@ struct RastArgs {
     float Rinv[16];         // glm::inverse(R), column-major
     RastTexMaps tx;
     int state16;            // colour mode 0: fill -> post state in 2 bytes per pixel (n < 32768)
+    const cg_rtri *tris;    // the clipped triangles (normals for the shading)
 };
 
 struct RastHdr {
@@ -45,18 +46,19 @@ struct RastHdr {
 };
 
 // Ordered per-row records (one wave per screen row): for every triangle in
-// order whose span on this row has a fragment on screen, a 64-byte record
-// with everything the fill needs -- one scalar load per record, no
-// dependent loads in the fill loop.
+// order whose span on this row has a fragment on screen, a 48-byte record
+// with everything the fill needs -- no dependent loads in the fill loop (the
+// shading reads the normal from the triangle, A.tris).
 struct alignas(16) RowRec {
     int lx, rx;
     float lz, sz, lX, sX, lY, sY;
-    int t, first_x;          // triangle index; x of the frame's first shaded fragment on this row, else -1
-    int shadow;              // colour.x < 0 (shadow-volume triangle)
-    float nx, ny, nz;
+    unsigned t_sh;           // triangle index | shadow-volume triangle (colour.x < 0) << 31
+    int first_x;             // x of the frame's first shaded fragment on this row, else -1
     int tex, index;          // the triangle's texture (0-3) and object index (findU/findV)
 };
-static_assert(sizeof(RowRec) == 64, "RowRec");
+static_assert(sizeof(RowRec) == 48, "RowRec");
+__device__ __forceinline__ int rec_t(const RowRec &r) { return (int)(r.t_sh & 0x7fffffffu); }
+__device__ __forceinline__ int rec_shadow(const RowRec &r) { return (int)(r.t_sh >> 31); }
 
 // calculateIllumination's direct term D (:674-683); the post-pass rebuilds
 // screen/low/high = colour * (D + indirect) from it with the same ops.

@@ -781,9 +781,11 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
 // point's lights in order and then its ambient term.  Every sum is the
 // reference's sum; each (point, light) pair is computed once instead of for
 // up to four pixels (1023 points for 240 pixels instead of 2160 sub-rays).
-// The tile's 15 pixel rows are swept in two halves (pixel rows 0-7 and
-// 8-14; lattice row 16 is computed by both) so the column buffers stay small
-// (2 x 17 rows x 3 x 64 floats).
+// The tile's 15 pixel rows are swept in thirds (pixel rows 0-4, 5-9, 10-14;
+// the lattice rows between two thirds are computed by both) so the column
+// buffers stay small (2 x 11 rows x 3 x 64 floats): 31.3 KB of LDS per
+// workgroup, 5 workgroups (waves per SIMD) per CU -- halves (17 rows, 40 KB)
+// allowed 4 and ran 4 % slower.
 // Whether triangle c stays a shadow candidate for hits in [lo, hi] of camera
 // rays (X, [y0, y1], focal) towards the frame's light set: cull_shadow, and
 // when every hit lies on c (own) the own-triangle certificate.
