@@ -57,6 +57,12 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
     return G;
 }
 
+// Tile row of a lattice workgroup: bottom rows first.  Workgroups are
+// dispatched x, then y, then frame; the floor and box tiles at the bottom of
+// the Cornell frame are the costliest, so starting them first leaves the
+// cheap ceiling tiles for the launch's tail.
+__device__ __forceinline__ int lat_tile_row() { return (int)(gridDim.y - 1 - blockIdx.y); }
+
 // Certificate units of a frame: tiles, or super-tiles of kSup x kSup tiles.
 __host__ __device__ __forceinline__ int rt_cert_units(const RtFrame &F, int sup)
 {
@@ -688,7 +694,8 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
     const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
+    const int by = lat_tile_row();
+    const LatTile G = lat_tile(F, blockIdx.x, by);
     const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
     // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
@@ -704,7 +711,7 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
     // sphere may be hit; bit 62: covered) and shadow mask for every hit the
     // tile can produce
-    const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const size_t tix = (size_t)by * gridDim.x + blockIdx.x;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
     const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
@@ -830,7 +837,8 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
     const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const LatTile G = lat_tile(F, blockIdx.x, blockIdx.y);
+    const int by = lat_tile_row();
+    const LatTile G = lat_tile(F, blockIdx.x, by);
     const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
     __shared__ float2 s_hit[kLatN];                                   // (t, hit index bits)
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
@@ -841,7 +849,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     const int npts = kLatW * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
     if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window
-    const size_t tix = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const size_t tix = (size_t)by * gridDim.x + blockIdx.x;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
     const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
