@@ -23,7 +23,7 @@ GeomParams geom_params(const cg_rast_params &p)
     return g;
 }
 
-// Device geometry in two launches, both spread over the chip.  Triangles
+// Device geometry in one launch spread over the chip.  Triangles
 // never interact while clipping, and the reference's plane-by-plane list (a
 // split inserting [modified, extra] in place, skeleton.cpp:720-1673) is, per
 // input triangle in order, that triangle's own plane-by-plane list -- the
@@ -33,24 +33,26 @@ GeomParams geom_params(const cg_rast_params &p)
 //                       triangle's list through planes 1..6 in LDS, children
 //                       placed by a ballot scan, the survivors staged at
 //                       stage[i * kGeomMaxLeaves ..] with their count;
-//  rast_compact_kernel  one wave per input triangle again: its offset is the
-//                       sum of the earlier counts, its survivors are copied
-//                       there, the total goes to out_n.
+//  (the span setup, cg_rast.hip, compacts them: clipped triangle t is the
+//  survivor t - pre[i] of the input triangle i whose prefix pre[i] of the
+//  counts holds it, so the list is in the reference's order.)
 // Every descendant carries its input triangle's normal, colour, texture and
 // index (a split's extra triangle copies them, :838-841), so lists hold only
 // vertices.  Planes 1-4 and 6 can split (plane 5 never does): at most 32
 // survivors per input triangle.
-constexpr int kGeomMaxLeaves = 32;
 
 __global__ __launch_bounds__(64) void rast_clip_kernel(GeomParams p, const cg_rtri *__restrict__ room, int n_room,
                                                        const cg_rtri *__restrict__ boxes, int n_boxes,
                                                        cg_rtri *__restrict__ stage, int *__restrict__ counts,
-                                                       cg_vec4 *__restrict__ out_light)
+                                                       cg_vec4 *__restrict__ out_light, int *__restrict__ first_tri)
 {
     __shared__ float4 s_v[2][kGeomMaxLeaves][3];
     const int i = blockIdx.x, lane = threadIdx.x;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    if (i == 0 && lane == 0) *out_light = C4(mat4_mul(p.R, geom_light_camera(p)));
+    if (i == 0 && lane == 0) {
+        *out_light = C4(mat4_mul(p.R, geom_light_camera(p)));
+        if (first_tri) *first_tri = 0x7f7f7f7f;   // the span setup's first-fragment minimum: none yet
+    }
     const cg_rtri root = geom_input(p, room, n_room, boxes, i);   // uniform over the wave
     int len = 1;
     for (int pl = 1; pl <= 6; ++pl) {
@@ -92,39 +94,17 @@ __global__ __launch_bounds__(64) void rast_clip_kernel(GeomParams p, const cg_rt
     if (lane == 0) counts[i] = len;
 }
 
-__global__ __launch_bounds__(64) void rast_compact_kernel(const cg_rtri *__restrict__ stage,
-                                                          const int *__restrict__ counts, int n_in,
-                                                          cg_rtri *__restrict__ out, int cap, int *__restrict__ out_n)
-{
-    const int i = blockIdx.x, lane = threadIdx.x;
-    int before = 0, total = 0;
-    for (int j = lane; j < n_in; j += 64) {
-        const int c = counts[j];
-        before += j < i ? c : 0;
-        total += c;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        before += __shfl_xor(before, o, 64);
-        total += __shfl_xor(total, o, 64);
-    }
-    const int n = counts[i];
-    if (lane < n && before + lane < cap) out[before + lane] = stage[(size_t)i * kGeomMaxLeaves + lane];
-    if (i == 0 && lane == 0) *out_n = min(total, cap);
-}
-
-hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
-                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_stage,
-                                int *d_counts, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st)
+// The clip alone: each input triangle's survivors staged at d_stage + 32 i,
+// their count at d_counts[i].  The span setup (cg_rast.hip) compacts them
+// into d_out in order (offset = sum of the earlier counts) as it reads them.
+hipError_t launch_rast_clip(const cg_rast_params &prm, const cg_rtri *d_room, int n_room, const cg_rtri *d_boxes,
+                            int n_boxes, cg_rtri *d_stage, int *d_counts, cg_vec4 *d_light, int *d_first,
+                            hipStream_t st)
 {
     const int n_in = n_room + 7 * n_boxes;
-    if (n_in <= 0) {   // empty scene: no triangles
-        hipLaunchKernelGGL(rast_compact_kernel, dim3(1), dim3(64), 0, st, d_stage, d_counts, 0, d_out, cap, d_n);
-        return hipGetLastError();
-    }
+    if (n_in <= 0) return hipSuccess;   // empty scene: the setup finds no triangle
     hipLaunchKernelGGL(rast_clip_kernel, dim3(n_in), dim3(64), 0, st, geom_params(prm), d_room, n_room, d_boxes,
-                       n_boxes, d_stage, d_counts, d_light);
-    hipLaunchKernelGGL(rast_compact_kernel, dim3(n_in), dim3(64), 0, st, d_stage, d_counts, n_in, d_out, cap, d_n);
+                       n_boxes, d_stage, d_counts, d_light, d_first);
     return hipGetLastError();
 }
 

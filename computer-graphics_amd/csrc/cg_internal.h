@@ -107,6 +107,7 @@ struct RtFrame {
 
 // ---- RAST --------------------------------------------------------------
 constexpr int kRastMaxH = 8192;
+constexpr int kGeomMaxLeaves = 32;   // clip survivors per input triangle (planes 1-4 and 6 split; 5 never)
 
 // Row span of one triangle (output of ComputePolygonRows, skeleton.cpp:433-498),
 // already reduced to what Interpolate (:524-551) needs for DrawPolygonRows:

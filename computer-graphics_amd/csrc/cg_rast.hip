@@ -128,31 +128,75 @@ __device__ __forceinline__ unsigned long long key_right(int x, unsigned seq)
     return ((unsigned long long)((unsigned)x ^ 0x80000000u) << 32) | (unsigned long long)seq;
 }
 
-__device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs &A, RastSpan *__restrict__ spans,
+__device__ void rast_setup_one(const cg_rtri &T, const RastArgs &A, RastSpan *__restrict__ spans,
                                RastHdr *__restrict__ hdr, int *__restrict__ first_tri, int t,
                                unsigned long long *lkey, unsigned long long *rkey, unsigned long long &fkey);
 
-// One workgroup per clipped triangle (grid-stride; the count may live on the
-// device when the geometry ran there).
+// One workgroup per clipped triangle (grid-stride).  With the device
+// geometry (stage != null) the clipped list is compacted here: the count
+// prefix of the n_in input triangles (LDS) locates clipped triangle t among
+// the staged survivors, the workgroup copies it to tris[t] for the later
+// kernels, and workgroup 0 stores the total at n_dev.
 __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
-    const cg_rtri *__restrict__ tris, RastArgs A, const int *__restrict__ n_dev, RastSpan *__restrict__ spans,
-    RastHdr *__restrict__ hdr, int *__restrict__ first_tri)
+    cg_rtri *__restrict__ tris, RastArgs A, int *__restrict__ n_dev, RastSpan *__restrict__ spans,
+    RastHdr *__restrict__ hdr, int *__restrict__ first_tri, const cg_rtri *__restrict__ stage,
+    const int *__restrict__ counts, int n_in)
 {
-    extern __shared__ unsigned long long s_keys[];          // [2 * H]: left | right keys per row
+    extern __shared__ unsigned long long s_keys[];          // [2 * H]: left | right keys per row; then [n_in + 1] ints
     __shared__ unsigned long long fkey;
+    __shared__ int s_carry;
     unsigned long long *lkey = s_keys, *rkey = s_keys + A.H;
-    const int n = n_dev ? min(*n_dev, A.n) : A.n;
+    int *s_pre = (int *)(s_keys + 2 * A.H);
+    int n = A.n;
+    if (stage) {
+        if (threadIdx.x < 64) {                            // wave 0: exclusive prefix of the counts
+            const int lane = threadIdx.x;
+            int carry = 0;
+            for (int i0 = 0; i0 < n_in; i0 += 64) {
+                const int c = i0 + lane < n_in ? counts[i0 + lane] : 0;
+                int x = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(x, o);
+                    if (lane >= o) x += y;
+                }
+                if (i0 + lane < n_in) s_pre[i0 + lane] = carry + x - c;
+                carry += __shfl(x, 63);
+            }
+            if (lane == 0) {
+                s_pre[n_in] = carry;
+                s_carry = carry;
+            }
+        }
+        __syncthreads();
+        n = min(s_carry, A.n);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *n_dev = n;
+    } else if (n_dev) {
+        n = min(*n_dev, A.n);
+    }
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
-        rast_setup_one(tris, A, spans, hdr, first_tri, t, lkey, rkey, fkey);
+        cg_rtri T;
+        if (stage) {
+            int lo = 0, hi = n_in - 1;                     // the input triangle whose survivors hold t
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_pre[mid] <= t) lo = mid;
+                else hi = mid - 1;
+            }
+            T = stage[(size_t)lo * kGeomMaxLeaves + (t - s_pre[lo])];
+            if (threadIdx.x == 0) tris[t] = T;
+        } else {
+            T = tris[t];
+        }
+        rast_setup_one(T, A, spans, hdr, first_tri, t, lkey, rkey, fkey);
         __syncthreads();
     }
 }
 
-__device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs &A, RastSpan *__restrict__ spans,
+__device__ void rast_setup_one(const cg_rtri &T, const RastArgs &A, RastSpan *__restrict__ spans,
                                RastHdr *__restrict__ hdr, int *__restrict__ first_tri, int t,
                                unsigned long long *lkey, unsigned long long *rkey, unsigned long long &fkey)
 {
-    const cg_rtri T = tris[t];
     Pix vp[3] = {vertex_shader(A, T.v0), vertex_shader(A, T.v1), vertex_shader(A, T.v2)};
     int mx = -INT_MAX, mn = INT_MAX;                        // :434-447
     for (int i = 0; i < 3; ++i) {
@@ -167,6 +211,10 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
     h.yhi = yhi;
     h.fy = INT_MAX;
     h.fx = INT_MAX;
+    h.t_sh = (unsigned)t | (T.color.x >= 0 ? 0u : 0x80000000u);
+    h.tex = T.texture;
+    h.index = T.index;
+    h.pad = 0;
     if (rows <= 0 || ylo > yhi) {
         if (threadIdx.x == 0) {
             h.ylo = 1;
@@ -280,6 +328,12 @@ __device__ void rast_setup_one(const cg_rtri *__restrict__ tris, const RastArgs 
 }
 
 
+// A wave per row: the records of the row's covering triangles in triangle
+// order.  The headers of a group of 64 * kRowBatches triangles are loaded in
+// one round trip (beside the triangle count), then the spans of those that
+// cover the row, then the ballot compaction -- two dependent round trips per
+// group instead of three per 64 triangles.
+constexpr int kRowBatches = 8;
 __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
                                                        const int *__restrict__ n_dev,
                                                        const RastSpan *__restrict__ spans,
@@ -296,32 +350,38 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
     const int ft = A.want_first ? *first_tri : INT_MAX;
     const int n = n_dev ? min(*n_dev, A.n) : A.n;
     int c = 0;
-    for (int base = 0; base < n; base += 64) {
-        const int t = base + lane;
-        bool keep = false;
-        RastSpan sp;
-        RastHdr h;
-        if (t < n) {
-            h = hdr[t];
-            if (h.ylo <= y && y <= h.yhi) {
-                sp = spans[(size_t)y * A.n + t];
-                // fragments x in [lx, rx - 1] (:504) intersecting [0, W)
-                keep = sp.rx > sp.lx && sp.rx - 1 >= 0 && sp.lx <= A.W - 1;
+    for (int g0 = 0; g0 == 0 || g0 < n; g0 += 64 * kRowBatches) {
+        RastHdr h[kRowBatches];
+#pragma unroll
+        for (int j = 0; j < kRowBatches; ++j) {   // in flight together (t < A.n: a valid header slot)
+            const int t = g0 + 64 * j + lane;
+            if (t < A.n) h[j] = hdr[t];
+        }
+        RastSpan sp[kRowBatches];
+        bool keep[kRowBatches];
+#pragma unroll
+        for (int j = 0; j < kRowBatches; ++j) {
+            const int t = g0 + 64 * j + lane;
+            keep[j] = t < n && h[j].ylo <= y && y <= h[j].yhi;
+            if (keep[j]) sp[j] = spans[(size_t)y * A.n + t];
+        }
+#pragma unroll
+        for (int j = 0; j < kRowBatches; ++j) {
+            const int t = g0 + 64 * j + lane;
+            // fragments x in [lx, rx - 1] (:504) intersecting [0, W)
+            const bool k = keep[j] && sp[j].rx > sp[j].lx && sp[j].rx - 1 >= 0 && sp[j].lx <= A.W - 1;
+            const unsigned long long mk = __ballot(k);
+            if (k) {
+                RowRec r;
+                r.lx = sp[j].lx; r.rx = sp[j].rx;
+                r.lz = sp[j].lz; r.sz = sp[j].sz; r.lX = sp[j].lX; r.sX = sp[j].sX; r.lY = sp[j].lY; r.sY = sp[j].sY;
+                r.t_sh = h[j].t_sh;
+                r.first_x = (t == ft && h[j].fy == y) ? h[j].fx : -1;
+                r.tex = h[j].tex; r.index = h[j].index;
+                recs[(size_t)y * A.n + c + __popcll(mk & ((1ull << lane) - 1ull))] = r;
             }
+            c += __popcll(mk);
         }
-        unsigned long long m = __ballot(keep);
-        unsigned long long below = lane ? (m & ((1ull << lane) - 1)) : 0ull;
-        if (keep) {
-            const cg_rtri T = tris[t];
-            RowRec r;
-            r.lx = sp.lx; r.rx = sp.rx;
-            r.lz = sp.lz; r.sz = sp.sz; r.lX = sp.lX; r.sX = sp.sX; r.lY = sp.lY; r.sY = sp.sY;
-            r.t_sh = (unsigned)t | (T.color.x >= 0 ? 0u : 0x80000000u);
-            r.first_x = (t == ft && h.fy == y) ? h.fx : -1;
-            r.tex = T.texture; r.index = T.index;
-            recs[(size_t)y * A.n + c + __popcll(below)] = r;
-        }
-        c += __popcll(m);
     }
     if (lane == 0) count[y] = c;
 }
@@ -635,16 +695,23 @@ int rast_colour_fill(cg_ctx *c, const RastArgs &A, const cg_rast_params *p, cons
                      const RastHdr *hdr, const int *n_dev, int max_recs, float4 *state, float *d_depth,
                      int32_t *shadow, hipStream_t st, long long *n_shaded);
 
-hipError_t launch_rast_geometry(const cg_rast_params &prm, const cg_rtri *d_room, int n_room,
-                                const cg_rtri *d_boxes, int n_boxes, cg_rtri *d_out, cg_rtri *d_stage,
-                                int *d_counts, int cap, int *d_n, cg_vec4 *d_light, hipStream_t st);
+hipError_t launch_rast_clip(const cg_rast_params &prm, const cg_rtri *d_room, int n_room, const cg_rtri *d_boxes,
+                            int n_boxes, cg_rtri *d_stage, int *d_counts, cg_vec4 *d_light, int *d_first,
+                            hipStream_t st);
 
 // The fill + post pipeline.  Either the triangle count is known on the host
 // (n_dev == nullptr, n = count) or it lives on the device (n_dev, n = capacity,
 // light read from d_light).
-static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_dev, const cg_rast_params *p,
+// Staged survivors of the device clip (rast_draw_device): the setup compacts them.
+struct RastStage {
+    const cg_rtri *stage;   // null: d_tris is already the list
+    const int *counts;
+    int n_in;
+};
+static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg_rast_params *p,
                          cg_vec4 light, const cg_vec4 *d_light, uint32_t *d_argb, float *d_depth,
-                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open, int tex_mask);
+                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open, int tex_mask,
+                         RastStage sg);
 int rast_tex_maps(cg_ctx *c, RastTexMaps *m);
 
 // glm::inverse for mat4 (glm/detail/type_mat4x4.inl:37-90), column-major
@@ -687,8 +754,8 @@ int rast_render_device(cg_ctx *c, const cg_rtri *d_tris, int n, const cg_rast_pa
                        uint32_t *d_argb, float *d_depth, int32_t *d_shadow, hipStream_t st,
                        cg_stats *stats, int tex_mask)
 {
-    return rast_pipeline(c, d_tris, n, nullptr, p, light, nullptr, d_argb, d_depth, d_shadow, st, stats, false,
-                         tex_mask);
+    return rast_pipeline(c, const_cast<cg_rtri *>(d_tris), n, nullptr, p, light, nullptr, d_argb, d_depth, d_shadow,
+                         st, stats, false, tex_mask, RastStage{nullptr, nullptr, 0});
 }
 
 // Whole rasteriser Draw on the device: geometry (shadow volumes + clip) then
@@ -707,20 +774,23 @@ int rast_draw_device(cg_ctx *c, const cg_rtri *d_room, int n_room, const cg_rtri
     if (!tris) return ctx_fail(c, e, "alloc clipped triangles");
     int *geo = (int *)ctx_buf(c, 9, 64 + 4 * (size_t)n_in, &e);   // [0] count, [4..7] light, [16..] counts
     if (!geo) return ctx_fail(c, e, "alloc geometry header");
+    int *misc = (int *)ctx_buf(c, 7, ((size_t)p->height + 16) * sizeof(int), &e);   // count[H] | first_tri
+    if (!misc) return ctx_fail(c, e, "alloc counts");
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
     if (stats && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
-    if ((e = launch_rast_geometry(*p, d_room, n_room, d_boxes, n_boxes, tris, tris + cap, geo + 16, cap, geo,
-                                  (cg_vec4 *)(geo + 4), st)) != hipSuccess)
-        return ctx_fail(c, e, "rast_geometry launch");
+    if ((e = launch_rast_clip(*p, d_room, n_room, d_boxes, n_boxes, tris + cap, geo + 16, (cg_vec4 *)(geo + 4),
+                              misc + p->height, st)) != hipSuccess)
+        return ctx_fail(c, e, "rast_clip launch");
     if (n_out) *n_out = geo;
     return rast_pipeline(c, tris, cap, geo, p, cg_vec4{0, 0, 0, 1}, (const cg_vec4 *)(geo + 4), d_argb, d_depth,
-                         d_shadow, st, stats, true, tex_mask);
+                         d_shadow, st, stats, true, tex_mask, RastStage{tris + cap, geo + 16, n_in});
 }
 
-static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_dev, const cg_rast_params *p,
+static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg_rast_params *p,
                          cg_vec4 light, const cg_vec4 *d_light, uint32_t *d_argb, float *d_depth,
-                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open, int tex_mask)
+                         int32_t *d_shadow, hipStream_t st, cg_stats *stats, bool events_open, int tex_mask,
+                         RastStage sg)
 {
     if (p->width <= 2 || p->height <= 2 || p->height > kRastMaxRows) return CG_E_INVALID;
     const int W = p->width, H = p->height;
@@ -770,12 +840,14 @@ static int rast_pipeline(cg_ctx *c, const cg_rtri *d_tris, int n, const int *n_d
     hipEvent_t e0, e1;
     ctx_events(c, &e0, &e1);
     if (stats && !events_open && (e = hipEventRecord(e0, st)) != hipSuccess) return ctx_fail(c, e, "event");
-    if (A.want_first && (e = hipMemsetAsync(first_tri, 0x7f, sizeof(int), st)) != hipSuccess)
+    // the device clip initialises the first-fragment minimum (rast_clip_kernel)
+    if (A.want_first && !(sg.stage && sg.n_in > 0) && (e = hipMemsetAsync(first_tri, 0x7f, sizeof(int), st)) != hipSuccess)
         return ctx_fail(c, e, "memset");
     if (n > 0) {
         const int grid = n < 1024 ? n : 1024;                // LDS 16 B per row: several workgroups per CU
-        hipLaunchKernelGGL(rast_setup_kernel, dim3(grid), dim3(kSetupThreads), 2 * (size_t)H * 8, st, d_tris, A, n_dev,
-                           spans, hdr, first_tri);
+        hipLaunchKernelGGL(rast_setup_kernel, dim3(grid), dim3(kSetupThreads),
+                           2 * (size_t)H * 8 + ((size_t)sg.n_in + 1) * 4, st, d_tris, A, n_dev, spans, hdr, first_tri,
+                           sg.stage, sg.counts, sg.n_in);
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
     }
     hipLaunchKernelGGL(rast_rows_kernel, dim3(xcd_grid(H, kXcdRows / 4)), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,

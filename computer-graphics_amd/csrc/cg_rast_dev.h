@@ -43,6 +43,8 @@ struct RastArgs {
 struct RastHdr {
     int ylo, yhi;           // visible rows [ylo, yhi] (ylo > yhi: none)
     int fy, fx;             // first shadeable fragment (if want_first), fy = INT_MAX none
+    unsigned t_sh;          // what the row records carry of the triangle: index | shadow volume << 31,
+    int tex, index, pad;    // texture, object index
 };
 
 // Ordered per-row records (one wave per screen row): for every triangle in
