@@ -5,9 +5,11 @@ For the C2 frame it measures, in steady state (calls of K frames back to
 back, so each call's certificate kernels overlap the previous lattice launch):
   * the whole frame's time per frame;
   * every 15-row band's time per frame (the row-cost profile);
-  * for N = 2, 4, 8: bands partitioned on that profile (cgdist.band_partition,
-    the rule cg_dist_rebalance applies), each rank's band timed on its own ->
-    max over ranks, and the render-only scaling bound whole / max.
+  * for N = 2, 4, 8: bands partitioned on that profile (cgdist.band_partition),
+    then re-partitioned from the measured per-rank times (cgdist.rebalance,
+    the rule cg_dist_rebalance applies during bench.py's warm-up) for
+    CG_BALANCE_ROUNDS rounds; each rank's band timed on its own -> max over
+    ranks, and the render-only scaling bound whole / max.
 The gap between the sum of the 15-row bands and the whole frame is the fixed
 per-band cost (launch tails, certificates) a small shard pays.
 usage: python scripts/shard_balance.py [rt|c4] [calls]
@@ -63,11 +65,22 @@ def main():
     res = {"workload": wl_name, "frames_per_call": K, "calls": calls, "whole_us_per_frame": whole,
            "sum_of_15row_bands_us": float(sum(band_us)),
            "band15_us": [round(u, 2) for u in band_us]}
+    rounds = int(os.environ.get("CG_BALANCE_ROUNDS", "3"))
     for N in (2, 4, 8):
+        # the 15-row profile's partition, then the library's own rebalance rule
+        # (cg_dist_rebalance / cgdist.rebalance: cost density uniform within each
+        # measured band) for `rounds` rounds, as bench.py's warm-up does
         part = cgdist.band_partition(cost, N)
-        us = [per_frame_us(cgamd.RtShard(row0=r0, rows=nr)) if nr else 0.0 for r0, nr in part]
-        res[f"N{N}"] = {"bands": part, "per_rank_us": [round(x, 2) for x in us], "max_us": max(us),
-                        "render_scaling_bound": whole / max(us)}
+        hist = []
+        for r in range(rounds + 1):
+            us = [per_frame_us(cgamd.RtShard(row0=r0, rows=nr)) if nr else 0.0 for r0, nr in part]
+            hist.append({"bands": part, "per_rank_us": [round(x, 2) for x in us], "max_us": max(us)})
+            if r < rounds:
+                part = cgdist.rebalance(part, us, np.zeros(N), H)
+        best = min(hist, key=lambda h: h["max_us"])
+        res[f"N{N}"] = dict(best, render_scaling_bound=whole / best["max_us"],
+                            profile_partition_max_us=hist[0]["max_us"],
+                            rounds=[h["max_us"] for h in hist])
     print(json.dumps(res), flush=True)
     ctx.close()
 
