@@ -1705,7 +1705,7 @@ static void lit_bounds(BigBufs &B, const RtFrame &F, const RtGrid &G)
 
 hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
                          const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const cg_tri *d_tris,
-                         int pend_cap, const BigCaps &caps, unsigned long long *h_demand, bool dry)
+                         int pend_cap, const BigCaps &caps, unsigned long long *h_demand, int dry)
 {
     BigBufs B = big_layout(F, caps);
     if (2 * B.bins_x * B.bins_y > kMaxSubs) return hipErrorInvalidValue;   // rt_bin_scan_kernel's LDS table
@@ -1734,17 +1734,22 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     hipLaunchKernelGGL(rt_bin_scan_kernel, dim3(1), dim3(1024), 0, st, B, 2 * bins);
-    if (dry) {   // sizing pass (cg_shim.hip): only the lists, for their demand
-        if (h_demand)
-            e = hipMemcpyAsync(h_demand, B.pool_n, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
-        return e != hipSuccess ? e : hipGetLastError();
-    }
+    // sizing passes (cg_shim.hip) stop early and report the demand: dry 1
+    // after the camera-ray lists, dry 2 after the many-light shadow lists
+    auto demand = [&]() {
+        const hipError_t c = h_demand ? hipMemcpyAsync(h_demand, B.pool_n, 4 * sizeof(unsigned long long),
+                                                       hipMemcpyDeviceToHost, st)
+                                      : hipSuccess;
+        return c != hipSuccess ? c : hipGetLastError();
+    };
+    if (dry == 1) return demand();
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
     if (lat) hipLaunchKernelGGL(rt_big_primary_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     else hipLaunchKernelGGL(rt_big_primary_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     if (!flags_fit) {
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
+        if (dry == 2) return demand();
     } else if (F.n_lights > 0) {
         hipLaunchKernelGGL(rt_lit_class_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
         if (lat) hipLaunchKernelGGL(rt_shadow_hints_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
@@ -1753,11 +1758,14 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     }
     if (lat) hipLaunchKernelGGL(rt_big_shade_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     else hipLaunchKernelGGL(rt_big_shade_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
-    if (h_demand) {   // the pools' demand, for the host's sizing (cg_shim.hip)
-        e = hipMemcpyAsync(h_demand, B.pool_n, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
-        if (e != hipSuccess) return e;
-    }
-    return hipGetLastError();
+    return demand();   // the pools' demand, for the host's sizing of the next frames
+}
+
+// Whether a frame's shading uses the per-bin shadow lists (per-pixel mode
+// with more than 7 lights): its sizing then needs a second dry stage.
+bool rt_big_shadow_lists(const RtFrame &F)
+{
+    return !rt_big_lattice(F) && 9 * F.n_lights > 64;
 }
 
 // Host build of the scene grid: cubic cells sized for ~2 triangle centroids

@@ -26,7 +26,8 @@ hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, con
 bool rt_use_lattice(const RtFrame &);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
-                         uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, bool);
+                         uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, int);
+bool rt_big_shadow_lists(const RtFrame &);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &, const BigCaps &);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
@@ -550,9 +551,10 @@ static bool big_observe(cg_ctx *c, bool sizing = false)
 // Large scene: binned certificates (cg_rt_big.hip).  The first frame of a
 // scene (or of a new frame shape / path) is sized first: dry passes of the
 // list kernels alone report the pools' demand until it fits (a pass in which
-// a list overflowed under-counts what depends on it).  Later frames stay
-// asynchronous and grow the pools for the next ones from their reported
-// demand; a frame that still overflows renders through the fallback.
+// a list overflowed under-counts what depends on it), then -- when the frame
+// shades through per-bin shadow lists -- dry passes up to those lists.  Later
+// frames stay asynchronous and grow the pools for the next ones from their
+// reported demand; a frame that still overflows renders through the fallback.
 static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
 {
     if (!c->big_demand) {
@@ -576,8 +578,9 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
     }
     if (c->big_fixed) c->big_sized = true;
     if (c->big_ev_live && hipEventQuery(c->big_ev) == hipSuccess) big_observe(c);
-    for (int pass = 0; pass < 6; ++pass) {
-        const bool dry = !c->big_sized && pass < 5;
+    int stage = c->big_sized ? 0 : 1;   // dry stage of the next pass (0: render)
+    for (int pass = 0; pass < 8; ++pass) {
+        const int dry = pass == 7 ? 0 : stage;
         const size_t need = rt_big_scratch_bytes(F, c->big_caps);
         if ((need > c->big.bytes || need < c->big.bytes / 2) && c->big.p) {   // grow, or give back a sized-down half
             CG_TRY(c, hipDeviceSynchronize(), "drain before resizing scratch");
@@ -592,7 +595,13 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
         c->big_ev_live = true;
         if (!dry) break;
         CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
-        if (!big_observe(c, true)) c->big_sized = true;   // fits: the next pass renders
+        if (big_observe(c, true)) continue;          // grown: the same stage again
+        if (stage == 1 && rt_big_shadow_lists(F)) {
+            stage = 2;
+        } else {
+            c->big_sized = true;                     // fits: the next pass renders
+            stage = 0;
+        }
     }
     return CG_OK;
 }
