@@ -36,11 +36,34 @@ __device__ __forceinline__ RtTri rt_tri_const(const cg_tri &T, float cx, float c
     return r;
 }
 
+// Lattice geometry (rt_lattice_ok).  R leaves y alone (dir.y = v - H/2 bit
+// for bit: mat4_mul adds only +-0 terms) and turns x into a function of x
+// alone, so sub-ray (i, j) of pixel (u, v) is (fl(dir.x(u) + 0.5 i), y + 0.5 j,
+// focal) (skeleton.cpp:126-137) and the rays of a column of pixels share rows.
+//  shared columns (dir.x = x exactly, R the identity): the x values are the
+//    half-pixel lattice too, pixel tx's sub-ray i is column 2 tx + 1 + i of
+//    2 nu + 1, shared with the neighbours;
+//  per-pixel columns (a yaw, :236-238): pixel tx keeps its three columns
+//    3 tx + 1 + i of 3 nu, x = fl(dir.x(u) + 0.5 i) formed as the reference
+//    forms it -- only the rows are shared (1488 rays for 240 pixels, not 2160).
+// dir.x is computed with y = 0: R's y weight is +-0, so y only adds a +-0 term,
+// which can change at most the sign of a zero dir.x, and fl(+-0 + 0.5 i) is the
+// same for both signs (for i = 0, -0 + +0 = +0).
+__host__ __device__ __forceinline__ bool lat_yaw(const RtFrame &F)
+{
+    return !(F.R[0] == 1.0f && F.R[8] == 0.0f && F.R[12] == 0.0f);
+}
+__host__ __device__ __forceinline__ float lat_dir_x(const RtFrame &F, int u)
+{
+    return mat4_mul(F.R, v4((float)(u - F.W / 2), 0.0f, F.focal, 1.0f)).x;   // :126-128
+}
+
 // A lattice tile (see rt_lattice_kernel): pixels u0 .. u0 + nu - 1 of rows
 // v0 .. v0 + nv - 1 (local rows L0 ..), lattice point (cx, cy) <-> ray
-// (0.5 (ax0 + cx), 0.5 (ay0 + cy), focal), needed points cols x rows.
+// (lat_x(cx), 0.5 (ay0 + cy), focal), needed points cols x rows.
 struct LatTile {
     int u0, L0, v0, nu, nv, ax0, ay0, cols, rows;
+    bool yaw;   // per-pixel columns
 };
 __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
 {
@@ -50,11 +73,34 @@ __device__ __forceinline__ LatTile lat_tile(const RtFrame &F, int bx, int by)
     G.v0 = shard_row(F, G.L0);   // the tile's rows v0 .. v0 + 14 lie in one stripe
     G.nu = min(kLatTileW, F.W - G.u0);
     G.nv = max(0, min(min(kLatTileH, F.rows_out - G.L0), F.H - G.v0));
+    G.yaw = lat_yaw(F);
     G.ax0 = 2 * (G.u0 - F.W / 2) - 1;
     G.ay0 = 2 * (G.v0 - F.H / 2) - 1;
-    G.cols = 2 * G.nu + 1;
+    G.cols = G.yaw ? 3 * G.nu : 2 * G.nu + 1;
     G.rows = G.nv > 0 ? 2 * G.nv + 1 : 0;
     return G;
+}
+// x of lattice column cx (the sub-ray's newDir.x, :137)
+__device__ __forceinline__ float lat_x(const RtFrame &F, const LatTile &G, int cx)
+{
+    if (!G.yaw) return 0.5f * (float)(G.ax0 + cx);
+    const int p = cx / 3, i = cx - 3 * p - 1;
+    return lat_dir_x(F, G.u0 + p) + (0.5f * (float)i);
+}
+// The x extent [x0, x1] of the sub-rays of tiles A .. B of one tile row.  Per-
+// pixel columns: every float op of dir.x(u) is monotone in u, and so is
+// fl(d + 0.5 i) in d, so the end pixels' outer sub-rays bound it exactly.
+__device__ __forceinline__ void lat_xrange(const RtFrame &F, const LatTile &A, const LatTile &B, float &x0,
+                                           float &x1)
+{
+    if (!A.yaw) {
+        x0 = 0.5f * (float)A.ax0;
+        x1 = 0.5f * (float)(B.ax0 + B.cols - 1);
+        return;
+    }
+    const float a = lat_dir_x(F, A.u0), b = lat_dir_x(F, B.u0 + B.nu - 1);
+    x0 = fminf(a, b) + (0.5f * -1.0f);
+    x1 = fmaxf(a, b) + (0.5f * 1.0f);
 }
 
 // Tile row of a lattice workgroup: bottom rows first.  Workgroups are
@@ -99,8 +145,7 @@ __device__ __forceinline__ bool unit_bundle(const RtFrame &F, int unit, int sup,
         by0 = by1 = unit / tiles_x;
     }
     const LatTile A = lat_tile(F, bx0, by0), B = lat_tile(F, bx1, by0);
-    x0 = 0.5f * (float)A.ax0;
-    x1 = 0.5f * (float)(B.ax0 + B.cols - 1);
+    lat_xrange(F, A, B, x0, x1);
     bool any = false;
     y0 = FLT_MAX;
     y1 = -FLT_MAX;
@@ -292,7 +337,8 @@ __global__ __launch_bounds__(64) void rt_tile_cert_kernel(const cg_tri *__restri
         int t;
         LatTile G;
         const bool act = tile_of(tl, t, G) && ci < cand;
-        const float x0 = 0.5f * (float)G.ax0, x1 = 0.5f * (float)(G.ax0 + G.cols - 1);
+        float x0, x1;
+        lat_xrange(F, G, G, x0, x1);
         const float y0 = 0.5f * (float)G.ay0, y1 = 0.5f * (float)(G.ay0 + G.rows - 1);
         const bool is_tri = act && ci < ntp;
         const int k = is_tri ? nth_bit(SPt, ci) : 0;
@@ -506,6 +552,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_pixel_kernel(RtFra
 // are formed exactly as the reference forms them.
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
+constexpr int kLatWY = 3 * kLatTileW;   // per-pixel columns (a yawed camera): 48 x 31 = 1488 rays
 
 // Shared pieces of the two lattice kernels.
 //
@@ -618,7 +665,7 @@ __device__ __forceinline__ void lat_store(const RtFrame &F, const LatTile &G, co
 // ray (rt_tile_cert_kernel: t > 0, u, v inside, nothing else can be hit), so
 // the reference's closest hit is k with t = detT / det (:306), formed with
 // closest_primary_n's float ops; the u, v tests and the distance are not needed.
-template <class Store>
+template <int PITCH, class Store>
 __device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__restrict__ tc,
                                             const RtSphere *__restrict__ sph, unsigned long long mask, bool covered,
                                             const LatTile &G, int p_lo, int p_hi, int lane, Store store)
@@ -631,10 +678,10 @@ __device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__re
 #pragma unroll
         for (int n = 0; n < NP; ++n) {
             const int p = p0 + 64 * n + lane;
-            const int cy = p / kLatW, cx = p - cy * kLatW;
+            const int cy = p / PITCH, cx = p - cy * PITCH;
             pp[n] = p;
             live[n] = p < p_hi && cx < G.cols;
-            X[n] = 0.5f * (float)(G.ax0 + cx);
+            X[n] = lat_x(Fp, G, cx);
             Y[n] = 0.5f * (float)(G.ay0 + cy);
         }
         int bi[NP];
@@ -681,6 +728,9 @@ __device__ __forceinline__ void lat_store_black(const RtFrame &F, const LatTile 
 // blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
 // tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
 // out + frame * out_stride.
+// PITCH: the LDS row pitch of the lattice, kLatW (shared columns) or kLatWY
+// (per-pixel columns; rt_lattice_ok).
+template <int PITCH>
 __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__restrict__ tc,
                                              const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
                                              const unsigned long long *__restrict__ lat_masks, const RtFrameCams &cams,
@@ -695,17 +745,18 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int by = lat_tile_row();
-    const LatTile G = lat_tile(F, blockIdx.x, by);
-    const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
+    LatTile G = lat_tile(F, blockIdx.x, by);
+    G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
+    const int ay0 = G.ay0, cols = G.cols, rows = G.rows;
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
     // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
-    __shared__ float4 s_pt[kLatN];
+    __shared__ float4 s_pt[PITCH * kLatH];
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ uint32_t s_px[kLatTileH * kLatTileW];
     lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
-    // the needed points, walked row-major at the full pitch kLatW; wave w takes
-    // the w-th quarter
-    const int npts = kLatW * rows;
+    // the needed points, walked row-major at the full pitch; wave w takes the
+    // w-th quarter
+    const int npts = PITCH * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
     if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window: whole workgroup
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
@@ -725,19 +776,19 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
         return;                            // the whole workgroup (m0 is uniform)
     }
     __syncthreads();                       // s_obj
-    lat_closest(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
+    lat_closest<PITCH>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_pt[p] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
     });
     // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
     // attributes from the LDS table
     for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
         const int p = p0 + lane;
-        const int cy = p / kLatW, cx = p - cy * kLatW, idx = p;
+        const int cy = p / PITCH, cx = p - cy * PITCH, idx = p;
         if (p < p_hi && cx < cols) {
             const float4 q = s_pt[idx];
             const int bi = __float_as_int(q.w);
             if (bi != INT_MIN) {
-                const float X = 0.5f * (float)(ax0 + cx), Y = 0.5f * (float)(ay0 + cy);
+                const float X = lat_x(F, G, cx), Y = 0.5f * (float)(ay0 + cy);
                 const float t = q.x;
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
                 const vec3 dl = lat_direct_light(Fs, tc, sph, s_obj, F.lights[0], bi, pos, smask);
@@ -756,7 +807,7 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
             const int i = k / 3 - 1, j = k % 3 - 1;
-            const int idx = (2 * ty + 1 + j) * kLatW + (2 * tx + 1 + i);
+            const int idx = (2 * ty + 1 + j) * PITCH + ((G.yaw ? 3 : 2) * tx + 1 + i);
             const float4 q = s_pt[idx];
             const int bi = __float_as_int(q.w);
             if (bi == INT_MIN) continue;
@@ -838,7 +889,8 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int by = lat_tile_row();
-    const LatTile G = lat_tile(F, blockIdx.x, by);
+    LatTile G = lat_tile(F, blockIdx.x, by);
+    G.yaw = false;   // shared columns only (rt_lattice_ok)
     const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
     __shared__ float2 s_hit[kLatN];                                   // (t, hit index bits)
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
@@ -870,7 +922,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
         }
     }
     __syncthreads();                       // s_obj
-    lat_closest(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
+    lat_closest<kLatW>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_hit[p] = make_float2(t, __int_as_float(bi));
     });
     __syncthreads();
@@ -1051,6 +1103,7 @@ __device__ __forceinline__ void lat_signal(uint32_t *frame_done, int frame)
     if (threadIdx.x == 0) atomicAdd(&frame_done[frame], 1u);
 }
 
+template <int PITCH>
 __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph,
@@ -1058,7 +1111,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
                                                                   RtFrameCams cams, size_t out_stride,
                                                                   uint32_t *__restrict__ out, uint32_t *frame_done)
 {
-    lattice_body(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
+    lattice_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
     lat_signal(frame_done, blockIdx.z);
 }
 
@@ -1268,16 +1321,22 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
 
 size_t rt_sup_units(const RtFrame &F) { return (size_t)rt_cert_units(F, 1); }
 
-// The lattice kernel's precondition: R is the identity up to the sign of its
-// zeros (then mat4_mul returns (x, y) bit for bit), pixel offsets stay far
-// inside float's exact integer range, and tiles do not straddle stripes.
+// The lattice kernels' precondition (lat_yaw): dir.y = y (R's y row (0, 1, 0,
+// 0) up to the sign of its zeros) and dir.x a function of x alone (R's y
+// weight +-0) -- shared columns when dir.x = x exactly (x row (1, 0, 0, 0)),
+// else per-pixel columns, which the one-light kernel handles (entries bounded,
+// so dir.x stays finite and monotone); pixel offsets stay far inside float's
+// exact integer range, and tiles do not straddle stripes.
 static bool rt_lattice_ok(const RtFrame &F)
 {
-    for (int r = 0; r < 4; ++r)
-        for (int c = 0; c < 4; ++c) {
-            const float e = F.R[4 * c + r];
-            if (r == c ? e != 1.0f : e != 0.0f) return false;
-        }
+    const float *R = F.R;
+    if (!(R[1] == 0.0f && R[5] == 1.0f && R[9] == 0.0f && R[13] == 0.0f && R[4] == 0.0f)) return false;
+    if (lat_yaw(F)) {
+        if (F.n_lights != 1) return false;
+        for (int k : {0, 8, 12})
+            if (!(fabsf(R[k]) <= 1e6f)) return false;
+        if (!(fabsf(F.focal) <= 1e6f)) return false;
+    }
     return F.W < (1 << 20) && F.H < (1 << 20) && (F.nranks == 1 || F.stripe_h % kLatTileH == 0);
 }
 
@@ -1302,8 +1361,11 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
                                     hipStream_t st, uint32_t *d_done)
 {
     const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
-    if (F.n_lights == 1)
-        hipLaunchKernelGGL(rt_lattice_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
+    if (F.n_lights == 1 && lat_yaw(F))
+        hipLaunchKernelGGL(rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+                           d_lat_masks, cams, out_stride, d_out, d_done);
+    else if (F.n_lights == 1)
+        hipLaunchKernelGGL(rt_lattice_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
                            cams, out_stride, d_out, d_done);
     else
         hipLaunchKernelGGL(rt_lattice_lights_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,

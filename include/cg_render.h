@@ -61,8 +61,9 @@ typedef struct {
 /* Row sharding for the multi-GPU path.  Stripes (rows == 0): stripes of
  * `stripe_h` rows are dealt round-robin over `nranks`; this rank renders
  * stripes k with k % nranks == rank, packed in order into its output.  Any
- * stripe_h >= 1 is exact; for speed use a multiple of 15 for the unrotated
- * one-light camera (the lattice kernel's tile height) and of 8 otherwise.
+ * stripe_h >= 1 is exact; for speed use a multiple of 15 for a one-light
+ * camera that is unrotated or only yawed, or an unrotated light set (the
+ * lattice kernels' tile height), and of 8 otherwise.
  * Band (rows > 0): this shard renders frame rows row0 .. row0 + rows - 1
  * (rows past the frame are padding); rank / nranks / stripe_h are ignored.
  * Window (cols > 0, CG_PIX_RGB24 output only): only columns col0 .. col0 +

@@ -7,7 +7,7 @@ figure doubles it (an upper bound for narrower accesses); WRITE_SIZE is exact fo
 import collections, csv, json, os, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"rt": ["rt_lattice_kernel"], "rast": ["rast_clip_kernel", "rast_compact_kernel", "rast_setup_kernel", "rast_rows_kernel", "rast_fill_kernel",
+DOMINANT = {"rt": ["rt_lattice_kernel"], "rast": ["rast_clip_kernel", "rast_setup_kernel", "rast_rows_kernel", "rast_fill_kernel",
                                                  "rast_post_kernel"]}
 
 

@@ -108,6 +108,46 @@ def test_rt_light_sets_vs_oracle(rt, case):
     assert bad.size == 0, f"{case}: {bad.size} pixels differ, first {bad[:8]}"
 
 
+@pytest.mark.parametrize("yaw", [0.1745, -0.52, 0.9, 2.0, -1.5707964, 3.1415927])
+def test_rt_yaw_lattice_vs_oracle(rt, yaw):
+    """A yawed one-light camera (skeleton.cpp:233-244) takes the lattice
+    kernel's per-pixel-column form (cg_rt.hip lat_yaw): dir.x = fl(c x + s f)
+    per pixel, rows shared.  Ragged size (partial tiles on both edges); yaws
+    past 90 degrees make dir.x decrease along a row (the certificates' x extent
+    comes from the end pixels either way); -90 degrees makes c ~ 0."""
+    W, H, f = 200, 118, 150.0
+    R = cgamd.yaw_matrix(yaw)
+    cam_pos = (0.05, -0.1, -2.7, 1.0)
+    ref = oracle.rt_draw(oracle.rt_params(W, H, f, cam_pos, list(R)), threads=os.cpu_count() or 8)
+    argb, _ = rt.rt_render(cgamd.rt_camera(W, H, f, cam_pos, R))
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"yaw {yaw}: {bad.size} pixels differ, first {bad[:8]}"
+
+
+def test_rt_yaw_lattice_stripes_vs_oracle(rt):
+    """Yawed lattice on 15-row stripes (2 and 3 ranks), reassembled, against
+    the oracle's whole frame."""
+    torch = pytest.importorskip("torch")
+    W, H, f = 192, 150, 140.0
+    R = cgamd.yaw_matrix(-0.3)
+    cam_pos = (0.1, 0.05, -2.8, 1.0)
+    ref = oracle.rt_draw(oracle.rt_params(W, H, f, cam_pos, list(R)), threads=os.cpu_count() or 8)
+    cam = cgamd.rt_camera(W, H, f, cam_pos, R)
+    full, _ = rt.rt_render(cam)
+    assert int((full != ref).sum()) == 0
+    st = torch.cuda.Stream()
+    for n in (2, 3):
+        S = cgdist.LATTICE_STRIPE
+        rows = cgdist.shard_rows(H, n, S)
+        g = torch.zeros(n * rows * W, dtype=torch.int32, device="cuda")
+        for r in range(n):
+            rt.rt_render_device(cam, g.data_ptr() + r * rows * W * 4, cgamd.RtShard(r, n, S), st.cuda_stream)
+        frame = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        rt.rt_unstripe_device(g.data_ptr(), W, H, n, S, frame.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        assert np.array_equal(frame.cpu().numpy().view(np.uint32), ref), n
+
+
 def test_rt_probe_closest_and_direct_light(rt, golden):
     rays = golden["rt_rays"]
     out, hit = rt.rt_probe_closest([r["start"] for r in rays], [r["dir"] for r in rays])
