@@ -427,20 +427,21 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
     // 64 records per round trip: lane q loads record base+q (coalesced), a
     // ballot keeps those with a fragment in this segment, and the set bits are
     // walked in ascending order (= triangle order) with readlane broadcasts.
-    for (int base = 0; base < cnt; base += 64) {
+    // The first 64 are loaded beside the count (a row has A.n record slots;
+    // those past the count are read but never used).
+    for (int base = 0; base == 0 || base < cnt; base += 64) {
         const int q = base + lane;
         int mlx = 0, mrx = 0, msh = 0, mtex = 0, midx = 0;
         float mlz = 0.f, msz = 0.f, mlX = 0.f, msX = 0.f, mlY = 0.f, msY = 0.f;
-        bool ov = false;
-        if (q < cnt) {
+        if (q < A.n) {
             const RowRec &mr = rr[q];
             mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = rec_shadow(mr);
             if (TEX) {
                 mtex = mr.tex; midx = mr.index;
                 mlX = mr.lX; msX = mr.sX; mlY = mr.lY; msY = mr.sY;
             }
-            ov = !(mrx - 1 < x0 || mlx > x0 + kFillPx - 1);
         }
+        const bool ov = q < cnt && !(mrx - 1 < x0 || mlx > x0 + kFillPx - 1);
         unsigned long long m = __ballot(ov);
         while (m) {
             const int b = __builtin_ctzll(m);
@@ -531,11 +532,14 @@ __device__ __forceinline__ void shade3c(const RastArgs &A, float4 st, cg_vec3 co
 // soft-shadow darkening amount of a pixel whose 3x3 shadow neighbourhood is
 // sh[cy-1..cy+1][cx-1..cx+1] (row stride ld), 0 if not shadowed
 // (:286-303, :1725-1733; [y+1][x-1] counted twice, [y+1][x+1] omitted)
-__device__ __forceinline__ float darken_at(const int *sh, int ld, int cy, int cx)
+// (sh: the marks as ints, or the post state words with the mark in bit 31)
+template <class T>
+__device__ __forceinline__ float darken_at(const T *sh, int ld, int cy, int cx)
 {
-    const int *c = sh + cy * ld + cx;
-    if (c[0] != 1) return 0.0f;
-    int k = c[0] + c[-ld] + c[-ld - 1] + c[-ld + 1] + c[ld - 1] + c[ld] + c[ld - 1] + c[-1] + c[1];
+    const T *p = sh + cy * ld + cx;
+    auto c = [&](int o) { return sizeof(T) == 4 && (T)-1 > (T)0 ? (int)((uint32_t)p[o] >> 31) : (int)p[o]; };
+    if (c(0) != 1) return 0.0f;
+    int k = c(0) + c(-ld) + c(-ld - 1) + c(-ld + 1) + c(ld - 1) + c(ld) + c(ld - 1) + c(-1) + c(1);
     float val = div_const((float)k, 9.0f, 1.0f / 9.0f);                 // val /= 9.0f
     if ((double)val < 0.6) return 0.05f;
     if ((double)val < 0.7) return 0.08f;
@@ -556,36 +560,6 @@ constexpr int kPostTW = 64, kPostTH = 8;
 constexpr int kPostHW = kPostTW + 2, kPostHH = kPostTH + 2;      // shade halo 1
 constexpr int kPostSW = kPostTW + 4, kPostSH = kPostTH + 4;      // shadow halo 2
 
-// A shading fragment rebuilt from its row record (DrawPolygonRows' Interpolate,
-// :543-548) and shaded (PixelShader :559-645 + calculateIllumination :674-683).
-template <bool TEX>
-__device__ __forceinline__ void shade_from_record(const cg_rtri *__restrict__ tris, const RastArgs &A,
-                                                  const RowRec *__restrict__ rr, uint32_t st, int x, int y, vec3 &sc,
-                                                  vec3 &lo, vec3 &hi)
-{
-    const int rec = (int)(st & ~kStShadow) - 1;
-    if (rec < 0) {
-        sc = lo = hi = v3(0.f, 0.f, 0.f);
-        return;
-    }
-    const RowRec r = rr[rec];
-    const float fi = (float)(x - r.lx);
-    const float z = r.lz + (r.sz * fi);                                    // :543, as the fill evaluated it
-    const float X = r.lX + (r.sX * fi), Y = r.lY + (r.sY * fi);            // :547-548 numerators
-    const int t = rec_t(r);
-    const cg_vec4 tn = tris[t].normal;
-    vec3 N = v3(tn.x, tn.y, tn.z);
-    int tex = 0;
-    uint32_t texel = 0u;
-    if (TEX && r.tex != 0 && rast_tex_present(A, r.tex)) {
-        tex = r.tex;
-        N = rast_tex_normal(A, tex, r.index, z, X, Y, x, y, N, texel);
-    }
-    const vec3 D = illum_D(A, z, X, Y, N);                                 // :580-585 (:590-645)
-    const float4 s4 = make_float4(__int_as_float(t | (x == r.first_x ? (1 << 30) : 0)), D.x, D.y, D.z);
-    shade3c(A, s4, tris[t].color, sc, lo, hi, tex, texel);
-}
-
 template <bool DIRECT, bool TEX>
 __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A0,
                                                        const void *__restrict__ state_v,
@@ -598,7 +572,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         const cg_vec4 L = *A.d_light;
         A.light[0] = L.x; A.light[1] = L.y; A.light[2] = L.z;
     }
-    __shared__ int s_sh[kPostSH][kPostSW];
+    __shared__ int s_sh[DIRECT ? kPostSH : 1][DIRECT ? kPostSW : 1];   // colour modes 1-2: the marks
     __shared__ float s_c[9][kPostHH][kPostHW];      // sc.xyz, lo.xyz, hi.xyz
     __shared__ float s_d[kPostHH][kPostHW];
     const int W = A.W, H = A.H;
@@ -617,46 +591,103 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
     const float4 *st16 = static_cast<const float4 *>(state_v);
     // all global loads first (shadow marks, shade state), so each thread has them in flight together
     constexpr int kShR = (kPostSH * kPostSW + 255) / 256, kStR = (kPostHH * kPostHW + 255) / 256;
-    int shv[kShR];
+    // mode 0: the state words (record + 1, mark in bit 31) of the tile + halo 2
+    __shared__ uint32_t s_st[DIRECT ? 1 : kPostSH][DIRECT ? 1 : kPostSW];
+    uint32_t shv[kShR];
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
         const int i = threadIdx.x + 256 * r;
         const int cy = i / kPostSW, cx = i - cy * kPostSW;
         const int gx = gx0 - 2 + cx, gy = gy0 - 2 + cy;
         const bool in = i < kPostSH * kPostSW && gx >= 0 && gy >= 0 && gx < W && gy < H;
-        if (DIRECT) shv[r] = in ? sh[(size_t)gy * W + gx] : 0;
-        else shv[r] = in ? (int)(state_at((size_t)gy * W + gx) >> 31) : 0;
+        if (DIRECT) shv[r] = in ? (uint32_t)sh[(size_t)gy * W + gx] : 0u;
+        else shv[r] = in ? state_at((size_t)gy * W + gx) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
         const int i = threadIdx.x + 256 * r;
-        if (i < kPostSH * kPostSW) (&s_sh[0][0])[i] = shv[r];
+        if (i < kPostSH * kPostSW) {
+            if (DIRECT) (&s_sh[0][0])[i] = (int)shv[r];
+            else (&s_st[0][0])[i] = shv[r];
+        }
     }
     __syncthreads();
+    if constexpr (DIRECT) {
 #pragma unroll
-    for (int r = 0; r < kStR; ++r) {
-        const int i = threadIdx.x + 256 * r;
-        if (i >= kPostHH * kPostHW) break;
-        const int cy = i / kPostHW, cx = i - cy * kPostHW;
-        const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
-        vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
-        float d = 0.0f;
-        if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
-            const size_t o = (size_t)gy * W + gx;
-            if (DIRECT) {
-                const float4 s4 = st16[o];
+        for (int r = 0; r < kStR; ++r) {
+            const int i = threadIdx.x + 256 * r;
+            if (i >= kPostHH * kPostHW) break;
+            const int cy = i / kPostHW, cx = i - cy * kPostHW;
+            const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
+            vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
+            float d = 0.0f;
+            if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
+                const float4 s4 = st16[(size_t)gy * W + gx];
                 const int tb = __float_as_int(s4.x);
                 const bool tri = tb >= 0 && !(tb & kStateDirect);
                 shade3c(A, s4, tri ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f}, sc, lo, hi);
-            } else {
-                shade_from_record<TEX>(tris, A, recs + (size_t)gy * A.n, state_at(o), gx, gy, sc, lo, hi);
+                if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
             }
-            if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
+            s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
+            s_c[3][cy][cx] = lo.x; s_c[4][cy][cx] = lo.y; s_c[5][cy][cx] = lo.z;
+            s_c[6][cy][cx] = hi.x; s_c[7][cy][cx] = hi.y; s_c[8][cy][cx] = hi.z;
+            s_d[cy][cx] = d;
         }
-        s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
-        s_c[3][cy][cx] = lo.x; s_c[4][cy][cx] = lo.y; s_c[5][cy][cx] = lo.z;
-        s_c[6][cy][cx] = hi.x; s_c[7][cy][cx] = hi.y; s_c[8][cy][cx] = hi.z;
-        s_d[cy][cx] = d;
+    } else {
+        // The shading fragments of the tile + halo 1: each thread's record
+        // loads go out together, then their triangles', then the arithmetic --
+        // two dependent round trips instead of two per pixel.
+        RowRec rv[kStR];
+        int recv[kStR];
+#pragma unroll
+        for (int r = 0; r < kStR; ++r) {
+            const int i = threadIdx.x + 256 * r;
+            const int cy = i / kPostHW, cx = i - cy * kPostHW;
+            const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
+            const bool in = i < kPostHH * kPostHW && gx >= 0 && gy >= 0 && gx < W && gy < H;
+            recv[r] = in ? (int)(s_st[cy + 1][cx + 1] & ~kStShadow) - 1 : -1;
+            if (recv[r] >= 0) rv[r] = recs[(size_t)gy * A.n + recv[r]];
+        }
+        cg_vec4 tnv[kStR];
+        cg_vec3 colv[kStR];
+#pragma unroll
+        for (int r = 0; r < kStR; ++r)
+            if (recv[r] >= 0) {
+                const int t = rec_t(rv[r]);
+                tnv[r] = tris[t].normal;
+                colv[r] = tris[t].color;
+            }
+#pragma unroll
+        for (int r = 0; r < kStR; ++r) {
+            const int i = threadIdx.x + 256 * r;
+            if (i >= kPostHH * kPostHW) break;
+            const int cy = i / kPostHW, cx = i - cy * kPostHW;
+            const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
+            vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
+            float d = 0.0f;
+            if (recv[r] >= 0) {   // a shading fragment (:580-585, rebuilt as shade_from_record does)
+                const RowRec &R = rv[r];
+                const float fi = (float)(gx - R.lx);
+                const float z = R.lz + (R.sz * fi);                               // :543, as the fill evaluated it
+                const float X = R.lX + (R.sX * fi), Y = R.lY + (R.sY * fi);       // :547-548 numerators
+                const int t = rec_t(R);
+                vec3 N = v3(tnv[r].x, tnv[r].y, tnv[r].z);
+                int tex = 0;
+                uint32_t texel = 0u;
+                if (TEX && R.tex != 0 && rast_tex_present(A, R.tex)) {
+                    tex = R.tex;
+                    N = rast_tex_normal(A, tex, R.index, z, X, Y, gx, gy, N, texel);
+                }
+                const vec3 D = illum_D(A, z, X, Y, N);                            // :580-585 (:590-645)
+                const float4 s4 = make_float4(__int_as_float(t | (gx == R.first_x ? (1 << 30) : 0)), D.x, D.y, D.z);
+                shade3c(A, s4, colv[r], sc, lo, hi, tex, texel);
+            }
+            if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_st[0][0], kPostSW, cy + 1, cx + 1);
+            s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
+            s_c[3][cy][cx] = lo.x; s_c[4][cy][cx] = lo.y; s_c[5][cy][cx] = lo.z;
+            s_c[6][cy][cx] = hi.x; s_c[7][cy][cx] = hi.y; s_c[8][cy][cx] = hi.z;
+            s_d[cy][cx] = d;
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kPostTH * kPostTW; i += 256) {
