@@ -538,8 +538,9 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_pixel_kernel(RtFra
 }
 
 // ---------------------------------------------------------------------------
-// Lattice form of Draw (skeleton.cpp:104-169) for an unrotated camera and one
-// light -- the C2 configuration.  With R the identity, a pixel's direction is
+// Lattice form of Draw (skeleton.cpp:104-169) for one light -- the C2
+// configuration; described here for the unrotated camera (shared columns; a
+// yawed camera keeps per-pixel columns, see lat_yaw).  With R the identity, a pixel's direction is
 // (u - W/2, v - H/2) exactly (mat4_mul adds only +-0 terms), and sub-ray
 // (i, j) is (x + 0.5 i, y + 0.5 j), exactly representable: the 9 sub-rays of
 // all pixels lie on a half-pixel lattice, and pixel (u, v)'s sub-ray (i, j) IS
@@ -822,7 +823,8 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
 
 // ---------------------------------------------------------------------------
 // Lattice form of Draw for a light set (C4's 8 x 8 area light: 2..64 lights),
-// unrotated camera.  A pixel forms
+// described for the unrotated camera (per-pixel columns under a yaw: column c
+// folds into pixel c/3 alone).  A pixel forms
 //   pc = (((0 + DL(s0, l0)) + DL(s0, l1)) + ... + DL(s0, l_last)) + amb(s0) + DL(s1, l0) ...
 // (:134-157): each lattice ray's per-light values are pixel-independent, but
 // their sum is not -- float addition is ordered -- so a pixel needs every
@@ -873,6 +875,7 @@ constexpr int kLatMaxLights = 64;
 // lights contiguous and in order, so one ds_read_b128 still yields l .. l + 3.
 __device__ __forceinline__ int lat_swz(int r, int c) { return 4 * ((r * 3 + c) & 15); }
 
+template <int PITCH>
 __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtTri *__restrict__ tc,
                                                     const RtShade *__restrict__ shade,
                                                     const RtSphere *__restrict__ sph,
@@ -890,15 +893,15 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int by = lat_tile_row();
     LatTile G = lat_tile(F, blockIdx.x, by);
-    G.yaw = false;   // shared columns only (rt_lattice_ok)
-    const int ax0 = G.ax0, ay0 = G.ay0, cols = G.cols, rows = G.rows;
-    __shared__ float2 s_hit[kLatN];                                   // (t, hit index bits)
+    G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
+    const int ay0 = G.ay0, cols = G.cols, rows = G.rows;
+    __shared__ float2 s_hit[PITCH * kLatH];                                   // (t, hit index bits)
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ float s_dl[2][kLatHalfRows][3][kLatMaxLights];         // column buffers
     __shared__ float s_pc[kLatTileH][kLatTileW][3];                   // pixel sums
     __shared__ uint8_t s_valid[kLatTileH][kLatTileW];
     lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
-    const int npts = kLatW * rows;
+    const int npts = PITCH * rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
     if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window
     const size_t tix = (size_t)by * gridDim.x + blockIdx.x;
@@ -922,7 +925,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
         }
     }
     __syncthreads();                       // s_obj
-    lat_closest<kLatW>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
+    lat_closest<PITCH>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_hit[p] = make_float2(t, __int_as_float(bi));
     });
     __syncthreads();
@@ -931,23 +934,24 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     // forms it below), plus the own-triangle certificate when every hit of the
     // unit lies on one triangle -- the same exact functions as
     // rt_tile_cert_kernel, over a box of up to 17 points instead of the tile's.
-    __shared__ unsigned long long s_umask[kLatParts][kLatW];
+    __shared__ unsigned long long s_umask[kLatParts][PITCH];
     // the units' boxes and sole hit triangles (-1: several, -2: no hit) live
     // in the column buffers, which the sweep below has not started using yet
-    static_assert(sizeof(s_dl) / 2 >= kLatParts * kLatW * 6 * sizeof(float), "unit scratch");
-    float(*s_ubox)[kLatW][6] = (float(*)[kLatW][6]) & s_dl[0][0][0][0];
-    int(*s_uone)[kLatW] = (int(*)[kLatW]) & s_dl[1][0][0][0];
+    static_assert(sizeof(s_dl) / 2 >= kLatParts * PITCH * 6 * sizeof(float), "unit scratch");
+    static_assert(kLatParts * PITCH <= kRtThreads, "a thread per unit");
+    float(*s_ubox)[PITCH][6] = (float(*)[PITCH][6]) & s_dl[0][0][0][0];
+    int(*s_uone)[PITCH] = (int(*)[PITCH]) & s_dl[1][0][0][0];
     const int nhalf = (G.nv + kLatHalfH - 1) / kLatHalfH;
-    if (threadIdx.x < kLatParts * kLatW) {
-        const int h = threadIdx.x / kLatW, cx = threadIdx.x - h * kLatW;
+    if (threadIdx.x < kLatParts * PITCH) {
+        const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
         if (h < nhalf && cx < cols) {
             const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
             LanePosBox pb;
             pb.init();
             int one = -2;
-            const float X = 0.5f * (float)(ax0 + cx);
+            const float X = lat_x(F, G, cx);
             for (int r = 0; r < nlr; ++r) {
-                const float2 hq = s_hit[(lr0 + r) * kLatW + cx];
+                const float2 hq = s_hit[(lr0 + r) * PITCH + cx];
                 const int bi = __float_as_int(hq.y);
                 if (bi == INT_MIN) continue;
                 const float Y = 0.5f * (float)(ay0 + lr0 + r), t = hq.x;
@@ -964,10 +968,10 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     }
     __syncthreads();
     {
-        const int nc = __popcll(smask), pairs = nhalf * kLatW * nc;
+        const int nc = __popcll(smask), pairs = nhalf * PITCH * nc;
         for (int it = threadIdx.x; it < pairs; it += kRtThreads) {
             const int unit = it / nc, ci = it - unit * nc;
-            const int h = unit / kLatW, cx = unit - h * kLatW;
+            const int h = unit / PITCH, cx = unit - h * PITCH;
             if (cx >= cols) continue;
             const int one = s_uone[h][cx];
             if (one == -2) continue;   // no hit, no shadow ray
@@ -975,7 +979,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
             const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
             const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
-            const float X = 0.5f * (float)(ax0 + cx);
+            const float X = lat_x(F, G, cx);
             const float y0 = 0.5f * (float)(ay0 + lr0), y1 = 0.5f * (float)(ay0 + lr0 + nlr - 1);
             if (lat_unit_keeps(F, tc[k], s_obj[k], one == k, X, y0, y1, lo, hi))
                 atomicOr(&s_umask[h][cx], 1ull << k);
@@ -983,10 +987,10 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
         // bit 63: a sphere may block a shadow ray of the unit -- the
         // sphere-shadow certificate of every light over the unit's hit box
         // (the tile's flag, rt_tile_cert_kernel, covers the whole tile)
-        const int spairs = Fs.n_sph > 0 ? nhalf * kLatW * F.n_lights : 0;
+        const int spairs = Fs.n_sph > 0 ? nhalf * PITCH * F.n_lights : 0;
         for (int it = threadIdx.x; it < spairs; it += kRtThreads) {
             const int unit = it / F.n_lights, l = it - unit * F.n_lights;
-            const int h = unit / kLatW, cx = unit - h * kLatW;
+            const int h = unit / PITCH, cx = unit - h * PITCH;
             if (cx >= cols || s_uone[h][cx] == -2) continue;
             const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
             const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
@@ -1021,10 +1025,10 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                 const unsigned long long um = um0 & ~(1ull << 63);
                 RtFrame Fu = Fs;                      // spheres only where one may block
                 if (!(um0 >> 63)) Fu.n_sph = 0;
-                const float X = 0.5f * (float)(ax0 + cx);
+                const float X = lat_x(F, G, cx);
                 auto item = [&](int r, int l, const RtLight &Lt) {
                     const int cy = lr0 + r;
-                    const float2 hq = s_hit[cy * kLatW + cx];
+                    const float2 hq = s_hit[cy * PITCH + cx];
                     const int bi = __float_as_int(hq.y);
                     if (bi == INT_MIN) return;
                     const float Y = 0.5f * (float)(ay0 + cy), t = hq.x;
@@ -1046,8 +1050,10 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             }
             if (step > 0 && folder) {   // fold column step - 1 into its pixels
                 const int cx = step - 1;
-                const int tx = fk == 0 ? cx / 2 : cx / 2 - 1;
-                const bool use = fpr < npr && tx >= 0 && tx < G.nu && (fk == 0 || (cx & 1) == 0);
+                // shared columns: an even column is the first of pixel cx/2 and
+                // the last of cx/2 - 1; per-pixel columns: column cx is pixel cx/3's
+                const int tx = G.yaw ? cx / 3 : (fk == 0 ? cx / 2 : cx / 2 - 1);
+                const bool use = fpr < npr && tx >= 0 && tx < G.nu && (fk == 0 || (!G.yaw && (cx & 1) == 0));
                 if (use) {
                     const int ty = pr0 + fpr;
                     float pc = s_pc[ty][tx][fcomp];
@@ -1055,7 +1061,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                     const float *buf = &s_dl[cx & 1][0][0][0];
                     for (int j = 0; j < 3; ++j) {
                         const int r = 2 * fpr + j;
-                        const int bi = __float_as_int(s_hit[(lr0 + r) * kLatW + cx].y);
+                        const int bi = __float_as_int(s_hit[(lr0 + r) * PITCH + cx].y);
                         if (bi == INT_MIN) continue;
                         valid = true;
                         const float *b = buf + (r * 3 + fcomp) * kLatMaxLights;
@@ -1115,6 +1121,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
     lat_signal(frame_done, blockIdx.z);
 }
 
+template <int PITCH>
 __global__ __launch_bounds__(kRtThreads, 5) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                           const RtShade *__restrict__ shade,
                                                                           const RtSphere *__restrict__ sph,
@@ -1123,7 +1130,7 @@ __global__ __launch_bounds__(kRtThreads, 5) void rt_lattice_lights_kernel(RtFram
                                                                           uint32_t *__restrict__ out,
                                                                           uint32_t *frame_done)
 {
-    lattice_lights_body(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
+    lattice_lights_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
     lat_signal(frame_done, blockIdx.z);
 }
 
@@ -1324,15 +1331,14 @@ size_t rt_sup_units(const RtFrame &F) { return (size_t)rt_cert_units(F, 1); }
 // The lattice kernels' precondition (lat_yaw): dir.y = y (R's y row (0, 1, 0,
 // 0) up to the sign of its zeros) and dir.x a function of x alone (R's y
 // weight +-0) -- shared columns when dir.x = x exactly (x row (1, 0, 0, 0)),
-// else per-pixel columns, which the one-light kernel handles (entries bounded,
-// so dir.x stays finite and monotone); pixel offsets stay far inside float's
+// else per-pixel columns (entries bounded, so dir.x stays finite and
+// monotone); pixel offsets stay far inside float's
 // exact integer range, and tiles do not straddle stripes.
 static bool rt_lattice_ok(const RtFrame &F)
 {
     const float *R = F.R;
     if (!(R[1] == 0.0f && R[5] == 1.0f && R[9] == 0.0f && R[13] == 0.0f && R[4] == 0.0f)) return false;
     if (lat_yaw(F)) {
-        if (F.n_lights != 1) return false;
         for (int k : {0, 8, 12})
             if (!(fabsf(R[k]) <= 1e6f)) return false;
         if (!(fabsf(F.focal) <= 1e6f)) return false;
@@ -1367,8 +1373,11 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
     else if (F.n_lights == 1)
         hipLaunchKernelGGL(rt_lattice_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
                            cams, out_stride, d_out, d_done);
+    else if (lat_yaw(F))
+        hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+                           d_lat_masks, cams, out_stride, d_out, d_done);
     else
-        hipLaunchKernelGGL(rt_lattice_lights_kernel, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+        hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, out_stride, d_out, d_done);
     return hipGetLastError();
 }

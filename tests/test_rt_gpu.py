@@ -84,18 +84,22 @@ _LIGHT_SET = [((0.0, -0.5, -0.7, 1.0), (14.0, 14.0, 14.0)), ((0.3, -0.6, 0.2, 1.
               ((0.0, -0.9, 0.0, 1.0), (2.5, 2.5, 2.5))]
 
 
-@pytest.mark.parametrize("case", ["lattice5", "lattice64", "yaw5", "yaw64"])
+_SET_YAWS = {"yaw5": 0.1, "yaw64": 0.1, "yaw2_5": 2.0, "yawneg_64": -0.52}
+
+
+@pytest.mark.parametrize("case", ["lattice5", "lattice64", "yaw5", "yaw64", "yaw2_5", "yawneg_64"])
 def test_rt_light_sets_vs_oracle(rt, case):
     """Light sets against the live oracle at a ragged size (partial lattice
-    tiles on both edges): unrotated cameras take rt_lattice_lights_kernel,
-    yawed ones rt_pixel_kernel.  5 lights (not a multiple of the fold's
-    4-light vector reads) and C4's 8 x 8 area light."""
+    tiles on both edges): rt_lattice_lights_kernel, unrotated cameras with
+    shared lattice columns, yawed ones (also past 90 degrees, dir.x decreasing)
+    with per-pixel columns.  5 lights (not a multiple of the fold's 4-light
+    vector reads) and C4's 8 x 8 area light."""
     W, H, f = 200, 118, 150.0
     if case.endswith("64"):
         lights = oracle.rt_area_lights((0.0, -0.5, -0.7, 1.0), (14.0, 14.0, 14.0), 0.1, 8)
     else:
         lights = _LIGHT_SET
-    R = cgamd.yaw_matrix(0.1) if case.startswith("yaw") else None
+    R = cgamd.yaw_matrix(_SET_YAWS[case]) if case.startswith("yaw") else None
     cam_pos = (0.05, -0.1, -2.7, 1.0)
     p = oracle.rt_params(W, H, f, cam_pos, list(R) if R is not None else None, lights=lights)
     ref = oracle.rt_draw(p, threads=os.cpu_count() or 8)
