@@ -427,13 +427,11 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
     // 64 records per round trip: lane q loads record base+q (coalesced), a
     // ballot keeps those with a fragment in this segment, and the set bits are
     // walked in ascending order (= triangle order) with readlane broadcasts.
-    // The first 64 are loaded beside the count (a row has A.n record slots;
-    // those past the count are read but never used).
-    for (int base = 0; base == 0 || base < cnt; base += 64) {
+    for (int base = 0; base < cnt; base += 64) {
         const int q = base + lane;
         int mlx = 0, mrx = 0, msh = 0, mtex = 0, midx = 0;
         float mlz = 0.f, msz = 0.f, mlX = 0.f, msX = 0.f, mlY = 0.f, msY = 0.f;
-        if (q < A.n) {
+        if (q < cnt) {
             const RowRec &mr = rr[q];
             mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = rec_shadow(mr);
             if (TEX) {

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU session collecting the round's profiles (kernel stats, PMC HBM
 # traffic, SQ executed-work counters) for every bench workload; each step has
-# its own time limit and a failure stops the script.  Then on the CPU:
+# its own time limit and a failure stops the script (WLS="rt rast ..." limits
+# the workloads).  Then on the CPU:
 #   scripts/collect_profiles.sh rNN ; python3 scripts/sq_summary.py ... (see below)
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -17,10 +18,13 @@ run() {  # name timeout cmd...
   [ $rc -eq 0 ] || { tail -5 "$OUT/$name.log"; exit $rc; }
 }
 B="python3 $ROOT/bench.py --no-cpu-baseline"
-for w in rt rast c4 c5 yaw; do
+WLS=${WLS:-rt rast c4 c5 yaw}
+has() { case " $WLS " in *" $1 "*) return 0;; esac; return 1; }
+for w in $WLS; do
   run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-rast
 done
 for wl in rt rast; do
+  has $wl || continue
   for ctr in FETCH_SIZE WRITE_SIZE; do
     run pmc_${wl}_$ctr 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${wl}_$ctr" -o pmc -- $B --workload $wl --steps 64 --warmup 32 --no-rast
   done
@@ -29,7 +33,8 @@ G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CY
 G2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"
 G3="SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_TRANS_F SQ_INSTS_VALU_CVT SQ_INST_LEVEL_SMEM"
 for w in rt c4 c5 yaw rast; do
-  case $w in rt|c4) S="--steps 32 --warmup 32";; rast) S="--steps 64 --warmup 64";; *) S="--steps 4 --warmup 2";; esac
+  has $w || continue
+  case $w in rt|c4|yaw) S="--steps 32 --warmup 32";; rast) S="--steps 64 --warmup 64";; *) S="--steps 4 --warmup 2";; esac
   i=0
   for g in "$G1" "$G2" "$G3"; do
     i=$((i+1))
