@@ -671,14 +671,21 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     unsigned long long *lat = (unsigned long long *)blat.p;
     CG_TRY(c, bsup.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
     unsigned long long *supm = (unsigned long long *)bsup.p;
-    // certificates on aux, after the slot's previous reader
-    hipStream_t cst = c->aux;
-    CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
+    // certificates on aux, after the slot's previous reader, so that they run
+    // beside the lattice launch still queued before them.  A cold call (every
+    // earlier lattice launch of this context complete: nothing to run beside)
+    // keeps them on the caller's stream -- the cross-stream wait would leave
+    // the GPU idle for ~12 us between certificates and lattice.
+    const bool cold = hipEventQuery(c->ev_lat[0]) == hipSuccess && hipEventQuery(c->ev_lat[1]) == hipSuccess;
+    hipStream_t cst = cold ? st : c->aux;
+    if (!cold) CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)btc.p,
                                 (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm),
            "rt_prepare launch");
-    CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
-    CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
+    if (!cold) {
+        CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
+        CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
+    }
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
                                        (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st,
                                        d_done),
