@@ -128,6 +128,24 @@ def test_rt_yaw_lattice_vs_oracle(rt, yaw):
     assert bad.size == 0, f"yaw {yaw}: {bad.size} pixels differ, first {bad[:8]}"
 
 
+@pytest.mark.parametrize("W,H,yaw,nl", [(1, 1, 0.3, 1), (17, 9, -2.5, 1), (33, 31, 0.3, 5), (15, 16, 1.2, 5)])
+def test_rt_yaw_lattice_small_frames(rt, W, H, yaw, nl):
+    """Yawed lattice kernels on frames smaller than / not multiples of a
+    16 x 15 tile (a single pixel, partial tiles only), one light and a
+    5-light set, against the live oracle."""
+    f = 40.0
+    R = cgamd.yaw_matrix(yaw)
+    cam_pos = (0.02, -0.05, -2.8, 1.0)
+    lights = _LIGHT_SET[:nl]
+    ref = oracle.rt_draw(oracle.rt_params(W, H, f, cam_pos, list(R), lights=lights), threads=4)
+    arr = (cgamd.Light * nl)()
+    for i, (pos, col) in enumerate(lights):
+        arr[i].position = cgamd.Vec4(*pos)
+        arr[i].colour = cgamd.Vec3(*col)
+    argb, _ = rt.rt_render(cgamd.rt_camera(W, H, f, cam_pos, R), arr)
+    assert np.array_equal(argb, ref), f"{W}x{H} yaw {yaw}: {int((argb != ref).sum())} pixels differ"
+
+
 def test_rt_yaw_lattice_stripes_vs_oracle(rt):
     """Yawed lattice on 15-row stripes (2 and 3 ranks), reassembled, against
     the oracle's whole frame."""
