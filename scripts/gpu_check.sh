@@ -31,6 +31,7 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench_c4 300 python bench.py --workload c4 --steps 30 --warmup 3
   step bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 2
   step bench_yaw 300 python bench.py --workload yaw
+  step bench_f256 300 python bench.py --workload f256
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
