@@ -103,6 +103,7 @@ struct BigBufs {
     double litD[3], lit_pn;
     int bins_x, bins_y, tiles_x, tiles_y;
     int lat_w, lat_h;             // lattice mode: (2 W + 1) x (2 rows + 1) points; 0 = per-pixel mode
+    int lat_yaw;                  // lattice columns per pixel (yawed camera): 3 W x (2 rows + 1) points
     int *sup_pool;                // [cap_sup] triangles the super-bins' certificates keep
     Chunk *sup_chunk;             // [n_sups][nch]
     int *sup_pre, *sup_tot;       // [n_sups][nch], [n_sups] (as bin_pre / bin_tot)
@@ -784,27 +785,37 @@ __device__ __forceinline__ LatOwn lat_own(const RtFrame &F, const BigBufs &B, in
 {
     LatOwn o;
     const int rows = min(F.rows_out, F.H - F.row0);    // rows with v < H
-    o.xi0 = 16 * tx;
+    const int cw = B.lat_yaw ? 24 : 16;                  // lattice columns of 8 pixels
+    o.xi0 = cw * tx;
     o.yi0 = 16 * ty;
-    const int xe = tx == (F.W - 1) / 8 ? B.lat_w : min(16 * tx + 16, B.lat_w);
+    const int xe = tx == (F.W - 1) / 8 ? B.lat_w : min(cw * tx + cw, B.lat_w);
     const int ye = ty == (rows - 1) / 8 ? B.lat_h : min(16 * ty + 16, B.lat_h);
     o.nx = max(0, xe - o.xi0);
     o.ny = ty > (rows - 1) / 8 ? 0 : max(0, ye - o.yi0);
     return o;
 }
-__device__ __forceinline__ float lat_x(const RtFrame &F, int Xi) { return 0.5f * (float)(Xi - 1 - 2 * (F.W / 2)); }
+// x of lattice column Xi: the half-pixel lattice, or (yawed camera, see
+// cg_rt.hip lat_yaw) pixel Xi / 3's sub-ray i = Xi % 3 - 1, fl(dir.x + 0.5 i)
+// -- dir.x formed with y = 0, which only changes the sign of a zero dir.x.
+__device__ __forceinline__ float lat_x(const RtFrame &F, const BigBufs &B, int Xi)
+{
+    if (!B.lat_yaw) return 0.5f * (float)(Xi - 1 - 2 * (F.W / 2));
+    const int u = Xi / 3, i = Xi - 3 * u - 1;
+    return mat4_mul(F.R, v4((float)(u - F.W / 2), 0.0f, F.focal, 1.0f)).x + (0.5f * (float)i);   // :126-137
+}
 __device__ __forceinline__ float lat_y(const RtFrame &F, int Yi)
 {
     return 0.5f * (float)(Yi - 1 + 2 * F.row0 - 2 * (F.H / 2));
 }
 
 // K1: closest hits of every ray slot of the tile.
-template <bool kLat>
+template <int LM>   // 0: per-pixel mode, 1: lattice, 2: lattice with per-pixel columns
 __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                     const RtShade *__restrict__ shade,
                                                                     const RtSphere *__restrict__ sph, BigBufs B)
 {
-    constexpr int NS = kLat ? 5 : 9;
+    constexpr bool kLat = LM > 0;
+    constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
@@ -825,7 +836,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, c
             const int k = s * 64 + lane;
             on[s] = k < n;
             const int kk = on[s] ? k : 0;
-            rx[s] = lat_x(F, o.xi0 + kk % max(o.nx, 1));
+            rx[s] = lat_x(F, B, o.xi0 + kk % max(o.nx, 1));
             ry[s] = lat_y(F, o.yi0 + kk / max(o.nx, 1));
             if (on[s]) {
                 a0 = fminf(a0, rx[s]); a1 = fmaxf(a1, rx[s]);
@@ -1169,12 +1180,13 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // n_lights + l, lattice mode point bits l.  Every lane walks the same (slot,
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
-template <bool kLat>
+template <int LM>
 __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
 {
-    constexpr int NS = kLat ? 5 : 9;
+    constexpr bool kLat = LM > 0;
+    constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
@@ -1206,7 +1218,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, 
             const int k = s * 64 + lane;
             on = k < n;
             const int kk = on ? k : 0, Xi = o.xi0 + kk % max(o.nx, 1), Yi = o.yi0 + kk / max(o.nx, 1);
-            nd = v3(lat_x(F, Xi), lat_y(F, Yi), F.focal);
+            nd = v3(lat_x(F, B, Xi), lat_y(F, Yi), F.focal);
             id = (size_t)Yi * B.lat_w + Xi;
             shadowed = pending = 0ull;
         } else {
@@ -1504,12 +1516,13 @@ __global__ __launch_bounds__(256) void rt_pending_lit_kernel(RtFrame F, const Rt
 // (per sub-ray in per-pixel mode, per lattice point in lattice mode); with
 // more than 7 lights in per-pixel mode each (s, l) is resolved here (grid,
 // then the bin's certified shadow list).
-template <bool kLat>
+template <int LM>
 __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph, BigBufs B,
                                                                   uint32_t *__restrict__ out)
 {
+    constexpr bool kLat = LM > 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
@@ -1534,7 +1547,8 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
         for (int s = 0; s < 9; ++s) {
             const int i = s / 3 - 1, j = s % 3 - 1;
             const vec3 nd = v3(dir.x + (m * (float)i), dir.y + (m * (float)j), F.focal);   // :137
-            const size_t id = kLat ? (size_t)(2 * L + j + 1) * B.lat_w + (2 * u + i + 1) : s * npix + pix;
+            const size_t id = kLat ? (size_t)(2 * L + j + 1) * B.lat_w + ((LM == 2 ? 3 : 2) * u + i + 1)
+                                   : s * npix + pix;
             int bi;
             vec3 pos, normal;
             hit_geometry(F, B, shade, sph, nd, id, bi, pos, normal);
@@ -1567,15 +1581,21 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
 }
 
 // ---------------------------------------------------------------------------
-// Lattice mode (K1): unrotated camera, contiguous rows (whole frame or band),
-// verdict bits for every light in one word per point.
-static bool rt_big_lattice(const RtFrame &F)
+// Lattice mode (K1): contiguous rows (whole frame or band), verdict bits for
+// every light in one word per point, and R leaving y alone with dir.x a
+// function of x alone (cg_rt.hip rt_lattice_ok): 1 = shared half-pixel
+// columns (dir.x = x exactly), 2 = per-pixel columns (a yaw; bounded entries).
+int rt_big_mode(const RtFrame &F)
 {
-    for (int r = 0; r < 4; ++r)
-        for (int c = 0; c < 4; ++c)
-            if (F.R[4 * c + r] != (r == c ? 1.0f : 0.0f)) return false;
-    return F.nranks == 1 && F.n_lights <= 64 && F.W < (1 << 20) && F.H < (1 << 20);
+    const float *R = F.R;
+    if (!(R[1] == 0.0f && R[5] == 1.0f && R[9] == 0.0f && R[13] == 0.0f && R[4] == 0.0f)) return 0;
+    if (!(F.nranks == 1 && F.n_lights <= 64 && F.W < (1 << 20) && F.H < (1 << 20))) return 0;
+    if (R[0] == 1.0f && R[8] == 0.0f && R[12] == 0.0f) return 1;
+    for (int k : {0, 8, 12})
+        if (!(std::fabs(R[k]) <= 1e6f)) return 0;
+    return std::fabs(F.focal) <= 1e6f ? 2 : 0;
 }
+static bool rt_big_lattice(const RtFrame &F) { return rt_big_mode(F) != 0; }
 
 BigBufs big_layout(const RtFrame &F, const BigCaps &caps)
 {
@@ -1592,8 +1612,10 @@ BigBufs big_layout(const RtFrame &F, const BigCaps &caps)
     B.cap_sbin = caps.sbin;
     B.cap_sorted = caps.sorted;
     const int rows = std::min(F.rows_out, F.H - F.row0);
-    if (rt_big_lattice(F) && rows > 0) {
-        B.lat_w = 2 * F.W + 1;
+    const int mode = rt_big_mode(F);
+    if (mode && rows > 0) {
+        B.lat_yaw = mode == 2;
+        B.lat_w = mode == 2 ? 3 * F.W : 2 * F.W + 1;
         B.lat_h = 2 * rows + 1;
     }
     return B;
@@ -1744,20 +1766,32 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     };
     if (dry == 1) return demand();
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
-    if (lat) hipLaunchKernelGGL(rt_big_primary_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-    else hipLaunchKernelGGL(rt_big_primary_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+    if (lat && B.lat_yaw)
+        hipLaunchKernelGGL(rt_big_primary_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+    else if (lat)
+        hipLaunchKernelGGL(rt_big_primary_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+    else
+        hipLaunchKernelGGL(rt_big_primary_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     if (!flags_fit) {
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
         hipLaunchKernelGGL(rt_bin_shadow_kernel, bgrid, dim3(256), 0, st, F, d_tc, B);
         if (dry == 2) return demand();
     } else if (F.n_lights > 0) {
         hipLaunchKernelGGL(rt_lit_class_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
-        if (lat) hipLaunchKernelGGL(rt_shadow_hints_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-        else hipLaunchKernelGGL(rt_shadow_hints_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        if (lat && B.lat_yaw)
+            hipLaunchKernelGGL(rt_shadow_hints_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        else if (lat)
+            hipLaunchKernelGGL(rt_shadow_hints_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        else
+            hipLaunchKernelGGL(rt_shadow_hints_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         hipLaunchKernelGGL(rt_pending_lit_kernel, dim3(1024), dim3(256), 0, st, F, d_tc, B);
     }
-    if (lat) hipLaunchKernelGGL(rt_big_shade_kernel<true>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
-    else hipLaunchKernelGGL(rt_big_shade_kernel<false>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    if (lat && B.lat_yaw)
+        hipLaunchKernelGGL(rt_big_shade_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    else if (lat)
+        hipLaunchKernelGGL(rt_big_shade_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
+    else
+        hipLaunchKernelGGL(rt_big_shade_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
     return demand();   // the pools' demand, for the host's sizing of the next frames
 }
 

@@ -28,6 +28,7 @@ size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, int);
 bool rt_big_shadow_lists(const RtFrame &);
+int rt_big_mode(const RtFrame &);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
 size_t rt_big_scratch_bytes(const RtFrame &, const BigCaps &);
 hipError_t launch_rt_unstripe(const uint32_t *, int, int, int, int, int, int, uint32_t *, hipStream_t);
@@ -568,10 +569,9 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
         c->big_caps = BigCaps{g, g, 4096, 2 * g};
     }
     // a new frame shape or path (lattice / per-pixel, many lights) is sized again
-    bool ident = true;
-    for (int k = 0; k < 16; ++k) ident &= F.R[k] == ((k % 5 == 0) ? 1.0f : 0.0f);
+    const int mode = rt_big_mode(F);   // per-pixel / lattice / lattice with per-pixel columns
     const int lclass = F.n_lights == 0 ? 0 : F.n_lights <= 7 ? 1 : F.n_lights <= 64 ? 2 : 3;
-    const long long key = ((((long long)F.W * 65536 + F.rows_out) * 4 + lclass) * 2 + ident) * 2 + (F.nranks == 1);
+    const long long key = ((((long long)F.W * 65536 + F.rows_out) * 4 + lclass) * 4 + mode) * 2 + (F.nranks == 1);
     if (key != c->big_key) {
         c->big_key = key;
         c->big_sized = false;

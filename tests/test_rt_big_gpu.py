@@ -1,11 +1,13 @@
 """GPU: the large-scene path (n_tris > 64, cg_rt_big.hip) in every mode it
 has, against the live oracle's whole frame, bit-exact (tolerance 0):
 
-* lattice mode (unrotated camera): one light (C5's shape) and 16 lights
-  (one verdict word per lattice point);
-* per-pixel mode: a yawed camera (raytracer/Source/skeleton.cpp:233-244) with
-  one light, and the many-light path (certified per-bin shadow lists) for 16
-  lights under yaw and for 81 lights (more than a lattice word holds);
+* lattice mode, unrotated camera (shared half-pixel columns): one light
+  (C5's shape) and 16 lights (one verdict word per lattice point);
+* lattice mode, yawed camera (raytracer/Source/skeleton.cpp:233-244; per-pixel
+  lattice columns, rows shared): one light and 16 lights;
+* per-pixel mode: a pitched camera (R turns y: no lattice) with one light, and
+  the many-light path (certified per-bin shadow lists) for 16 lights under the
+  pitch and for 81 lights (more than a lattice word holds);
 * each also with the pools pinned far too small (every list overflows: the
   consumers' fallback over all triangles) and with a one-entry pending queue
   (the shading kernel's per-lane lit search)."""
@@ -23,11 +25,24 @@ pytestmark = pytest.mark.gpu
 L0 = [[0.0, -0.5, -0.7, 1.0], [14.0, 14.0, 14.0]]
 SCENE = dict(random=500, seed=0x5EED)
 YAW = mg.yaw_R(np.float32(0.0) - np.float32(0.174533))
+
+
+def _pitch(a):
+    """Rotation about x (column-major m[4 c + r]), float32 cos/sin."""
+    c, sn = float(np.cos(np.float32(a), dtype=np.float32)), float(np.sin(np.float32(a), dtype=np.float32))
+    m = [1.0 if k % 5 == 0 else 0.0 for k in range(16)]
+    m[1 * 4 + 1], m[1 * 4 + 2], m[2 * 4 + 1], m[2 * 4 + 2] = c, sn, -sn, c
+    return m
+
+
+PITCH = _pitch(0.15)
 CASES = {
     "lat_1": dict(R=None, lights=[L0]),
     "lat_area16": dict(R=None, lights=[L0], area=dict(side=0.1, n=4)),
-    "pix_yaw_1": dict(R=YAW, lights=[L0]),
-    "pix_yaw_area16": dict(R=YAW, lights=[L0], area=dict(side=0.1, n=4)),
+    "yawlat_1": dict(R=YAW, lights=[L0]),
+    "yawlat_area16": dict(R=YAW, lights=[L0], area=dict(side=0.1, n=4)),
+    "pix_pitch_1": dict(R=PITCH, lights=[L0]),
+    "pix_pitch_area16": dict(R=PITCH, lights=[L0], area=dict(side=0.1, n=4)),
     "pix_area81": dict(R=None, lights=[L0], area=dict(side=0.1, n=9)),
 }
 
