@@ -4,7 +4,7 @@
 set -eu
 cd "$(dirname "$0")/.."
 R=${1:-r02}
-for w in rt rast c4 c5 yaw f256; do
+for w in rt rast c4 c5 c5yaw yaw f256; do
   [ -f gpurun_out/prof_$w/${w}_kernel_stats.csv ] && cp gpurun_out/prof_$w/${w}_kernel_stats.csv profiles/${R}_${w}_kernel_stats.csv
   [ -f gpurun_out/bench_$w.log ] && tail -n 1 gpurun_out/bench_$w.log > profiles/${R}_bench_$w.json
 done

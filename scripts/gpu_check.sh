@@ -32,6 +32,7 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench_c5 300 python bench.py --workload c5 --steps 20 --warmup 2
   step bench_yaw 300 python bench.py --workload yaw
   step bench_f256 300 python bench.py --workload f256
+  step bench_c5yaw 300 python bench.py --workload c5yaw --steps 20 --warmup 2
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
