@@ -104,6 +104,7 @@ _SIGS = {
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
     "cg_rt_set_pending_cap": (C.c_int, [P, C.c_int]),
     "cg_rt_scratch_info": (C.c_int, [P, C.POINTER(C.c_uint64)]),
+    "cg_rt_route": (C.c_int, [C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "cg_rt_set_pool_caps": (C.c_int, [P, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
@@ -197,6 +198,19 @@ def yaw_matrix(yaw: float):
     m[0 * 4 + 0], m[0 * 4 + 2] = float(c), float(-s)
     m[2 * 4 + 0], m[2 * 4 + 2] = float(s), float(c)
     return (C.c_float * 16)(*m)
+
+
+ROUTES = ("pixel", "lattice", "lattice_yaw", "lights", "lights_yaw", "big_pixel", "big_lattice", "big_lattice_yaw")
+
+
+def rt_route(cam, n_tris, n_spheres, n_lights, shard=None):
+    """cg_rt_route: the kernels a frame of this shape takes (host-only; no GPU
+    needed), as a name from ROUTES."""
+    lib = load()
+    rc = lib.cg_rt_route(C.byref(cam), n_tris, n_spheres, n_lights, C.cast(C.byref(shard), C.c_void_p) if shard else None)
+    if rc < 0:
+        raise ValueError(f"cg_rt_route: {rc}")
+    return ROUTES[rc]
 
 
 def rt_camera(width, height, focal=256.0, cam=(0.0, 0.0, -3.0, 1.0), R=None, indirect=0.5):

@@ -1354,6 +1354,9 @@ bool rt_use_lattice(const RtFrame &F)
            F.n_lights <= kLatMaxLights && rt_lattice_ok(F);
 }
 
+// 0: no lattice kernel, 1: shared columns, 2: per-pixel columns (cg_rt_route)
+int rt_lattice_kind(const RtFrame &F) { return rt_use_lattice(F) ? (lat_yaw(F) ? 2 : 1) : 0; }
+
 size_t rt_lattice_tiles(const RtFrame &F)
 {
     return (size_t)((F.W + kLatTileW - 1) / kLatTileW) * ((F.rows_out + kLatTileH - 1) / kLatTileH);

@@ -24,6 +24,7 @@ hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShad
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                             const unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
+int rt_lattice_kind(const RtFrame &);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, int);
@@ -407,16 +408,9 @@ static int set_lights(cg_ctx *c, const cg_light *lights, int n, hipStream_t st, 
     return CG_OK;
 }
 
-static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
-                      const cg_rt_shard *shard, hipStream_t st, RtFrame &F)
+// The frame's shape and sharding (no scene, lights or device state).
+static int frame_shape(const cg_rt_camera *cam, const cg_rt_shard *shard, RtFrame &F)
 {
-    if (!cam || cam->width <= 0 || cam->height <= 0 || n_lights < 0 || n_lights > kMaxLights ||
-        (n_lights && !lights))
-        return CG_E_INVALID;
-    if (c->n_tris < 0) {
-        c->err = "render before cg_rt_set_scene";
-        return CG_E_NOSCENE;
-    }
     std::memset(&F, 0, sizeof(F));
     F.W = cam->width;
     F.H = cam->height;
@@ -424,9 +418,6 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     F.indirect = cam->indirect;
     F.cam[0] = cam->camera.x; F.cam[1] = cam->camera.y; F.cam[2] = cam->camera.z; F.cam[3] = cam->camera.w;
     std::memcpy(F.R, cam->R, sizeof(F.R));
-    F.n_tris = c->n_tris;
-    F.n_sph = c->n_sph;
-    F.nbound = c->nbound;
     cg_rt_shard one{0, 1, kRtTileH, 0, 0, 0, 0};
     const cg_rt_shard *s = shard ? shard : &one;
     if (s->rows > 0) {   // band: rows row0 .. row0 + rows - 1
@@ -454,8 +445,47 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     }
     F.cull_primary = 1;   // exact certificates (cg_rt_dev.h); the probes run without them
     F.cull_shadow = 1;
+    return CG_OK;
+}
+
+static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                      const cg_rt_shard *shard, hipStream_t st, RtFrame &F)
+{
+    if (!cam || cam->width <= 0 || cam->height <= 0 || n_lights < 0 || n_lights > kMaxLights ||
+        (n_lights && !lights))
+        return CG_E_INVALID;
+    if (c->n_tris < 0) {
+        c->err = "render before cg_rt_set_scene";
+        return CG_E_NOSCENE;
+    }
+    const int rc = frame_shape(cam, shard, F);
+    if (rc) return rc;
+    F.n_tris = c->n_tris;
+    F.n_sph = c->n_sph;
+    F.nbound = c->nbound;
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     return set_lights(c, lights, n_lights, st, F);
+}
+
+extern "C" int cg_rt_route(const cg_rt_camera *cam, int n_tris, int n_spheres, int n_lights, const cg_rt_shard *shard)
+{
+    if (!cam || cam->width <= 0 || cam->height <= 0 || n_tris < 0 || n_spheres < 0 || n_lights < 0 ||
+        n_lights > kMaxLights)
+        return CG_E_INVALID;
+    RtFrame F;
+    const int rc = frame_shape(cam, shard, F);
+    if (rc) return rc;
+    F.n_tris = n_tris;
+    F.n_sph = n_spheres;
+    F.n_lights = n_lights;
+    if (F.n_tris > 64) {   // rt_enqueue_kernels: the large-scene path
+        const int m = rt_big_mode(F);
+        return m == 0 ? CG_RT_ROUTE_BIG_PIXEL : m == 1 ? CG_RT_ROUTE_BIG_LATTICE : CG_RT_ROUTE_BIG_LATTICE_YAW;
+    }
+    const int k = rt_lattice_kind(F);
+    if (k == 0) return CG_RT_ROUTE_PIXEL;
+    if (n_lights == 1) return k == 1 ? CG_RT_ROUTE_LATTICE : CG_RT_ROUTE_LATTICE_YAW;
+    return k == 1 ? CG_RT_ROUTE_LIGHTS : CG_RT_ROUTE_LIGHTS_YAW;
 }
 
 static bool big_observe(cg_ctx *c, bool sizing);

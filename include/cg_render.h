@@ -186,6 +186,23 @@ int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphere *spheres
                         const cg_rt_camera *cam, int *col0, int *col1);
 /* Rows a shard renders (including padding rows of its last stripe). */
 int cg_rt_shard_rows(int height, const cg_rt_shard *shard);
+/* Which kernels a frame of this shape takes (host-only, no device work):
+ * CG_RT_ROUTE_* below, or CG_E_INVALID.  The lattice kernels share sub-rays
+ * between pixels (half-pixel columns for an unrotated camera, per-pixel
+ * columns with shared rows under a yaw); the large-scene path (n_tris > 64)
+ * has the same two lattice modes and a per-pixel mode.  Every route gives
+ * the reference's image; this only says how. */
+enum {
+    CG_RT_ROUTE_PIXEL = 0,            /* rt_pixel_kernel: 9 sub-rays per pixel */
+    CG_RT_ROUTE_LATTICE = 1,          /* rt_lattice_kernel, one light */
+    CG_RT_ROUTE_LATTICE_YAW = 2,      /* the same, per-pixel columns */
+    CG_RT_ROUTE_LIGHTS = 3,           /* rt_lattice_lights_kernel, 2..64 lights */
+    CG_RT_ROUTE_LIGHTS_YAW = 4,
+    CG_RT_ROUTE_BIG_PIXEL = 5,        /* large scene, per-pixel mode */
+    CG_RT_ROUTE_BIG_LATTICE = 6,      /* large scene, lattice mode */
+    CG_RT_ROUTE_BIG_LATTICE_YAW = 7
+};
+int cg_rt_route(const cg_rt_camera *cam, int n_tris, int n_spheres, int n_lights, const cg_rt_shard *shard);
 /* Reassemble a frame from gathered shards: d_gathered holds nranks blocks of
  * cg_rt_shard_rows() rows each, in rank order. */
 int cg_rt_unstripe_device(cg_ctx *ctx, const uint32_t *d_gathered, int width, int height,
