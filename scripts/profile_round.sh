@@ -18,7 +18,7 @@ run() {  # name timeout cmd...
   [ $rc -eq 0 ] || { tail -5 "$OUT/$name.log"; exit $rc; }
 }
 B="python3 $ROOT/bench.py --no-cpu-baseline"
-WLS=${WLS:-rt rast c4 c5 yaw f256}
+WLS=${WLS:-rt rast c4 c5 c5yaw yaw f256}
 has() { case " $WLS " in *" $1 "*) return 0;; esac; return 1; }
 for w in $WLS; do
   run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-rast
@@ -32,7 +32,7 @@ done
 G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 G2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"
 G3="SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_TRANS_F SQ_INSTS_VALU_CVT SQ_INST_LEVEL_SMEM"
-for w in rt c4 c5 yaw f256 rast; do
+for w in rt c4 c5 c5yaw yaw f256 rast; do
   has $w || continue
   case $w in rt|c4|yaw|f256) S="--steps 32 --warmup 32";; rast) S="--steps 64 --warmup 64";; *) S="--steps 4 --warmup 2";; esac
   i=0
