@@ -769,7 +769,7 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs 
 // Ray slots of one wave tile (K1, K4 and the shading kernel read them):
 //  * per-pixel mode: the tile's 8x8 pixels, lane = pixel, slot s = its
 //    sub-ray s (skeleton.cpp:134-140), stored at s * npix + pixel;
-//  * lattice mode (unrotated camera, rows contiguous, <= 64 lights): with R =
+//  * lattice mode (rt_big_mode; rows contiguous, <= 64 lights): with R =
 //    identity pixel (u, v)'s sub-ray (i, j) has the exact direction ((u - W/2)
 //    + i/2, (v - H/2) + j/2, f) (cg_rt.hip), the half-pixel lattice point
 //    (2u + i, 2v + j) its neighbours share.  Its closest hit and its shadow
@@ -778,6 +778,9 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs 
 //    = 2 (v - row0) + j + 1 in [16 ty, 16 ty + 16) (the last tile of a row or
 //    column also the one beyond), slot s of a lane is owned point s * 64 +
 //    lane, stored at Yi * lat_w + Xi: 4 rays per lane instead of 9.
+//    Under a yaw (rt_big_mode 2) the rows are still that lattice but each
+//    pixel keeps its own three columns Xi = 3u + i + 1 (lat_x): the tile owns
+//    [24 tx, 24 tx + 24), up to 7 slots per lane.
 struct LatOwn {
     int xi0, nx, yi0, ny;
 };
