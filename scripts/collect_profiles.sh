@@ -10,11 +10,14 @@ for w in rt rast c4 c5 c5yaw yaw f256; do
 done
 [ -f gpurun_out/pytest_gpu.log ] && tail -n 3 gpurun_out/pytest_gpu.log > profiles/${R}_pytest_gpu_tail.log
 [ -f gpurun_out/bal_rt16.log ] && cp gpurun_out/bal_rt16.log profiles/${R}_shard_balance_rt_k16.json
-if [ -d gpurun_out/pmc_rt_FETCH_SIZE ]; then
+pmc=0
+for w in rt rast c4 c5 c5yaw yaw f256; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    cp gpurun_out/pmc_rt_$c/pmc_counter_collection.csv profiles/${R}_pmc_rt_$c.csv
-    cp gpurun_out/pmc_rast_$c/pmc_counter_collection.csv profiles/${R}_pmc_rast_$c.csv
+    if [ -f gpurun_out/pmc_${w}_$c/pmc_counter_collection.csv ]; then
+      cp gpurun_out/pmc_${w}_$c/pmc_counter_collection.csv profiles/${R}_pmc_${w}_$c.csv
+      pmc=1
+    fi
   done
-  CG_PMC_RT_FRAMES=32 python3 scripts/pmc_summary.py $R > /dev/null
-fi
+done
+[ $pmc = 1 ] && CG_PMC_RT_FRAMES=32 python3 scripts/pmc_summary.py $R > /dev/null
 echo collected

@@ -8,16 +8,21 @@ import collections, csv, json, os, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"rt": ["rt_lattice_kernel"], "rast": ["rast_clip_kernel", "rast_setup_kernel", "rast_rows_kernel", "rast_fill_kernel",
-                                                 "rast_post_kernel"]}
+                                                 "rast_post_kernel"],
+            "c4": ["rt_lattice_lights_kernel"], "yaw": ["rt_lattice_kernel"], "f256": ["rt_lattice_kernel"],
+            "c5": None, "c5yaw": None}   # None: every rt_* kernel of the frame (per frame, see below)
+FRAMES_PER_LAUNCH = {"rt": int(os.environ.get("CG_PMC_RT_FRAMES", "32")), "c4": 32, "yaw": 32, "f256": 32}
 
 
 def per_kernel(wl, ctr):
+    """Median counter value per dispatch (robust to a first frame's sizing passes) and dispatch
+    count, per kernel (base name)."""
     path = os.path.join(ROOT, "gpurun_out", f"pmc_{wl}_{ctr}", "pmc_counter_collection.csv")
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]
         agg[name.split("::")[-1]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    return {k: sorted(v)[len(v) // 2] for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
 
 
 path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -28,11 +33,20 @@ except (OSError, ValueError):
 out.update({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 20",
             "units": "bytes per launch", "round": sys.argv[1] if len(sys.argv) > 1 else "r01"})
 for wl, kernels in DOMINANT.items():
-    f, w = per_kernel(wl, "FETCH_SIZE"), per_kernel(wl, "WRITE_SIZE")
-    det = {k: {"fetch_kib_raw": f.get(k), "write_kib": w.get(k),
-               "hbm_bytes_corrected": (2 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024} for k in kernels}
-    out.setdefault(wl, {}).update({"kernels": det,
-                                   "frames_per_launch": int(os.environ.get("CG_PMC_RT_FRAMES", "32")) if wl == "rt" else 1,
+    if not os.path.isdir(os.path.join(ROOT, "gpurun_out", f"pmc_{wl}_FETCH_SIZE")):
+        continue
+    (f, nf), (w, _) = per_kernel(wl, "FETCH_SIZE"), per_kernel(wl, "WRITE_SIZE")
+    mult = {}
+    if kernels is None:   # large scenes: per frame = every rt_* kernel, weighted by its dispatches per
+        # frame: rt_big_primary_kernel runs once per rendered frame, the list kernels also in the first
+        # frame's sizing passes (once per pass, like rt_sup_primary_kernel)
+        frames = max(1, nf.get("rt_big_primary_kernel", 1))
+        passes = max(1, nf.get("rt_sup_primary_kernel", frames))
+        kernels = sorted(k for k in f if k.startswith("rt_"))
+        mult = {k: max(1, round(nf[k] / (passes if nf[k] > frames else frames))) for k in kernels}
+    det = {k: {"fetch_kib_raw": f.get(k), "write_kib": w.get(k), "dispatches_per_frame": mult.get(k, 1),
+               "hbm_bytes_corrected": (2 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024 * mult.get(k, 1)} for k in kernels}
+    out.setdefault(wl, {}).update({"kernels": det, "frames_per_launch": FRAMES_PER_LAUNCH.get(wl, 1),
                                    "hbm_bytes_per_launch": sum(d["hbm_bytes_corrected"] for d in det.values())})
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 with open(path, "w") as fh:

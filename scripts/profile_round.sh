@@ -23,10 +23,11 @@ has() { case " $WLS " in *" $1 "*) return 0;; esac; return 1; }
 for w in $WLS; do
   run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-rast
 done
-for wl in rt rast; do
+for wl in rt rast c4 c5 c5yaw yaw f256; do
   has $wl || continue
+  case $wl in rt|rast) S="--steps 64 --warmup 32";; c4|yaw|f256) S="--steps 32 --warmup 32";; *) S="--steps 4 --warmup 2";; esac
   for ctr in FETCH_SIZE WRITE_SIZE; do
-    run pmc_${wl}_$ctr 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${wl}_$ctr" -o pmc -- $B --workload $wl --steps 64 --warmup 32 --no-rast
+    run pmc_${wl}_$ctr 180 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${wl}_$ctr" -o pmc -- $B --workload $wl $S --no-rast
   done
 done
 G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
