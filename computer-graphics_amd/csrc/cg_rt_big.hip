@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const Rt
 // key: every float distance fl(t |nd|) a ray of the bin computes for the
 // triangle is >= key (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23)
 // since nd.z = f, :137).  One chunk of the bin list per super-list chunk.
-__global__ __launch_bounds__(256) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                              const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int bin = blockIdx.y;
@@ -592,7 +592,7 @@ __device__ __forceinline__ int depth_bucket(unsigned kbits, const BigBufs &B, in
 
 // Per bin: bucket sizes and each bucket's smallest key (workgroups stride
 // over the bin's chunks).
-__global__ __launch_bounds__(256) void rt_bin_count_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(256, 4) void rt_bin_count_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                            const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int bin = blockIdx.y, nc = B.bin_nch[bin];
@@ -813,7 +813,7 @@ __device__ __forceinline__ float lat_y(const RtFrame &F, int Yi)
 
 // K1: closest hits of every ray slot of the tile.
 template <int LM>   // 0: per-pixel mode, 1: lattice, 2: lattice with per-pixel columns
-__global__ __launch_bounds__(kRtThreads) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                     const RtShade *__restrict__ shade,
                                                                     const RtSphere *__restrict__ sph, BigBufs B)
 {
