@@ -1184,7 +1184,7 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
 template <int LM>
-__global__ __launch_bounds__(kRtThreads) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, 5) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
 {
