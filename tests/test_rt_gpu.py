@@ -261,7 +261,7 @@ def test_rt_render_frames_batched(rt, golden):
 
 
 @pytest.mark.parametrize("window", [False, True])
-@pytest.mark.parametrize("kind", ["lattice", "yaw", "c4"])
+@pytest.mark.parametrize("kind", ["lattice", "yaw", "yaw_batch", "c4", "c4yaw"])
 def test_rt_bands_rgb24_assemble(rt, kind, window):
     """bench.py's N > 1 layout on one GPU: uneven bands, rank 0's band rendered
     ARGB straight into the frames, the others in the RGB24 wire format into
@@ -271,11 +271,17 @@ def test_rt_bands_rgb24_assemble(rt, kind, window):
     if kind == "lattice":   # batched lattice launches, RGB24 stored by the kernel
         cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, z, 1.0)) for z in (-3.0, -2.95, -2.8)]
         lights = cgamd.default_lights()
-    elif kind == "yaw":     # general kernel, one frame at a time + pack pass
+    elif kind == "yaw":     # yawed lattice, one frame at a time (R differs between the frames)
         cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, -3.0, 1.0), cgamd.yaw_matrix(y)) for y in (0.05, -0.1)]
         lights = cgamd.default_lights()
-    else:                   # light set (general kernel)
+    elif kind == "yaw_batch":   # yawed lattice, one batched launch (same R, cameraPos moving)
+        cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, z, 1.0), cgamd.yaw_matrix(0.12)) for z in (-3.0, -2.9, -2.75)]
+        lights = cgamd.default_lights()
+    elif kind == "c4":      # light set (light-set lattice kernel)
         cams = [cgamd.rt_camera(W, H, 256.0)]
+        lights = cgamd.area_lights(None, 0.1, 3)
+    else:                   # light set under a yaw (light-set lattice, per-pixel columns)
+        cams = [cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, z, 1.0), cgamd.yaw_matrix(-0.2)) for z in (-3.0, -2.85)]
         lights = cgamd.area_lights(None, 0.1, 3)
     singles = [rt.rt_render(c, lights)[0] for c in cams]
     K = len(cams)
@@ -290,7 +296,7 @@ def test_rt_bands_rgb24_assemble(rt, kind, window):
         t_, n_, s_ = cgamd.rt_scene()
         c0, c1 = cgamd.frame_columns(t_, n_, s_, 1, cams[0])
         cols = c1 - c0 if c1 - c0 < W else 0
-        if kind != "yaw":
+        if "yaw" not in kind:
             assert 0 < cols < W
     pitch = cols or W
     frames.fill_(-1)                                  # the assembly must write every pixel
