@@ -99,6 +99,18 @@ int main(int argc, char **argv)
         int c0 = 0, c1 = 0;
         (void)cg_rt_frame_columns(t, n, &sph, 1, &cam, &c0, &c1);
         (void)cg_rt_frame_columns(rnd.data(), 5000, nullptr, 0, &cam, &c0, &c1);
+        // kernel routes (host-only): identity, a yaw, NaN and huge entries, shards, large scenes
+        const cg_rt_shard shards[3] = {{0, 1, 15, 0, 0, 0, 0}, {1, 3, 8, 0, 0, 0, 0}, {0, 1, 15, 135, 270, 0, 0}};
+        for (int variant = 0; variant < 4; ++variant) {
+            cg_rt_camera rc = cam;
+            if (variant == 1) { rc.R[0] = 0.98f; rc.R[2] = -0.17f; rc.R[8] = 0.17f; rc.R[10] = 0.98f; }
+            if (variant == 2) rc.R[0] = __builtin_nanf("");
+            if (variant == 3) rc.R[8] = 1e30f;
+            for (const cg_rt_shard &sh : shards)
+                for (int nt : {28, 1000000})
+                    for (int nl : {1, 64, 81})
+                        if (cg_rt_route(&rc, nt, 1, nl, &sh) < 0) fail("cg_rt_route", -1);
+        }
     }
     cg_light centre{{0, -0.5f, -0.7f, 1}, {14, 14, 14}}, area[64];
     if (int rc = cg_rt_area_lights(&centre, 0.1f, 8, area, 64); rc < 0) fail("cg_rt_area_lights", rc);
