@@ -105,6 +105,8 @@ struct cg_dist {
     size_t done_cap[2] = {0, 0};
     std::vector<uint32_t> target[2];
     hipEvent_t ev_call[2] = {};       // ranks > 0: slot free again (its sends / copies done)
+    hipEvent_t ev_zero[2] = {};       // ranks > 0: the slot's counts zeroed for this call (on st)
+    hipEvent_t ev_start = nullptr;    // rank 0: the caller's stream at the start of the call
     int cur = 0;                      // slot of the last call
 };
 
@@ -197,7 +199,10 @@ int ensure_events(cg_dist *d)
     for (int k = 0; k < 2; ++k) {
         DT(d, hipEventCreateWithFlags(&d->ev_call[k], hipEventDisableTiming), "event");
         DT(d, hipEventRecord(d->ev_call[k], d->xs), "event");
+        DT(d, hipEventCreateWithFlags(&d->ev_zero[k], hipEventDisableTiming), "event");
+        DT(d, hipEventRecord(d->ev_zero[k], d->xs), "event");
     }
+    DT(d, hipEventCreateWithFlags(&d->ev_start, hipEventDisableTiming), "event");
     int wait_value = 0;
     d->signals = hipDeviceGetAttribute(&wait_value, hipDeviceAttributeCanUseStreamWaitValue, ctx_device(d->ctx)) ==
                      hipSuccess && wait_value != 0;
@@ -334,8 +339,10 @@ extern "C" void cg_dist_destroy(cg_dist *d)
         for (hipEvent_t e : {d->ev_rend[k], d->ev_sent[k], d->ev_recv[k], d->ev_asm[k]})
             if (e) (void)hipEventDestroy(e);
     if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+    if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     for (int k = 0; k < 2; ++k) {
         if (d->ev_call[k]) (void)hipEventDestroy(d->ev_call[k]);
+        if (d->ev_zero[k]) (void)hipEventDestroy(d->ev_zero[k]);
         if (d->done[k]) (void)hipFree(d->done[k]);
     }
     for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
@@ -411,13 +418,16 @@ extern "C" int cg_dist_band_partition(const double *row_cost, int height, int nr
 }
 
 // New bands from per-rank (render ms/frame, fixed ms/frame) pairs t[2 r], t[2 r + 1].
+// The fixed term (rank 0's assembly) adds to rank 0's time only in the chunked
+// pipeline, where the assembly runs on the render stream; the signalled
+// pipeline assembles on the transfer stream beside rank 0's own render.
 static void rebalance_bands(cg_dist *d, const double *t)
 {
     const int n = d->nranks, H = d->height;
     std::vector<double> cost(H, 0.0), ovh(n);
     for (int r = 0; r < n; ++r) {
         for (int y = d->row0[r]; y < d->row0[r] + d->rows[r]; ++y) cost[y] = std::max(t[2 * r], 1e-12) / d->rows[r];
-        ovh[r] = t[2 * r + 1];
+        ovh[r] = d->signals ? 0.0 : t[2 * r + 1];
     }
     std::vector<int> a(n), b(n);
     band_partition(cost.data(), H, n, ovh.data(), a.data(), b.data());
@@ -514,6 +524,13 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
         }
         d->target[s].assign(n_frames, 0u);
         DT(d, hipMemsetAsync(d->done[s], 0, (size_t)n_frames * sizeof(uint32_t), st), "zero signals");
+        // The slot's counts still hold the totals of the call two calls ago,
+        // and the targets repeat for the same frame size: every wait on them
+        // (this rank's transfer stream, or rank 0's in the local transport)
+        // is ordered after this memset, else it could pass on stale counts
+        // and send a half-written band.
+        DT(d, hipEventRecord(d->ev_zero[s], st), "event");
+        if (!d->group) DT(d, hipStreamWaitEvent(d->xs, d->ev_zero[s], 0), "wait");
         if (nr > 0) {
             rc = render_band(d, lights, n_lights, cams, n_frames, r0, nr, c0, cols, out.p, (size_t)nr * pitch,
                              CG_PIX_RGB24, st, d->done[s], d->target[s].data());
@@ -537,13 +554,18 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
         DT(d, hipEventRecord(d->ev_call[s], d->xs), "event");
         return CG_OK;
     }
-    // rank 0: own band straight into the frames (ARGB), on the caller's stream
+    // rank 0: the assembly below writes the caller's frames on the transfer
+    // stream, so it is ordered after whatever the caller queued on `st`
+    // before this call (e.g. a copy-out of the previous call's frames).
+    DT(d, hipEventRecord(d->ev_start, st), "event");
+    // own band straight into the frames (ARGB), on the caller's stream
     if (nr > 0) {
         rc = render_band(d, lights, n_lights, cams, n_frames, r0, nr, 0, 0, d_frames + (size_t)r0 * W, frame_stride,
                          CG_PIX_ARGB8888, st);
         if (rc) return rc;
     }
     if (n > 1) {
+        bool ordered = false;   // xs waited on ev_start
         size_t per_frame = 0;
         for (int p = 1; p < n; ++p) per_frame += (size_t)d->rows[p] * row_bytes;
         DT(d, d->rbuf[0].ensure(std::max<size_t>((size_t)n_frames * per_frame, 1)), "alloc receive buffer");
@@ -564,6 +586,8 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
                     if (m->last_frames != (size_t)n_frames || m->last_pitch != pitch || m->cur != s ||
                         m->calls != d->calls)
                         return fail(d, CG_E_INVALID, "local transport: ranks > 0 must render this call first");
+                    // the peer's counts for this call are zeroed before we poll them
+                    if (f0 == 0) DT(d, hipStreamWaitEvent(d->xs, m->ev_zero[s], 0), "wait");
                     for (int f = f0; f < f0 + nf; ++f)
                         if (m->target[s][f])
                             DT(d, hipStreamWaitValue32(d->xs, m->done[s] + f, m->target[s][f],
@@ -588,6 +612,10 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
             rc = timed(d, d->t_asm, d->n_asm, t);
             if (rc) return rc;
             t->frames = nf;
+            if (!ordered) {   // the receives may start earlier; the writes into d_frames may not
+                DT(d, hipStreamWaitEvent(d->xs, d->ev_start, 0), "wait");
+                ordered = true;
+            }
             DT(d, hipEventRecord(t->a, d->xs), "event");
             rc = cg_rt_assemble_device(d->ctx, cb, CG_PIX_RGB24, br0.data(), brows.data(), n - 1, W, H, nf,
                                        d_frames + (size_t)f0 * frame_stride, frame_stride, cols ? c0 : 0, cols, d->xs);

@@ -50,17 +50,24 @@ constexpr int kZigzag[80] = {
 
 struct HuffTable {
     bool present = false;
+    bool dc_ok = false;   // every symbol <= 15: usable as a DC table (libjpeg jdhuff.c)
     // lookahead: the next 9 bits -> (length << 8 | symbol), 0 = longer code
     uint16_t fast[512];
     int32_t maxcode[18], valoff[17];
     uint8_t vals[256];
-    void build(const uint8_t *counts, const uint8_t *symbols, int total)
+    // false for an over-subscribed code (libjpeg jdhuff.c: JERR_BAD_HUFF_TABLE)
+    bool build(const uint8_t *counts, const uint8_t *symbols, int total)
     {
+        present = false;
+        memset(vals, 0, sizeof(vals));
         memcpy(vals, symbols, (size_t)total);
         memset(fast, 0, sizeof(fast));
+        dc_ok = true;
+        for (int i = 0; i < total; ++i) dc_ok &= symbols[i] <= 15;
         int code = 0, k = 0;
         for (int len = 1; len <= 16; ++len) {
             valoff[len] = k - code;
+            if (code + counts[len - 1] > (1 << len)) return false;
             for (int i = 0; i < counts[len - 1]; ++i, ++code, ++k)
                 if (len <= 9) {
                     int lo = code << (9 - len), hi = (code + 1) << (9 - len);
@@ -71,6 +78,7 @@ struct HuffTable {
         }
         maxcode[17] = 0x7fffffff;
         present = true;
+        return true;
     }
 };
 
@@ -155,6 +163,8 @@ struct Component {
     int blocks_x, blocks_y;   // coefficient plane, padded to whole MCUs
     int samp_w, samp_h;       // component size in samples
     int scale;                // IDCT output = 8 * scale per block side (1 or 2)
+    bool latched = false;     // quantisation table copied at its first scan (libjpeg jdinput.c)
+    uint16_t q[64] = {};
     std::vector<int16_t> coef;
     int pred = 0;
     int16_t *block(int bx, int by) { return coef.data() + ((size_t)by * blocks_x + bx) * 64; }
@@ -164,7 +174,8 @@ struct JpegFrame {
     int width = 0, height = 0, ncomp = 0;
     bool progressive = false, adobe_rgb = false;
     int hmax = 1, vmax = 1, mcus_x = 0, mcus_y = 0, restart = 0;
-    uint16_t quant[4][64];   // natural order
+    uint16_t quant[4][64] = {};   // natural order
+    bool quant_present[4] = {};
     HuffTable dc[4], ac[4];
     Component comp[3];
     int eobrun = 0;
@@ -179,7 +190,7 @@ class JpegDecoder {
     const char *parse(const uint8_t *data, size_t n, bool header_only);
 
   private:
-    const char *frame(const uint8_t *p, int marker);
+    const char *frame(const uint8_t *p, int len, int marker);
     const char *scan(const uint8_t *&p, const uint8_t *end);
     void block_seq(BitReader &br, Component &c, int16_t *b, const HuffTable &dct, const HuffTable &act);
     void block_dc(BitReader &br, Component &c, int16_t *b, const HuffTable &dct, int ah, int al);
@@ -189,14 +200,17 @@ class JpegDecoder {
     bool have_frame_ = false;
 };
 
-const char *JpegDecoder::frame(const uint8_t *p, int marker)
+const char *JpegDecoder::frame(const uint8_t *p, int len, int marker)
 {
+    if (have_frame_) return "duplicate JPEG frame header";
+    if (len < 8) return "truncated JPEG frame header";
     if (p[2] != 8) return "only 8-bit JPEG is supported";
     f_.progressive = marker == 0xC2;
     f_.height = be16(p + 3);
     f_.width = be16(p + 5);
     f_.ncomp = p[7];
     if (f_.ncomp != 1 && f_.ncomp != 3) return "only 1- or 3-component JPEG is supported";
+    if (len < 8 + 3 * f_.ncomp) return "truncated JPEG frame header";
     if (f_.width <= 0 || f_.height <= 0) return "bad JPEG dimensions";
     for (int i = 0; i < f_.ncomp; ++i) {
         Component &c = f_.comp[i];
@@ -319,7 +333,9 @@ void JpegDecoder::block_ac_refine(BitReader &br, int16_t *b, const HuffTable &ac
 
 const char *JpegDecoder::scan(const uint8_t *&p, const uint8_t *end)
 {
-    int len = be16(p), ns = p[2];
+    int len = be16(p);
+    if (len < 3) return "bad JPEG scan header";
+    int ns = p[2];
     if (ns < 1 || ns > f_.ncomp || len != 6 + 2 * ns) return "bad JPEG scan header";
     Component *sc[4];
     const HuffTable *dct[4], *act[4];
@@ -336,6 +352,19 @@ const char *JpegDecoder::scan(const uint8_t *&p, const uint8_t *end)
     if (!f_.progressive) ss = 0, se = 63, ah = al = 0;
     else if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || al > 13)
         return "bad progressive scan parameters";
+    // the tables the scan decodes with must exist (libjpeg: JERR_NO_HUFF_TABLE,
+    // JERR_NO_QUANT_TABLE); a DC table's symbols are magnitude categories <= 15
+    for (int i = 0; i < ns; ++i) {
+        const bool need_dc = ss == 0 && ah == 0, need_ac = se > 0;
+        if (need_dc && (!dct[i]->present || !dct[i]->dc_ok)) return "JPEG scan uses an undefined DC table";
+        if (need_ac && !act[i]->present) return "JPEG scan uses an undefined AC table";
+        Component &c = *sc[i];
+        if (!c.latched) {
+            if (!f_.quant_present[c.tq]) return "JPEG component uses an undefined quantisation table";
+            memcpy(c.q, f_.quant[c.tq], sizeof(c.q));
+            c.latched = true;
+        }
+    }
     p += len;
     BitReader br(p, end);
     for (int i = 0; i < ns; ++i) sc[i]->pred = 0;
@@ -402,25 +431,30 @@ const char *JpegDecoder::parse(const uint8_t *data, size_t n, bool header_only)
         if (m == 0xDB) {
             for (const uint8_t *q = p + 2; q < p + len;) {
                 int prec = q[0] >> 4, id = q[0] & 15;
-                if (id > 3) return "bad JPEG quantisation table";
+                if (id > 3 || prec > 1) return "bad JPEG quantisation table";
+                if (q + 1 + (prec ? 128 : 64) > p + len) return "truncated JPEG quantisation table";
                 for (int k = 0; k < 64; ++k) f_.quant[id][kZigzag[k]] = (uint16_t)(prec ? be16(q + 1 + 2 * k) : q[1 + k]);
+                f_.quant_present[id] = true;
                 q += 1 + (prec ? 128 : 64);
             }
         } else if (m == 0xC4) {
             for (const uint8_t *q = p + 2; q < p + len;) {
                 int cls = q[0] >> 4, id = q[0] & 15, total = 0;
                 if (cls > 1 || id > 3) return "bad JPEG Huffman table";
+                if (q + 17 > p + len) return "truncated JPEG Huffman table";
                 for (int l = 0; l < 16; ++l) total += q[1 + l];
                 if (total > 256) return "bad JPEG Huffman table";
-                (cls ? f_.ac[id] : f_.dc[id]).build(q + 1, q + 17, total);
+                if (q + 17 + total > p + len) return "truncated JPEG Huffman table";
+                if (!(cls ? f_.ac[id] : f_.dc[id]).build(q + 1, q + 17, total)) return "bad JPEG Huffman table";
                 q += 17 + total;
             }
         } else if (m == 0xDD) {
+            if (len < 4) return "truncated JPEG restart interval";
             f_.restart = be16(p + 2);
-        } else if (m == 0xEE && len >= 12 && !memcmp(p + 2, "Adobe", 5)) {
+        } else if (m == 0xEE && len >= 14 && !memcmp(p + 2, "Adobe", 5)) {
             f_.adobe_rgb = p[13] == 0;
         } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
-            if (const char *e = frame(p, m)) return e;
+            if (const char *e = frame(p, len, m)) return e;
             if (header_only) return nullptr;
         } else if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
             return "lossless / arithmetic / hierarchical JPEG is not supported";
@@ -655,7 +689,9 @@ int decode_into(cg_ctx *c, const uint8_t *data, size_t n, uint8_t *d_out, size_t
                                 hipMemcpyHostToDevice, st)) != hipSuccess)
             return ctx_fail(c, e, "jpeg coefficient upload");
     QuantTables qt;
-    for (int i = 0; i < f.ncomp; ++i) memcpy(qt.q[i], f.quant[f.comp[i].tq], sizeof(qt.q[i]));
+    // a component no scan reached keeps a zero table (libjpeg jddctmgr.c:
+    // its multipliers stay zero, the samples mid-grey)
+    for (int i = 0; i < f.ncomp; ++i) memcpy(qt.q[i], f.comp[i].q, sizeof(qt.q[i]));
     uint8_t *planes = scratch + coef_bytes;
     for (int i = 0; i < f.ncomp; ++i) {
         const Component &cp = f.comp[i];

@@ -33,6 +33,71 @@ static void fail(const char *what, int rc)
     exit(1);
 }
 
+// A crafted JPEG: SOI, the given segments (marker, payload), a few entropy bytes, EOI.
+static std::vector<uint8_t> crafted(std::initializer_list<std::pair<int, std::vector<uint8_t>>> segs)
+{
+    std::vector<uint8_t> j = {0xFF, 0xD8};
+    for (const auto &sg : segs) {
+        j.push_back(0xFF);
+        j.push_back((uint8_t)sg.first);
+        const size_t len = sg.second.size() + 2;
+        j.push_back((uint8_t)(len >> 8));
+        j.push_back((uint8_t)len);
+        j.insert(j.end(), sg.second.begin(), sg.second.end());
+        if (sg.first == 0xDA)
+            for (int k = 0; k < 64; ++k) j.push_back((uint8_t)(0x5A ^ k));
+    }
+    j.push_back(0xFF);
+    j.push_back(0xD9);
+    return j;
+}
+
+// Malformed headers the damaged-file loop cannot reach: each must
+// be rejected (CG_E_INVALID) without reading outside the buffer or using
+// undefined tables.
+static int malformed_jpegs()
+{
+    const std::vector<uint8_t> sof1 = {8, 0, 16, 0, 16, 1, 1, 0x11, 0};                // 16x16 gray, tq 0
+    std::vector<uint8_t> dqt(65, 1);
+    dqt[0] = 0;                                                                        // table 0, 8-bit
+    std::vector<uint8_t> dht_dc = {0x00, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // one 1-bit code
+    std::vector<uint8_t> dht_dc_bad = dht_dc;
+    dht_dc_bad[17] = 20;                                                               // DC category 20 > 15
+    std::vector<uint8_t> dht_ac = {0x10, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x00};
+    std::vector<uint8_t> dht_over = {0x10, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 2, 3};  // 3 1-bit codes
+    const std::vector<uint8_t> sos1 = {1, 1, 0x00, 0, 63, 0};
+    std::vector<uint8_t> dqt_short(dqt.begin(), dqt.begin() + 20);
+    std::vector<uint8_t> dht_short(dht_ac.begin(), dht_ac.begin() + 10);
+    std::vector<uint8_t> dht_short_syms = {0x10, 0, 0, 0, 0, 0, 0, 0, 40, 0, 0, 0, 0, 0, 0, 0, 0, 1, 2};
+    const std::vector<uint8_t> sof3_short = {8, 0, 16, 0, 16, 3, 1, 0x11, 0};         // 3 components, 1 described
+    const std::vector<uint8_t> adobe_short = {'A', 'd', 'o', 'b', 'e', 0, 100, 0, 0, 0};
+    const std::vector<std::vector<uint8_t>> cases = {
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc_bad}, {0xC4, dht_ac}, {0xDA, sos1}}),   // DC s > 15
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xDA, sos1}}),                                        // no Huffman tables
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xDA, sos1}}),                        // no AC table
+        crafted({{0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_ac}, {0xDA, sos1}}),                     // no quant table
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_over}, {0xDA, sos1}}),      // over-subscribed
+        crafted({{0xDB, dqt_short}, {0xC0, sof1}}),                                                // DQT past its segment
+        crafted({{0xC4, dht_short}, {0xC0, sof1}}),                                                // DHT counts cut off
+        crafted({{0xC4, dht_short_syms}, {0xC0, sof1}}),                                           // DHT symbols cut off
+        crafted({{0xDB, dqt}, {0xC0, sof3_short}}),                                                // SOF shorter than 3 comps
+        crafted({{0xDB, dqt}, {0xC0, {8, 0, 16}}}),                                                // SOF cut off
+        crafted({{0xDD, {}}, {0xDB, dqt}, {0xC0, sof1}}),                                          // DRI without its value
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC0, sof1}}),                                        // two frame headers
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_ac}, {0xDA, {}}}),          // empty SOS
+    };
+    int rejected = 0;
+    for (const auto &j : cases) {
+        if (cg_image_jpeg_check(j.data(), j.size()) != CG_E_INVALID) fail("malformed JPEG accepted", -1);
+        ++rejected;
+    }
+    // an Adobe segment too short for its transform byte is ignored, not read past
+    const auto ok = crafted({{0xEE, adobe_short}, {0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_ac},
+                             {0xDA, sos1}});
+    if (int rc = cg_image_jpeg_check(ok.data(), ok.size())) fail("well-formed crafted JPEG", rc);
+    return rejected;
+}
+
 int main(int argc, char **argv)
 {
     const std::string dir = argc > 1 ? argv[1] : "tests/golden/textures";
@@ -125,6 +190,8 @@ int main(int argc, char **argv)
     for (int k = 0; k < 100; ++k) cg_starfield_update(stars.data(), 1000, 16.0f);
     cg_rt_shard sh{1, 3, 15, 0, 0, 0, 0};
     (void)cg_rt_shard_rows(1080, &sh);
-    printf("sanitized host code: %d JPEGs, %ld clipped triangles, clean\n", checked, tris);
+    const int malformed = malformed_jpegs();
+    printf("sanitized host code: %d JPEGs, %d malformed JPEGs rejected, %ld clipped triangles, clean\n", checked,
+           malformed, tris);
     return 0;
 }

@@ -10,8 +10,11 @@
  * Float ops follow GLM 0.9.7.2 association; doubles where the reference
  * promotes.  Build with -O3 -ffp-contract=off, no -march.
  *
- * Pinned by the reference's ComputePolygonRows KAT (skeleton.cpp:183-199)
- * and by the frame fingerprints recorded in SURVEY.md section 8c.
+ * Pinned by the reference's own output, rasteriser/screenshot.bmp: the
+ * metal-grill room after the recovered Update() key sequence matches it bit
+ * for bit on all 602,987 pixels the missing marble map does not touch
+ * (tests/test_rast_screenshot.py, texels from cg_oracle_jpeg.c = IJG libjpeg 9),
+ * and by the reference's ComputePolygonRows KAT (skeleton.cpp:183-199).
  */
 #include "cg_oracle.h"
 

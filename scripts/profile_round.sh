@@ -18,16 +18,20 @@ run() {  # name timeout cmd...
   [ $rc -eq 0 ] || { tail -5 "$OUT/$name.log"; exit $rc; }
 }
 B="python3 $ROOT/bench.py --no-cpu-baseline"
+# the machine code these counters describe (bench.py nulls roofline.frac for other code)
+python3 -c "import json, sys; sys.path.insert(0, '$ROOT/computer-graphics_amd'); import codeobj; \
+json.dump({k: codeobj.kernel_sha256(k) for k in ('rt_lattice_kernel', 'rt_lattice_lights_kernel', \
+'rt_big_primary_kernel', 'rt_pixel_kernel', 'rast_fill_kernel', 'rast_post_kernel')}, open('$OUT/code_sha256.json', 'w'), indent=1)"
 WLS=${WLS:-rt rast c4 c5 c5yaw yaw f256}
 has() { case " $WLS " in *" $1 "*) return 0;; esac; return 1; }
 for w in $WLS; do
-  run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-rast
+  run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-sub
 done
 for wl in rt rast c4 c5 c5yaw yaw f256; do
   has $wl || continue
   case $wl in rt|rast) S="--steps 64 --warmup 32";; c4|yaw|f256) S="--steps 32 --warmup 32";; *) S="--steps 4 --warmup 2";; esac
   for ctr in FETCH_SIZE WRITE_SIZE; do
-    run pmc_${wl}_$ctr 180 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${wl}_$ctr" -o pmc -- $B --workload $wl $S --no-rast
+    run pmc_${wl}_$ctr 180 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${wl}_$ctr" -o pmc -- $B --workload $wl $S --no-sub
   done
 done
 G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
@@ -39,7 +43,7 @@ for w in rt c4 c5 c5yaw yaw f256 rast; do
   i=0
   for g in "$G1" "$G2" "$G3"; do
     i=$((i+1))
-    run sq_${w}_$i 180 rocprofv3 --pmc $g --output-format csv -d "$OUT/sq_${w}_$i" -o sq -- $B --workload $w $S --no-rast
+    run sq_${w}_$i 180 rocprofv3 --pmc $g --output-format csv -d "$OUT/sq_${w}_$i" -o sq -- $B --workload $w $S --no-sub
   done
 done
 echo profiles done

@@ -14,6 +14,22 @@ SECTION = sys.argv[3] if len(sys.argv) > 3 else "rt"
 FPL = int(sys.argv[4]) if len(sys.argv) > 4 else 32     # frames per launch of the profiled kernel
 SIMDS = 256 * 4
 
+
+
+def code_sha256(kernel):
+    """The profiled kernel's machine code identity: gpurun_out/code_sha256.json written on the
+    GPU box by scripts/profile_round.sh (the library the counters ran on), else this tree's build."""
+    sys.path.insert(0, os.path.join(ROOT, "computer-graphics_amd"))
+    import codeobj
+    try:
+        rec = json.load(open(os.path.join(ROOT, "gpurun_out", "code_sha256.json")))
+        if kernel in rec:
+            return rec[kernel]
+    except (OSError, ValueError):
+        pass
+    return codeobj.kernel_sha256(kernel)
+
+
 agg = collections.defaultdict(list)
 for f in sorted(glob.glob(SRC)):
     for r in csv.DictReader(open(f)):
@@ -28,6 +44,7 @@ sq = {"kernel": KERNEL, "counters_per_launch": c,
       "wave_state_frac": {"active": c["SQ_ACTIVE_INST_ANY"] / wave, "issue_stall": c["SQ_WAIT_INST_ANY"] / wave,
                           "waiting": c["SQ_WAIT_ANY"] / wave},
       "frames_per_launch": FPL,
+      "code_sha256": code_sha256(KERNEL),
       "note": "valu_issue_frac = SQ_INSTS_VALU x 2 cyc / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
 path = os.path.join(ROOT, "profiles", "pmc_summary.json")
 out = json.load(open(path))

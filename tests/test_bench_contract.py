@@ -5,6 +5,7 @@ parity flags the run checked."""
 import json
 import os
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -54,3 +55,65 @@ def test_headline_line_checks_parity_and_roofline():
     c3 = d["rast"]
     assert c3["value"] > 0 and c3["single_frame_ms"] > 0 and 0 < c3["roofline"]["frac"] <= 1
     assert c3["cpu_baseline"]["frame_matches_gpu"] is True
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_roofline_frac_is_tied_to_the_profiled_machine_code(monkeypatch):
+    """the executed-work fraction scales SQ counters of one build of a
+    kernel; a profile whose code_sha256 differs from this build's kernel code nulls it."""
+    import cgamd
+    import codeobj
+    if not os.path.exists(cgamd.LIB_PATH):
+        pytest.skip("libcgamd.so not built")
+    b = _bench()
+    have = codeobj.kernel_sha256("rt_lattice_kernel", cgamd.LIB_PATH)
+    assert have and len(have) == 64
+    prof = {"valu_lane_ops_per_launch": 5.7e10, "frames_per_launch": 32, "wave_state_frac": {}}
+    monkeypatch.setattr(b, "load_sq", lambda kernel, section="rt": dict(prof, code_sha256="0" * 64))
+    r = b.valu_roofline("rt_lattice_kernel", "rt", 32, 1.0, 1.5)
+    assert r["frac"] is None and r["achieved"] is None and "re-profile" in r["frac_null_reason"]
+    monkeypatch.setattr(b, "load_sq", lambda kernel, section="rt": dict(prof))          # no hash recorded
+    assert b.valu_roofline("rt_lattice_kernel", "rt", 32, 1.0, 1.5)["frac"] is None
+    monkeypatch.setattr(b, "load_sq", lambda kernel, section="rt": dict(prof, code_sha256=have))
+    r = b.valu_roofline("rt_lattice_kernel", "rt", 32, 1.0, 1.5)
+    assert r["frac"] == pytest.approx(5.7e10 / 1.5e-3 / 1e12 / r["peak"])
+
+
+def test_kernel_hash_tracks_machine_code():
+    """Template instances are hashed together, unknown kernels have no hash, and different
+    kernels hash differently."""
+    import cgamd
+    import codeobj
+    if not os.path.exists(cgamd.LIB_PATH):
+        pytest.skip("libcgamd.so not built")
+    hs = {k: codeobj.kernel_sha256(k, cgamd.LIB_PATH)
+          for k in ("rt_lattice_kernel", "rt_lattice_lights_kernel", "rt_big_primary_kernel", "rast_fill_kernel")}
+    assert all(hs.values()) and len(set(hs.values())) == len(hs)
+    assert codeobj.kernel_sha256("no_such_kernel", cgamd.LIB_PATH) is None
+
+
+def test_r2_sample_covers_the_whole_frame():
+    """C4/C5 CPU baselines sample an R2 sequence over the whole frame (not the
+    central half): a short prefix already reaches every quadrant and both borders."""
+    b = _bench()
+    W, H = 3840, 2160
+    xy = b.r2_pixels(W, H, 0, 64)
+    assert xy[:, 0].min() >= 0 and xy[:, 0].max() < W and xy[:, 1].min() >= 0 and xy[:, 1].max() < H
+    q = {(x * 4 // W, y * 4 // H) for x, y in xy}
+    assert len(q) == 16
+    assert xy[:, 0].min() < W // 8 and xy[:, 0].max() > 7 * W // 8
+    assert xy[:, 1].min() < H // 8 and xy[:, 1].max() > 7 * H // 8
+    assert np.array_equal(b.r2_pixels(W, H, 16, 8), xy[16:24])      # prefixes compose
+
+
+def test_cpu_info_reports_physical_cores():
+    b = _bench()
+    ci = b.cpu_info()
+    assert 1 <= ci["usable_cores"] <= ci["physical_cores"] <= ci["logical_cpus"]

@@ -85,16 +85,55 @@ def test_dist_local_matches_single_gpu(nranks, chunk, pipeline):
             c.close()
 
 
-@pytest.mark.parametrize("kind", ["c4", "yaw"])
+@pytest.mark.parametrize("pipeline", [cgamd.DIST_SIGNALLED, cgamd.DIST_CHUNKED])
+def test_dist_local_back_to_back_calls(pipeline):
+    """Several calls on the same streams with no synchronisation in between,
+    each with its own cameras and output buffer (a call's slot
+    counters are reused two calls later; a wait that passed on the stale
+    counts would ship a half-written band).  Every call's frames must equal
+    the single-GPU render of its cameras."""
+    W, H, calls, nf = 320, 256, 5, 6
+    lights = cgamd.default_lights()
+    ctxs = _ctxs(3)
+    ds = cgamd.Dist.local(ctxs)
+    try:
+        for d in ds:
+            d.set_chunk(2)
+            d.set_pipeline(pipeline)
+        cams = [[cgamd.rt_camera(W, H, 256.0, (0.03 * (c - 2) + 0.002 * k, 0.01 * c, -3.0 + 0.05 * c + 0.01 * k, 1.0))
+                 for k in range(nf)] for c in range(calls)]
+        outs = [torch.zeros(nf * W * H, dtype=torch.int32, device="cuda") for _ in range(calls)]
+        for c in range(calls):
+            for d in reversed(ds):
+                d.render_frames(cams[c], outs[c].data_ptr() if d.rank == 0 else None, lights=lights)
+        torch.cuda.synchronize()
+        for c in range(calls):
+            want = _single(ctxs[0], cams[c], lights)
+            got = outs[c].cpu().numpy().view(np.uint32).reshape(nf, H * W)
+            assert np.array_equal(got, want), f"call {c}"
+    finally:
+        for d in ds:
+            d.close()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("kind", ["c4", "yaw", "big"])
 def test_dist_local_light_set_and_rotated_camera(kind):
-    """The light-set lattice kernel (C4's 8x8 area light) and the general
-    kernel (yawed camera: full-width rows, pack pass) through the bands."""
+    """The light-set lattice kernel (C4's 8x8 area light), the general kernel
+    (yawed camera: full-width rows, pack pass) and the large-scene pipeline
+    (C5's random scene, here 20k triangles) through the bands."""
     W, H = 240, 120   # whole frames: a multiple of the 8-row tile (no padding rows)
+    scene = None
     if kind == "c4":
         cams, lights = _cams(W, H, 135.0, 3), cgamd.area_lights(None, 0.1, 8)
+    elif kind == "big":
+        n = 20000
+        scene = (cgamd.random_scene(n, 0x5EED), n, None)
+        cams, lights = _cams(W, H, 135.0, 3), cgamd.default_lights()
     else:
         cams, lights = _cams(W, H, 135.0, 3, cgamd.yaw_matrix(0.1745)), cgamd.default_lights()
-    ctxs = _ctxs(4)
+    ctxs = _ctxs(4, scene)
     ds = cgamd.Dist.local(ctxs)
     try:
         want = _single(ctxs[0], cams, lights)

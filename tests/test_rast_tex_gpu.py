@@ -1,9 +1,14 @@
 """GPU: rasteriser texture modes 1-3 (skeleton.cpp:588-645) against the oracle,
-bit-exact in colour, depth and shadow.  The maps are synthetic (seeded): the
-reference's own JPEGs need OpenCV's decoder and Marble2000x2000.jpg is missing,
-so no reference-rendered textured frame exists ("parity unpinned" against the
-reference; pinned against the CPU restatement, which follows the reference
-line by line)."""
+bit-exact in colour, depth and shadow.
+
+Two sets of maps: seeded synthetic maps (every mode, including marble, whose
+Marble2000x2000.jpg is missing from the reference tree), and the reference's
+own grill and woven-wood JPEGs (tests/golden/textures), decoded on the GPU by
+cg_image_decode_jpeg -- bit-equal to IJG libjpeg 9, which OpenCV 3.4's imread
+uses -- and thresholded as skeleton.cpp:138-155 does.  The grill mode with
+the real maps is also pinned to the reference's rasteriser/screenshot.bmp
+(tests/test_rast_screenshot.py); woven wood (mode 3, :622-645) has no
+reference-rendered frame, so it is pinned through the restatement."""
 import ctypes as C
 
 import numpy as np
@@ -146,3 +151,45 @@ def test_device_list_with_unloaded_texture_shades_as_texture_0(ctx):
         _check((a.cpu().numpy().view(np.uint32), d.cpu().numpy(), s.cpu().numpy()), (ra, rd, rs), "device list")
     finally:
         ctx.rast_set_textures(None)
+
+
+@pytest.fixture(scope="module")
+def real_maps(ctx):
+    """The reference's JPEG maps decoded on the GPU, and the oracle's decode of the same files."""
+    import make_golden as mg
+    jp = mg.texture_jpegs()
+    gpu = {k: ctx.decode_jpeg(v) for k, v in jp.items()}
+    ref = {k: oracle.jpeg_decode(v) for k, v in jp.items()}
+    for k in jp:
+        assert np.array_equal(gpu[k], ref[k]), k
+    return gpu, ref
+
+
+REAL_CASES = [(3, 3, 0.2, 0.0), (3, 0, 0.2, 0.35), (0, 3, 0.15, 0.1745), (2, 3, 0.2, -0.52),
+              (3, 2, 0.2, 0.0), (2, 2, 0.15, -0.1745)]
+
+
+@pytest.mark.parametrize("setting,boxes,ind,yaw", REAL_CASES)
+def test_real_maps_draw_matches_oracle(ctx, real_maps, setting, boxes, ind, yaw):
+    """Woven-wood (mode 3) and grill (mode 2) rooms and boxes with the reference's maps,
+    yawed cameras included (findU/findV through inverse(R), :1756-1825)."""
+    gpu, ref = real_maps
+    R = cgamd.yaw_matrix(yaw) if yaw else None
+    p = cgamd.rast_params(W, H, F, R=R, indirect_first=ind, yaw=yaw)
+    po = oracle.rast_params(W, H, F, R=list(R) if R is not None else None, indirect_first=ind,
+                            setting=setting, setting_boxes=boxes, yaw=yaw)
+    oracle.rast_set_textures(ref)
+    ctx.rast_set_textures(gpu)
+    try:
+        want = oracle.rast_draw(po)
+        ctx.rast_set_scene(*cgamd.rast_scene(setting, boxes))
+        got = ctx.rast_draw(p)[:3]
+    finally:
+        oracle.rast_set_textures(None)
+        ctx.rast_set_textures(None)
+        ctx.rast_set_scene()
+    _check(got, want, f"real maps {setting}/{boxes} yaw {yaw}")
+    # the textures matter: the frame differs from texture 0's
+    ref0 = oracle.rast_draw(oracle.rast_params(W, H, F, R=list(R) if R is not None else None, indirect_first=ind,
+                                               yaw=yaw))
+    assert (got[0] != ref0[0]).mean() > 0.05
