@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_pixel_kernel(RtFra
 // (pc += DirectLight; pc += objColor * indirect, k = 0..8), so the float sums
 // are formed exactly as the reference forms them.
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
-constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1, kLatN = kLatW * kLatH;
+constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1;
 constexpr int kLatWY = 3 * kLatTileW;   // per-pixel columns (a yawed camera): 48 x 31 = 1488 rays
 
 // Shared pieces of the two lattice kernels.
@@ -843,9 +843,13 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
 // up to four pixels (1023 points for 240 pixels instead of 2160 sub-rays).
 // The tile's 15 pixel rows are swept in thirds (pixel rows 0-4, 5-9, 10-14;
 // the lattice rows between two thirds are computed by both) so the column
-// buffers stay small (2 x 11 rows x 3 x 64 floats): 31.3 KB of LDS per
+// buffers stay small (2 x 11 rows x 3 x 64 floats): 28.2 KB of LDS per
 // workgroup, 5 workgroups (waves per SIMD) per CU -- halves (17 rows, 40 KB)
-// allowed 4 and ran 4 % slower.
+// allowed 4 and ran 4 % slower; quarters (9 rows, 25.4 KB) allow 6 and ran
+// 6 % slower (the shared rows cost more than the sixth wave gains), fifths
+// 10 % slower.  The per-unit shadow certificates run in a kernel of their own
+// (rt_lattice_units_kernel): inside this one their FP64 work needed ~120
+// VGPRs and spilled 112 B per lane at 5 waves.
 // Whether triangle c stays a shadow candidate for hits in [lo, hi] of camera
 // rays (X, [y0, y1], focal) towards the frame's light set: cull_shadow, and
 // when every hit lies on c (own) the own-triangle certificate.
@@ -875,73 +879,101 @@ constexpr int kLatMaxLights = 64;
 // lights contiguous and in order, so one ds_read_b128 still yields l .. l + 3.
 __device__ __forceinline__ int lat_swz(int r, int c) { return 4 * ((r * 3 + c) & 15); }
 
+// The tile state both light-set kernels start from: the frame's camera, the
+// tile, its certificates (rt_prepare_kernel) and pass 1 (the closest hit of
+// every needed lattice point) in s_t / s_bi (kLatNoHit: no hit).  False: the tile is done (outside the
+// RGB24 window, or certified black -- then stored black when store_black).
+constexpr int kLatNoHit = -128;   // s_bi: hit indices are -kLatMaxSph .. 62
+struct LatLightsTile {
+    RtFrame F, Fs;
+    LatTile G;
+    LatOut o;
+    unsigned long long smask;
+    size_t tix;
+    int nhalf;
+};
 template <int PITCH>
-__device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtTri *__restrict__ tc,
-                                                    const RtShade *__restrict__ shade,
-                                                    const RtSphere *__restrict__ sph,
-                                                    const unsigned long long *__restrict__ lat_masks,
-                                                    const RtFrameCams &cams, size_t out_stride,
-                                                    uint32_t *__restrict__ out)
+__device__ __forceinline__ bool lat_lights_tile(const RtFrame &F0, const RtTri *__restrict__ &tc,
+                                                const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
+                                                const unsigned long long *__restrict__ lat_masks,
+                                                const RtFrameCams &cams, size_t out_stride, uint32_t *out,
+                                                bool store_black, float *s_t, int8_t *s_bi, LatObj *s_obj,
+                                                LatLightsTile &T)
 {
     const int frame = blockIdx.z;
-    RtFrame F = F0;
+    RtFrame &F = T.F;
+    F = F0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
     tc += (size_t)frame * F.n_tris;
     lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
-    const LatOut o = lat_out(F, frame, out_stride, out);
+    T.o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int by = lat_tile_row();
-    LatTile G = lat_tile(F, blockIdx.x, by);
+    LatTile &G = T.G;
+    G = lat_tile(F, blockIdx.x, by);
     G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
-    const int ay0 = G.ay0, cols = G.cols, rows = G.rows;
-    __shared__ float2 s_hit[PITCH * kLatH];                                   // (t, hit index bits)
-    __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
-    __shared__ float s_dl[2][kLatHalfRows][3][kLatMaxLights];         // column buffers
-    __shared__ float s_pc[kLatTileH][kLatTileW][3];                   // pixel sums
-    __shared__ uint8_t s_valid[kLatTileH][kLatTileW];
     lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
-    const int npts = PITCH * rows;
+    const int npts = PITCH * G.rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
-    if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window
-    const size_t tix = (size_t)by * gridDim.x + blockIdx.x;
-    const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
-    const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
-    const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
+    if (G.u0 + G.nu <= T.o.wc0 || G.u0 >= T.o.wc0 + T.o.pitch) return false;   // outside the RGB24 window
+    T.tix = (size_t)by * gridDim.x + blockIdx.x;
+    const unsigned long long m0 = uniform_u64(lat_masks[2 * T.tix]);
+    const unsigned long long s0 = uniform_u64(lat_masks[2 * T.tix + 1]);
+    const unsigned long long mask = m0 & ~(3ull << 62);
+    T.smask = s0 & ~(1ull << 63);
     const bool covered = (m0 >> 62) & 1ull;
     RtFrame Fp = F;
     if (!(m0 >> 63)) Fp.n_sph = 0;
-    RtFrame Fs = F;
-    if (!(s0 >> 63)) Fs.n_sph = 0;
+    T.Fs = F;
+    if (!(s0 >> 63)) T.Fs.n_sph = 0;
+    T.nhalf = (G.nv + kLatHalfH - 1) / kLatHalfH;
     if (m0 == 0ull) {
-        lat_store_black(F, G, o);
-        return;
-    }
-    {
-        const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
-        if (ty < kLatTileH) {
-            s_pc[ty][tx][0] = s_pc[ty][tx][1] = s_pc[ty][tx][2] = 0.0f;
-            s_valid[ty][tx] = 0;
-        }
+        if (store_black) lat_store_black(F, G, T.o);
+        return false;
     }
     __syncthreads();                       // s_obj
     lat_closest<PITCH>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
-        s_hit[p] = make_float2(t, __int_as_float(bi));
+        s_t[p] = t;
+        s_bi[p] = (int8_t)(bi == INT_MIN ? kLatNoHit : bi);
     });
-    __syncthreads();
-    // Shadow candidates per (half, column) unit: the tile's shadow mask
-    // re-certified over the unit's exact hit positions (pos as DirectLight
-    // forms it below), plus the own-triangle certificate when every hit of the
-    // unit lies on one triangle -- the same exact functions as
-    // rt_tile_cert_kernel, over a box of up to 17 points instead of the tile's.
+    return true;
+}
+
+// Shadow candidates per (part, column) unit of a light-set tile, from
+// rt_lattice_units_kernel to rt_lattice_lights_kernel: [frame][tile][part][PITCH].
+template <int PITCH>
+__host__ __device__ constexpr int lat_unit_slots() { return kLatParts * PITCH; }
+
+// The unit certificates of a light-set tile: the tile's shadow mask
+// re-certified over each (part, column) unit's exact hit positions (pos as
+// DirectLight forms it), plus the own-triangle certificate when every hit of
+// the unit lies on one triangle -- the same exact functions as
+// rt_tile_cert_kernel, over a box of up to 11 points instead of the tile's.
+// A kernel of its own: the FP64 certificates need ~120 VGPRs, which would
+// cost the sweep (82) its fifth wave per SIMD or spill.
+template <int PITCH>
+__device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTri *__restrict__ tc,
+                                                   const RtShade *__restrict__ shade,
+                                                   const RtSphere *__restrict__ sph,
+                                                   const unsigned long long *__restrict__ lat_masks,
+                                                   const RtFrameCams &cams, unsigned long long *__restrict__ umask)
+{
+    __shared__ float s_t[PITCH * kLatH];                               // pass 1: t and hit index
+    __shared__ int8_t s_bi[PITCH * kLatH];
+    __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
+    __shared__ float s_ubox[kLatParts][PITCH][6];                     // the units' hit boxes
+    __shared__ int s_uone[kLatParts][PITCH];                          // sole hit triangle (-1: several, -2: none)
     __shared__ unsigned long long s_umask[kLatParts][PITCH];
-    // the units' boxes and sole hit triangles (-1: several, -2: no hit) live
-    // in the column buffers, which the sweep below has not started using yet
-    static_assert(sizeof(s_dl) / 2 >= kLatParts * PITCH * 6 * sizeof(float), "unit scratch");
     static_assert(kLatParts * PITCH <= kRtThreads, "a thread per unit");
-    float(*s_ubox)[PITCH][6] = (float(*)[PITCH][6]) & s_dl[0][0][0][0];
-    int(*s_uone)[PITCH] = (int(*)[PITCH]) & s_dl[1][0][0][0];
-    const int nhalf = (G.nv + kLatHalfH - 1) / kLatHalfH;
+    LatLightsTile T;
+    // black tiles are stored by the sweep kernel; no output here
+    if (!lat_lights_tile<PITCH>(F0, tc, shade, sph, lat_masks, cams, 0, nullptr, false, s_t, s_bi, s_obj, T)) return;
+    const RtFrame &F = T.F;
+    const LatTile &G = T.G;
+    const int ay0 = G.ay0, cols = G.cols, nhalf = T.nhalf;
+    const unsigned long long smask = T.smask;
+    __syncthreads();
     if (threadIdx.x < kLatParts * PITCH) {
         const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
         if (h < nhalf && cx < cols) {
@@ -951,10 +983,9 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             int one = -2;
             const float X = lat_x(F, G, cx);
             for (int r = 0; r < nlr; ++r) {
-                const float2 hq = s_hit[(lr0 + r) * PITCH + cx];
-                const int bi = __float_as_int(hq.y);
-                if (bi == INT_MIN) continue;
-                const float Y = 0.5f * (float)(ay0 + lr0 + r), t = hq.x;
+                const int bi = s_bi[(lr0 + r) * PITCH + cx];
+                if (bi == kLatNoHit) continue;
+                const float Y = 0.5f * (float)(ay0 + lr0 + r), t = s_t[(lr0 + r) * PITCH + cx];
                 pb.add(v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal));
                 one = (one == -2 || one == bi) ? bi : -1;
             }
@@ -967,38 +998,81 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
         }
     }
     __syncthreads();
+    const int nc = __popcll(smask), pairs = nhalf * PITCH * nc;
+    for (int it = threadIdx.x; it < pairs; it += kRtThreads) {
+        const int unit = it / nc, ci = it - unit * nc;
+        const int h = unit / PITCH, cx = unit - h * PITCH;
+        if (cx >= cols) continue;
+        const int one = s_uone[h][cx];
+        if (one == -2) continue;   // no hit, no shadow ray
+        const int k = nth_bit(smask, ci);
+        const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
+        const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
+        const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
+        const float X = lat_x(F, G, cx);
+        const float y0 = 0.5f * (float)(ay0 + lr0), y1 = 0.5f * (float)(ay0 + lr0 + nlr - 1);
+        if (lat_unit_keeps(F, tc[k], s_obj[k], one == k, X, y0, y1, lo, hi))
+            atomicOr(&s_umask[h][cx], 1ull << k);
+    }
+    // bit 63: a sphere may block a shadow ray of the unit -- the sphere-shadow
+    // certificate of every light over the unit's hit box (the tile's flag,
+    // rt_tile_cert_kernel, covers the whole tile)
+    const int spairs = T.Fs.n_sph > 0 ? nhalf * PITCH * F.n_lights : 0;
+    for (int it = threadIdx.x; it < spairs; it += kRtThreads) {
+        const int unit = it / F.n_lights, l = it - unit * F.n_lights;
+        const int h = unit / PITCH, cx = unit - h * PITCH;
+        if (cx >= cols || s_uone[h][cx] == -2) continue;
+        const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
+        const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
+        const RtLight Lt = F.lights[l];
+        const double Lp[3] = {(double)Lt.x, (double)Lt.y, (double)Lt.z};
+        bool may = false;
+        for (int q = 0; q < T.Fs.n_sph && !may; ++q) may = !sphere_shadow_surely_missed(sph[q], Lp, lo, hi);
+        if (may) atomicOr(&s_umask[h][cx], 1ull << 63);
+    }
+    __syncthreads();
+    if (threadIdx.x < kLatParts * PITCH) {
+        const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
+        if (h < nhalf && cx < cols)
+            umask[((size_t)blockIdx.z * gridDim.x * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x] =
+                s_umask[h][cx];
+    }
+}
+
+template <int PITCH>
+__device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtTri *__restrict__ tc,
+                                                    const RtShade *__restrict__ shade,
+                                                    const RtSphere *__restrict__ sph,
+                                                    const unsigned long long *__restrict__ lat_masks,
+                                                    const unsigned long long *__restrict__ umask,
+                                                    const RtFrameCams &cams, size_t out_stride,
+                                                    uint32_t *__restrict__ out)
+{
+    __shared__ float s_t[PITCH * kLatH];                              // pass 1: t and hit index
+    __shared__ int8_t s_bi[PITCH * kLatH];
+    __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
+    __shared__ float s_dl[2][kLatHalfRows][3][kLatMaxLights];         // column buffers
+    __shared__ float s_pc[kLatTileH][kLatTileW][3];                   // pixel sums
+    __shared__ uint8_t s_valid[kLatTileH][kLatTileW];
+    __shared__ unsigned long long s_umask[kLatParts][PITCH];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    LatLightsTile T;
+    if (!lat_lights_tile<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out, true, s_t, s_bi, s_obj, T)) return;
+    const RtFrame &F = T.F, &Fs = T.Fs;
+    const LatTile &G = T.G;
+    const int ay0 = G.ay0, cols = G.cols;
     {
-        const int nc = __popcll(smask), pairs = nhalf * PITCH * nc;
-        for (int it = threadIdx.x; it < pairs; it += kRtThreads) {
-            const int unit = it / nc, ci = it - unit * nc;
-            const int h = unit / PITCH, cx = unit - h * PITCH;
-            if (cx >= cols) continue;
-            const int one = s_uone[h][cx];
-            if (one == -2) continue;   // no hit, no shadow ray
-            const int k = nth_bit(smask, ci);
-            const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
-            const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
-            const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
-            const float X = lat_x(F, G, cx);
-            const float y0 = 0.5f * (float)(ay0 + lr0), y1 = 0.5f * (float)(ay0 + lr0 + nlr - 1);
-            if (lat_unit_keeps(F, tc[k], s_obj[k], one == k, X, y0, y1, lo, hi))
-                atomicOr(&s_umask[h][cx], 1ull << k);
+        const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+        if (ty < kLatTileH) {
+            s_pc[ty][tx][0] = s_pc[ty][tx][1] = s_pc[ty][tx][2] = 0.0f;
+            s_valid[ty][tx] = 0;
         }
-        // bit 63: a sphere may block a shadow ray of the unit -- the
-        // sphere-shadow certificate of every light over the unit's hit box
-        // (the tile's flag, rt_tile_cert_kernel, covers the whole tile)
-        const int spairs = Fs.n_sph > 0 ? nhalf * PITCH * F.n_lights : 0;
-        for (int it = threadIdx.x; it < spairs; it += kRtThreads) {
-            const int unit = it / F.n_lights, l = it - unit * F.n_lights;
-            const int h = unit / PITCH, cx = unit - h * PITCH;
-            if (cx >= cols || s_uone[h][cx] == -2) continue;
-            const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
-            const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
-            const RtLight Lt = F.lights[l];
-            const double Lp[3] = {(double)Lt.x, (double)Lt.y, (double)Lt.z};
-            bool may = false;
-            for (int q = 0; q < Fs.n_sph && !may; ++q) may = !sphere_shadow_surely_missed(sph[q], Lp, lo, hi);
-            if (may) atomicOr(&s_umask[h][cx], 1ull << 63);
+        // the units' shadow candidates (rt_lattice_units_kernel)
+        if (threadIdx.x < kLatParts * PITCH) {
+            const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
+            if (h < T.nhalf && cx < cols)
+                s_umask[h][cx] =
+                    umask[((size_t)blockIdx.z * gridDim.x * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x];
         }
     }
     __syncthreads();
@@ -1028,10 +1102,9 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                 const float X = lat_x(F, G, cx);
                 auto item = [&](int r, int l, const RtLight &Lt) {
                     const int cy = lr0 + r;
-                    const float2 hq = s_hit[cy * PITCH + cx];
-                    const int bi = __float_as_int(hq.y);
-                    if (bi == INT_MIN) return;
-                    const float Y = 0.5f * (float)(ay0 + cy), t = hq.x;
+                    const int bi = s_bi[cy * PITCH + cx];
+                    if (bi == kLatNoHit) return;
+                    const float Y = 0.5f * (float)(ay0 + cy), t = s_t[cy * PITCH + cx];
                     const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
                     const vec3 dl = lat_direct_light(Fu, tc, sph, s_obj, Lt, bi, pos, um);
                     float *b = &s_dl[step & 1][r][0][0];
@@ -1061,8 +1134,8 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                     const float *buf = &s_dl[cx & 1][0][0][0];
                     for (int j = 0; j < 3; ++j) {
                         const int r = 2 * fpr + j;
-                        const int bi = __float_as_int(s_hit[(lr0 + r) * PITCH + cx].y);
-                        if (bi == INT_MIN) continue;
+                        const int bi = s_bi[(lr0 + r) * PITCH + cx];
+                        if (bi == kLatNoHit) continue;
                         valid = true;
                         const float *b = buf + (r * 3 + fcomp) * kLatMaxLights;
                         const int sw = lat_swz(r, fcomp);
@@ -1092,7 +1165,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
         const vec3 pc = v3(s_pc[ty][tx][0], s_pc[ty][tx][1], s_pc[ty][tx][2]);
         px = s_valid[ty][tx] ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
     }
-    lat_store(F, G, o, px, tx, ty, (uint32_t *)&s_dl[0][0][0][0]);
+    lat_store(F, G, T.o, px, tx, ty, (uint32_t *)&s_dl[0][0][0][0]);
 }
 
 // The kernels.  frame_done (optional, cg_dist's transfer pipeline): when a
@@ -1122,15 +1195,27 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
 }
 
 template <int PITCH>
+__global__ __launch_bounds__(kRtThreads) void rt_lattice_units_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+                                                                      const RtShade *__restrict__ shade,
+                                                                      const RtSphere *__restrict__ sph,
+                                                                      const unsigned long long *__restrict__ lat_masks,
+                                                                      RtFrameCams cams,
+                                                                      unsigned long long *__restrict__ umask)
+{
+    lattice_units_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, umask);
+}
+
+template <int PITCH>
 __global__ __launch_bounds__(kRtThreads, 5) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                           const RtShade *__restrict__ shade,
                                                                           const RtSphere *__restrict__ sph,
                                                                           const unsigned long long *__restrict__ lat_masks,
+                                                                          const unsigned long long *__restrict__ umask,
                                                                           RtFrameCams cams, size_t out_stride,
                                                                           uint32_t *__restrict__ out,
                                                                           uint32_t *frame_done)
 {
-    lattice_lights_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
+    lattice_lights_body<PITCH>(F0, tc, shade, sph, lat_masks, umask, cams, out_stride, out);
     lat_signal(frame_done, blockIdx.z);
 }
 
@@ -1364,12 +1449,38 @@ size_t rt_lattice_tiles(const RtFrame &F)
 
 // Batched lattice launch: nframes frames of F's geometry, frame f with camera
 // cams.c[f] into d_out + f * out_stride (rt_use_lattice(F) must hold).
+// Light sets (n_lights > 1) need the per-unit shadow masks of
+// rt_lattice_units_kernel: rt_lattice_unit_bytes(F, nframes) of scratch,
+// filled by launch_rt_lattice_units before the lattice launch reads them.
+size_t rt_lattice_unit_bytes(const RtFrame &F, int nframes)
+{
+    if (!rt_use_lattice(F) || F.n_lights <= 1) return 0;
+    const int slots = lat_yaw(F) ? lat_unit_slots<kLatWY>() : lat_unit_slots<kLatW>();
+    return (size_t)nframes * rt_lattice_tiles(F) * slots * sizeof(unsigned long long);
+}
+
+hipError_t launch_rt_lattice_units(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
+                                   const RtSphere *d_sph, const unsigned long long *d_lat_masks,
+                                   const RtFrameCams &cams, int nframes, unsigned long long *d_umask, hipStream_t st)
+{
+    if (F.n_lights <= 1) return hipSuccess;
+    const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
+    if (lat_yaw(F))
+        hipLaunchKernelGGL(rt_lattice_units_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+                           d_lat_masks, cams, d_umask);
+    else
+        hipLaunchKernelGGL(rt_lattice_units_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+                           d_lat_masks, cams, d_umask);
+    return hipGetLastError();
+}
+
 hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
                                     const RtSphere *d_sph, const unsigned long long *d_lat_masks,
-                                    const RtFrameCams &cams, int nframes, size_t out_stride, uint32_t *d_out,
-                                    hipStream_t st, uint32_t *d_done)
+                                    const unsigned long long *d_umask, const RtFrameCams &cams, int nframes,
+                                    size_t out_stride, uint32_t *d_out, hipStream_t st, uint32_t *d_done)
 {
     const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
+    if (F.n_lights > 1 && !d_umask) return hipErrorInvalidValue;
     if (F.n_lights == 1 && lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, out_stride, d_out, d_done);
@@ -1378,22 +1489,25 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
                            cams, out_stride, d_out, d_done);
     else if (lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                           d_lat_masks, cams, out_stride, d_out, d_done);
+                           d_lat_masks, d_umask, cams, out_stride, d_out, d_done);
     else
         hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                           d_lat_masks, cams, out_stride, d_out, d_done);
+                           d_lat_masks, d_umask, cams, out_stride, d_out, d_done);
     return hipGetLastError();
 }
 
 hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
-                            const RtSphere *d_sph, const unsigned long long *d_lat_masks, uint32_t *d_out,
-                            hipStream_t st)
+                            const RtSphere *d_sph, const unsigned long long *d_lat_masks,
+                            unsigned long long *d_umask, uint32_t *d_out, hipStream_t st)
 {
     dim3 grid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
     if (d_lat_masks && rt_use_lattice(F)) {
         RtFrameCams cams{};
         for (int c = 0; c < 4; ++c) cams.c[0][c] = F.cam[c];
-        return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, 0, d_out, st, nullptr);
+        hipError_t e = launch_rt_lattice_units(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, d_umask, st);
+        if (e != hipSuccess) return e;
+        return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, d_umask, cams, 1, 0, d_out, st,
+                                        nullptr);
     } else if (F.n_tris <= 64 && F.cull_primary)
         hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);

@@ -19,10 +19,14 @@ hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTr
                              const RtFrame *, const RtSphere *, unsigned long long *, unsigned long long *);
 size_t rt_sup_units(const RtFrame &);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
-                                    const unsigned long long *, const RtFrameCams &, int, size_t, uint32_t *,
-                                    hipStream_t, uint32_t *);
+                                    const unsigned long long *, const unsigned long long *, const RtFrameCams &,
+                                    int, size_t, uint32_t *, hipStream_t, uint32_t *);
+hipError_t launch_rt_lattice_units(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
+                                   const unsigned long long *, const RtFrameCams &, int, unsigned long long *,
+                                   hipStream_t);
+size_t rt_lattice_unit_bytes(const RtFrame &, int);
 hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
-                            const unsigned long long *, uint32_t *, hipStream_t);
+                            const unsigned long long *, unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
 int rt_lattice_kind(const RtFrame &);
 size_t rt_lattice_tiles(const RtFrame &);
@@ -85,13 +89,14 @@ struct cg_ctx {
     DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
     DevBuf latmask;                     // lattice tiles' certificates (two masks per tile)
     DevBuf supmask;                     // their super-tiles' certificates (two-level path)
+    DevBuf umask;                       // light sets: the tiles' per-unit shadow masks
     // Batched lattice launches pipeline their certificate kernels on `aux`:
     // call j+1's certificates run beside call j's lattice kernel, each call
     // with its own slot of buffers (rt_enqueue_lattice_batch).
     hipStream_t aux = nullptr;
     hipEvent_t ev_cert[2] = {nullptr, nullptr}, ev_lat[2] = {nullptr, nullptr};
     int slot = 0;
-    DevBuf ptc[2], pshade[2], plat[2], psup[2];
+    DevBuf ptc[2], pshade[2], plat[2], psup[2], pumask[2];
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     int pend_cap = 0;                   // cg_rt_set_pending_cap (0 = default)
     // large-scene pools (cg_rt_big.hip): capacities in entries, sized on the
@@ -272,6 +277,7 @@ extern "C" void cg_destroy(cg_ctx *c)
     if (c->start_ev) (void)hipEventDestroy(c->start_ev);
     for (int k = 0; k < 2; ++k) {
         c->ptc[k].release(); c->pshade[k].release(); c->plat[k].release(); c->psup[k].release();
+        c->pumask[k].release();
         if (c->ev_cert[k]) (void)hipEventDestroy(c->ev_cert[k]);
         if (c->ev_lat[k]) (void)hipEventDestroy(c->ev_lat[k]);
     }
@@ -645,7 +651,11 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
     }
     RtFrameCams cams{};
     for (int k = 0; k < 4; ++k) cams.c[0][k] = F.cam[k];
-    unsigned long long *supm = nullptr;
+    unsigned long long *supm = nullptr, *um = nullptr;
+    if (lat && rt_lattice_unit_bytes(F, 1)) {
+        CG_TRY(c, c->umask.ensure(rt_lattice_unit_bytes(F, 1)), "alloc lattice unit masks");
+        um = (unsigned long long *)c->umask.p;
+    }
     if (lat) {   // two-level tile certificates: super-tiles, then tiles
         CG_TRY(c, c->supmask.ensure(rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
         supm = (unsigned long long *)c->supmask.p;
@@ -654,7 +664,7 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
                                 (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
     if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st);
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
-                               (const RtSphere *)c->sph.p, lat, d_out, st), "rt_pixel launch");
+                               (const RtSphere *)c->sph.p, lat, um, d_out, st), "rt_pixel launch");
     return CG_OK;
 }
 
@@ -688,7 +698,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     // calls ago, ev_lat[k])
     const int k = c->slot;
     c->slot ^= 1;
-    DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k];
+    DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k], &bum = c->pumask[k];
     const size_t tiles = rt_lattice_tiles(F);
     CG_TRY(c, blat.ensure((size_t)nf * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
     CG_TRY(c, btc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
@@ -712,12 +722,21 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)btc.p,
                                 (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm),
            "rt_prepare launch");
+    // light sets: the per-unit shadow certificates, with the other certificates
+    unsigned long long *um = nullptr;
+    if (rt_lattice_unit_bytes(F, nf)) {
+        CG_TRY(c, bum.ensure(rt_lattice_unit_bytes(F, nf)), "alloc lattice unit masks");
+        um = (unsigned long long *)bum.p;
+        CG_TRY(c, launch_rt_lattice_units(F, (const RtTri *)btc.p, (const RtShade *)bsh.p, (const RtSphere *)c->sph.p,
+                                          lat, fc, nf, um, cst),
+               "rt_lattice_units launch");
+    }
     if (!cold) {
         CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
         CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
     }
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
-                                       (const RtSphere *)c->sph.p, lat, fc, nf, stride, (uint32_t *)d_out, st,
+                                       (const RtSphere *)c->sph.p, lat, um, fc, nf, stride, (uint32_t *)d_out, st,
                                        d_done),
            "rt_lattice launch");
     CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
