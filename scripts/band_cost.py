@@ -18,6 +18,7 @@ W, H, F = 1920, 1080, 1080.0
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 ONLY = sys.argv[3] if len(sys.argv) > 3 else None   # "whole" / "band": one configuration (for a trace)
+COLD_ONLY = ONLY is not None
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 st = torch.cuda.current_stream(dev)
@@ -50,6 +51,7 @@ with cgamd.Context(0) as ctx:
                 dspan.append(a.elapsed_time(b) * 1e-3)
             host.append(t1 - t0)
         if not cold:
+            torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             for _ in range(n_calls):
                 ctx.rt_render_frames_device(cams, out.data_ptr(), shard=shard, stream=st.cuda_stream, lights=lights,
@@ -61,11 +63,15 @@ with cgamd.Context(0) as ctx:
 
     for name, shard, out, fmt in (("whole", None, whole, 0),) if ONLY in (None, "whole") else ():
         run(shard, out, fmt, 5, True)
-        res[name] = {"cold": run(shard, out, fmt, N, True), "b2b": run(shard, out, fmt, N, False)}
+        res[name] = {"cold": run(shard, out, fmt, N, True)}
+        if not COLD_ONLY:
+            res[name]["b2b"] = run(shard, out, fmt, N, False)
     rows = H // 8
     for r0 in (0, 3 * rows, 5 * rows) if ONLY is None else ((5 * rows,) if ONLY == "band" else ()):
         shard = cgamd.RtShard(row0=r0, rows=rows)
         name = f"band_{r0}"
         run(shard, band, 1, 5, True)
-        res[name] = {"cold": run(shard, band, 1, N, True), "b2b": run(shard, band, 1, N, False)}
+        res[name] = {"cold": run(shard, band, 1, N, True)}
+        if not COLD_ONLY:
+            res[name]["b2b"] = run(shard, band, 1, N, False)
 print(json.dumps(res, indent=1))

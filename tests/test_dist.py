@@ -82,8 +82,9 @@ def test_row_maps_partition_the_frame(S):
 
 def _band_worker(rank, world, port, q):
     """Rank r renders its band (oracle), ranks > 0 send it as RGB24 with gloo
-    p2p, rank 0 assembles: == the single-process frame.  Bands come from a
-    rebalance of skewed timings, so they are uneven."""
+    p2p, rank 0 assembles: == the single-process frame.  Bands come from the
+    library's native partition (cg_dist_band_partition) over all-gathered,
+    skewed timings, so they are uneven."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "computer-graphics_amd"), os.path.join(root, "oracle")]
@@ -93,12 +94,28 @@ def _band_worker(rank, world, port, q):
     try:
         Fb = 40.0   # a focal length at which the scene leaves black columns to crop
         full = oracle.rt_draw(oracle.rt_params(W, H, Fb)).reshape(H, W)
-        bands = cgdist.rebalance(cgdist.equal_bands(H, world), [1.0 + 0.7 * r for r in range(world)],
-                                 [0.3] + [0.0] * (world - 1), H)
+        import cgamd
+        # the library's rebalance, as cg_dist_rebalance runs it: every rank
+        # contributes its measured per-frame time (skewed here), the times are
+        # all-gathered, each rank spreads its time over its band's rows and
+        # calls the native partition (cg_dist_band_partition) -- every rank
+        # must arrive at the same bands
+        eq = cgdist.equal_bands(H, world)
+        t = torch.tensor([1.0 + 0.7 * rank, 0.3 if rank == 0 else 0.0], dtype=torch.float64)
+        allt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        cost = np.zeros(H)
+        for r, (a, n) in enumerate(eq):
+            cost[a:a + n] = float(allt[r][0]) / n
+        bands = cgamd.band_partition_native(cost, world, np.array([float(x[1]) for x in allt]))
+        assert bands == cgdist.rebalance(eq, [float(x[0]) for x in allt], [float(x[1]) for x in allt], H)
+        mine_b = torch.tensor([v for b_ in bands for v in b_], dtype=torch.int64)
+        allb = [torch.empty_like(mine_b) for _ in range(world)]
+        dist.all_gather(allb, mine_b)
+        assert all(torch.equal(x, mine_b) for x in allb)
         r0, nr = bands[rank]
         mine = full[r0:r0 + nr].reshape(-1)
         # the RGB24 window: columns the camera can see anything in
-        import cgamd
         t_, n_, s_ = cgamd.rt_scene()
         c0, c1 = cgamd.frame_columns(t_, n_, s_, 1, cgamd.rt_camera(W, H, Fb))
         cols = c1 - c0
