@@ -9,7 +9,7 @@ import collections, csv, json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"rt": ["rt_lattice_kernel"], "rast": ["rast_clip_kernel", "rast_setup_kernel", "rast_rows_kernel", "rast_fill_kernel",
                                                  "rast_post_kernel"],
-            "c4": ["rt_lattice_lights_kernel"], "yaw": ["rt_lattice_kernel"], "f256": ["rt_lattice_kernel"],
+            "c4": ["rt_lattice_lights_kernel", "rt_lattice_units_kernel"], "yaw": ["rt_lattice_kernel"], "f256": ["rt_lattice_kernel"],
             "c5": None, "c5yaw": None}   # None: every rt_* kernel of the frame (per frame, see below)
 FRAMES_PER_LAUNCH = {"rt": int(os.environ.get("CG_PMC_RT_FRAMES", "32")), "c4": 32, "yaw": 32, "f256": 32}
 
