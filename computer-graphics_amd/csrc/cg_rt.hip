@@ -446,9 +446,12 @@ __global__ __launch_bounds__(256) void rt_tile_cert_kernel(const cg_tri *__restr
 
 // Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
 // one certificate mask per wave (lane k certifies triangle k).
-constexpr int kRtMinWaves = 6;   // waves per SIMD: 80 VGPRs + some scratch; measured fastest (5: no scratch, ~1% slower)
+constexpr int kRtMinWaves = 6;   // waves per SIMD of rt_lattice_kernel (52 VGPRs: 8 fit)
+// The pixel kernel (rotations other than a yaw; no bench configuration) at 5
+// waves per SIMD: 96 VGPRs and no scratch -- 6 spilled 52 B per lane for ~1 %.
+constexpr int kRtPixelWaves = 5;
 template <bool CULL>
-__global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, kRtPixelWaves) void rt_pixel_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                               const RtShade *__restrict__ shade,
                                                               const RtSphere *__restrict__ sph,
                                                               uint32_t *__restrict__ out)
