@@ -104,6 +104,7 @@ _SIGS = {
     "cg_rt_set_scene": (C.c_int, [P, C.POINTER(Tri), C.c_int, C.POINTER(Sphere), C.c_int]),
     "cg_rt_set_pending_cap": (C.c_int, [P, C.c_int]),
     "cg_rt_scratch_info": (C.c_int, [P, C.POINTER(C.c_uint64)]),
+    "cg_rt_pool_demand": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "cg_rt_route": (C.c_int, [C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "cg_rt_set_pool_caps": (C.c_int, [P, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
@@ -506,6 +507,12 @@ class Context:
         out = (C.c_uint64 * 4)()
         self._check(self.lib.cg_rt_scratch_info(self.h, out), "cg_rt_scratch_info")
         return dict(bytes=out[0], listed=out[1], capacity=out[2], overflows=out[3])
+
+    def rt_pool_demand(self):
+        """Entries the latest large-scene frame listed per pool: dict(sup, bin, sbin, sorted)."""
+        out = (C.c_uint64 * 4)()
+        self._check(self.lib.cg_rt_pool_demand(self.h, out), "cg_rt_pool_demand")
+        return dict(sup=out[0], bin=out[1], sbin=out[2], sorted=out[3])
 
     def rt_render(self, cam, lights=None, n_lights=None):
         lights = default_lights() if lights is None else lights

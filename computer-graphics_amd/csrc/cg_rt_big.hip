@@ -105,6 +105,7 @@ struct BigBufs {
     int lat_w, lat_h;             // lattice mode: (2 W + 1) x (2 rows + 1) points; 0 = per-pixel mode
     int lat_yaw;                  // lattice columns per pixel (yawed camera): 3 W x (2 rows + 1) points
     int *sup_pool;                // [cap_sup] triangles the super-bins' certificates keep
+    unsigned long long *sup_pbox_pool, *sup_flat_pbox;   // [cap_sup]: their projected boxes (super-bin bundle)
     Chunk *sup_chunk;             // [n_sups][nch]
     int *sup_pre, *sup_tot;       // [n_sups][nch], [n_sups] (as bin_pre / bin_tot)
     int *sup_flat, *sup_base;     // [cap_sup]: the super lists compacted, super-bin s at sup_base[s]
@@ -257,7 +258,8 @@ __device__ __forceinline__ int pool_reserve(unsigned long long *pool_n, long lon
 // Append this workgroup's kept triangles (kept[r]: triangle base + r*256 +
 // tid) to a pooled list as one chunk, recorded in *slot.
 __device__ __forceinline__ void pooled_append(const bool kept[4], int base, int *pool, unsigned long long *pool_n,
-                                              long long cap, Chunk *slot, int *over)
+                                              long long cap, Chunk *slot, int *over,
+                                              const unsigned long long *val = nullptr, unsigned long long *vpool = nullptr)
 {
     __shared__ int s_w[4][4];
     __shared__ int s_base;
@@ -285,7 +287,11 @@ __device__ __forceinline__ void pooled_append(const bool kept[4], int base, int 
     for (int r = 0; r < 4; ++r) {
         int before = 0;
         for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
-        if (kept[r]) pool[off + before + __popcll(m[r] & lt)] = base + r * 256 + (int)threadIdx.x;
+        if (kept[r]) {
+            const int at = off + before + __popcll(m[r] & lt);
+            pool[at] = base + r * 256 + (int)threadIdx.x;
+            if (vpool) vpool[at] = val[r];
+        }
         for (int q = 0; q < 4; ++q) off += s_w[r][q];
     }
 }
@@ -360,8 +366,11 @@ __global__ __launch_bounds__(256) void rt_sup_compact_kernel(BigBufs B)
     const int sup = blockIdx.y, c = blockIdx.x;
     if (B.sup_over[sup]) return;
     const Chunk ch = B.sup_chunk[(size_t)sup * B.nch + c];
-    int *dst = B.sup_flat + B.sup_base[sup] + B.sup_pre[(size_t)sup * B.nch + c];
-    for (int e = (int)threadIdx.x; e < ch.n; e += 256) dst[e] = B.sup_pool[ch.off + e];
+    const size_t at = (size_t)B.sup_base[sup] + B.sup_pre[(size_t)sup * B.nch + c];
+    for (int e = (int)threadIdx.x; e < ch.n; e += 256) {
+        B.sup_flat[at + e] = B.sup_pool[ch.off + e];
+        B.sup_flat_pbox[at + e] = B.sup_pbox_pool[ch.off + e];
+    }
 }
 
 // Append the kept triangles of this workgroup to a plain list (one atomic per
@@ -403,8 +412,10 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
 // triangle (v0, v0 + e1, v0 + e2) widened by sig (|e1| + |e2|), sig = 2 (Ed +
 // Eu + Ev) / dmin + 2^-21 (the barycentric slack of primary_hit_box), and the
 // ray through X has x = f (X - cam).x / (X - cam).z (nd.z = f, :137).  Without
-// a certain sign, or with the widened box reaching the camera plane, the box
-// is everything.
+// a certain sign, with the widened box reaching the camera plane, or past the
+// int16 range, the box is everything.  (Projecting the three vertices' boxes
+// instead of the triangle's box measured no shorter lists for C5 and a
+// slower super-bin pass.)
 constexpr unsigned long long kProjAll = 0x7fff8000ull | (0x7fff8000ull << 32);
 constexpr unsigned long long kProjNone = 0x80007fffull | (0x80007fffull << 32);   // x0 > x1: meets nothing
 __device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, const cg_tri &T, const float cam[4],
@@ -440,11 +451,11 @@ __device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, cons
     range(lo[0], hi[0], xl, xh);
     range(lo[1], hi[1], yl, yh);
     auto q = [](double v, bool up) -> unsigned long long {
-        double r = up ? ceil(v) : floor(v);
-        r = fmin(fmax(r, -32768.0), 32767.0);
+        const double r = up ? ceil(v) : floor(v);
         return (unsigned long long)(unsigned short)(short)(int)r;
     };
-    if (!(isfinite(xl) && isfinite(xh) && isfinite(yl) && isfinite(yh))) return kProjAll;
+    // past the int16 range (frames over 64k pixels wide; NaN fails too) no box
+    if (!(xl >= -32768.0 && xh <= 32766.0 && yl >= -32768.0 && yh <= 32766.0)) return kProjAll;
     return q(xl, false) | (q(xh, true) << 16) | (q(yl, false) << 32) | (q(yh, true) << 48);
 }
 
@@ -456,75 +467,126 @@ __device__ __forceinline__ bool proj_meets(unsigned long long b, float x0, float
     return !(x1 < bx0 || x0 > bx1 || y1 < by0 || y0 > by1);
 }
 
+// max |det| over the directions (x, y, f), x in [x0, x1], y in [y0, y1], of
+// the exact linear form det = -d.(e1 x e2) (cull_primary's lin_range; its
+// FP64 rounding is far inside the 2^-20 margins the keys carry).
+__device__ __forceinline__ double det_abs_max(const RtTri &c, float x0, float x1, float y0, float y1, float f)
+{
+    const double Nx = (double)c.e1y * c.e2z - (double)c.e2y * c.e1z, Ny = (double)c.e1z * c.e2x - (double)c.e2z * c.e1x,
+                 Nz = (double)c.e1x * c.e2y - (double)c.e2x * c.e1y;
+    double lo, hi;
+    lin_range(0.5 * ((double)x0 + x1), 0.5 * ((double)y0 + y1), 0.5 * ((double)x1 - x0), 0.5 * ((double)y1 - y0), f,
+              Nx, Ny, Nz, lo, hi);
+    return fmax(fabs(lo), fabs(hi)) * (1.0 + 1e-12);
+}
+
 // K00: camera-ray certificate per (super-bin, triangle) -> super list; the
 // bins then certify only their super-bin's survivors (a bin's bundle lies in
 // its super-bin's, so a triangle the super-bin culls is culled for the bin).
-__global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+// The certificate's edge-function tests alone keep a small triangle whose
+// edge lines all cross the bundle (4-5x the triangles the super-bin's pixels
+// see); its projected box (proj_box16 over the super-bin's PrimDet) is the
+// missing separating axis: a box that misses the bundle culls it too, and
+// the box travels with the entry so that the bins test it before gathering
+// the triangle (every direction a super-bin ray can accept lies in it, and a
+// bin's rays are super-bin rays).
+__global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                             const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int sup = blockIdx.y;
     float x0, x1, y0, y1;
     const bool ok = sup_bundle(F, sup % B.sups_x, sup / B.sups_x, x0, x1, y0, y1);
     const int base = blockIdx.x * kBinTris;
     bool kept[4];
+    unsigned long long pb[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = base + r * 256 + (int)threadIdx.x;
-        kept[r] = ok && i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal);
+        PrimDet pd;
+        kept[r] = ok && i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
+        pb[r] = kProjAll;
+        if (kept[r]) {
+            pb[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+            kept[r] = proj_meets(pb[r], x0, x1, y0, y1);
+        }
     }
     pooled_append(kept, base, B.sup_pool, B.pool_n + kPoolSup, B.cap_sup, B.sup_chunk + (size_t)sup * B.nch + blockIdx.x,
-                  B.sup_over + sup);
+                  B.sup_over + sup, pb, B.sup_pbox_pool);
 }
 
 // K0: camera-ray certificate per (bin, triangle of its super list), with the
 // key: every float distance fl(t |nd|) a ray of the bin computes for the
 // triangle is >= key (t >= tlo by primary_t_range; |nd| >= f (1 - 2^-23)
-// since nd.z = f, :137).  One chunk of the bin list per super-list chunk.
-__global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
-                                                             const cg_tri *__restrict__ tris, BigBufs B)
+// since nd.z = f, :137).
+// The super-bin's box is tested first (no gather for a bin it misses: ~1 in
+// 10 entries meets a bin), and the entries that pass are compacted into an
+// LDS queue certified 1024 at a time, so that every lane of the FP64
+// certificate has work; each certified batch is one chunk of the bin list
+// (a workgroup's batches never outnumber its 1024-entry passes, so a list
+// keeps <= nch chunks).
+__device__ void bin_certify_batch(const RtFrame &F, const RtTri *__restrict__ tc, const cg_tri *__restrict__ tris,
+                                  const BigBufs &B, int bin, bool all, const int *slist,
+                                  const unsigned long long *sbox, const int *q, int cnt, float x0, float x1,
+                                  float y0, float y1)
 {
-    const int bin = blockIdx.y;
-    float x0, x1, y0, y1;
-    if (!bin_bundle(F, bin % B.bins_x, bin / B.bins_x, x0, x1, y0, y1)) return;
-    const int bx = bin % B.bins_x, by = bin / B.bins_x;
-    const int sup = (bx / kSupBins) + (by / kSupBins) * B.sups_x;
-    const bool all = B.sup_over[sup] != 0;               // overflowed super list: every triangle
-    const int ns = all ? F.n_tris : B.sup_tot[sup];
-    const int *slist = B.sup_flat + (all ? 0 : B.sup_base[sup]);
     __shared__ int s_w[4][4];
     __shared__ int s_base;
     __shared__ unsigned s_lo, s_hi;
-    for (int base = blockIdx.x * kBinTris; base < ns; base += gridDim.x * kBinTris) {   // over the super list
     if (threadIdx.x == 0) {
         s_lo = 0u;
         s_hi = 0u;
     }
-    bool kept[4];
+    bool kept[4], ranged[4];
     int tri[4];
     unsigned kbits[4];
-    unsigned long long pbox[4], pbox2[4];
+    unsigned long long pbox[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int e = base + r * 256 + (int)threadIdx.x;
-        const int i = e < ns ? (all ? e : slist[e]) : 0;
+        const int k = r * 256 + (int)threadIdx.x;
+        const int e = k < cnt ? q[k] : -1;
+        const int i = e >= 0 ? (all ? e : slist[e]) : 0;
         tri[r] = i;
-        kept[r] = false;
+        kept[r] = ranged[r] = false;
         kbits[r] = 0u;
-        pbox[r] = pbox2[r] = kProjAll;
-        if (e < ns) {
+        pbox[r] = kProjAll;
+        if (e >= 0) {
+            // the bin's own certificate and box; a box that misses the bin
+            // culls, and without one of its own the bin keeps the super-bin's
+            const unsigned long long sb = all ? kProjAll : sbox[e];
             PrimDet pd;
             kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
-            double tlo, thi;
-            if (kept[r] && primary_t_range(tc[i], pd, tlo, thi)) {
-                const double kd = tlo * (double)F.focal * (1.0 - 0x1p-20);
-                float k = (float)kd;
-                if ((double)k > kd) k = nextafterf(k, 0.0f);
-                kbits[r] = __float_as_uint(k);
+            if (kept[r]) {
+                unsigned long long b = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                if (b == kProjAll) b = sb;
+                kept[r] = proj_meets(b, x0, x1, y0, y1);
+                pbox[r] = b;
+                // the key: t = fl(detT / det_f) and an accepting ray's
+                // direction lies in the box, so |t| >= |detT| / dabs (1 -
+                // 2^-20) with dabs = max |det| + Ed over the bin's part of the
+                // box -- a bound for that triangle's own rays, not the whole
+                // bin's (the walk then meets it at its depth), and one
+                // whatever det's sign.  Keys of triangles whose plane the
+                // bin's rays graze (sign uncertain) stay out of the bin's
+                // bucketing range (ranged)
+                double dabs = fmax(fabs(pd.dlo - pd.Ed), fabs(pd.dhi + pd.Ed));
+                if (kept[r] && b != kProjAll) {
+                    const float bx0 = fmaxf(x0, (float)(short)(b & 0xffff)), bx1 = fminf(x1, (float)(short)((b >> 16) & 0xffff));
+                    const float by0 = fmaxf(y0, (float)(short)((b >> 32) & 0xffff)), by1 = fminf(y1, (float)(short)((b >> 48) & 0xffff));
+                    dabs = fmin(dabs, det_abs_max(tc[i], bx0, bx1, by0, by1, F.focal) + pd.Ed);
+                }
+                const double tlo = fabs((double)tc[i].detT) / dabs * (1.0 - 0x1p-20);
+                if (kept[r] && isfinite(tlo) && tlo > 0.0) {
+                    const double kd = fmin(tlo * (double)F.focal * (1.0 - 0x1p-20), (double)FLT_MAX);
+                    float kf = (float)kd;
+                    if ((double)kf > kd) kf = nextafterf(kf, 0.0f);
+                    kbits[r] = __float_as_uint(kf);
+                    ranged[r] = pd.dlo - pd.Ed > 0 || pd.dhi + pd.Ed < 0;
+                }
             }
-            if (kept[r]) pbox[r] = pbox2[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
         }
     }
     __syncthreads();
-    // append (one reservation per pass), and the bin's positive key range
+    // append (one reservation per batch), and the bin's positive key range
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned long long m[4];
@@ -533,7 +595,7 @@ __global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const
     for (int r = 0; r < 4; ++r) {
         m[r] = __ballot(kept[r]);
         if (lane == 0) s_w[r][w] = __popcll(m[r]);
-        if (kept[r] && kbits[r]) {
+        if (kept[r] && kbits[r] && ranged[r]) {
             lo_inv = max(lo_inv, ~kbits[r]);
             hi = max(hi, kbits[r]);
         }
@@ -550,7 +612,7 @@ __global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const
     if (threadIdx.x == 0) {
         int tot = 0;
         for (int r = 0; r < 4; ++r)
-            for (int q = 0; q < 4; ++q) tot += s_w[r][q];
+            for (int qq = 0; qq < 4; ++qq) tot += s_w[r][qq];
         const int g = pool_reserve(B.pool_n + kPoolBin, B.cap_bin, tot, B.bin_over + bin);
         s_base = tot ? g : -1;
         if (tot && g >= 0) {
@@ -565,29 +627,91 @@ __global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             int before = 0;
-            for (int q = 0; q < 4; ++q) before += q < w ? s_w[r][q] : 0;
+            for (int qq = 0; qq < 4; ++qq) before += qq < w ? s_w[r][qq] : 0;
             if (kept[r]) {
                 const size_t at = (size_t)off + before + __popcll(m[r] & lt);
                 B.bin_ent[at] = ((unsigned long long)kbits[r] << 32) | (unsigned)tri[r];
                 B.bin_pbox[at] = pbox[r];
-                B.bin_pbox2[at] = pbox2[r];
+                B.bin_pbox2[at] = pbox[r];
             }
-            for (int q = 0; q < 4; ++q) off += s_w[r][q];
+            for (int qq = 0; qq < 4; ++qq) off += s_w[r][qq];
         }
     }
-    __syncthreads();                                        // s_w / s_base / s_lo reused by the next chunk
+    __syncthreads();                                        // s_w / s_base / s_lo reused by the next batch
+}
+
+__global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+                                                             const cg_tri *__restrict__ tris, BigBufs B)
+{
+    const int bin = blockIdx.y;
+    float x0, x1, y0, y1;
+    if (!bin_bundle(F, bin % B.bins_x, bin / B.bins_x, x0, x1, y0, y1)) return;
+    const int bx = bin % B.bins_x, by = bin / B.bins_x;
+    const int sup = (bx / kSupBins) + (by / kSupBins) * B.sups_x;
+    const bool all = B.sup_over[sup] != 0;               // overflowed super list: every triangle
+    const int ns = all ? F.n_tris : B.sup_tot[sup];
+    const int *slist = B.sup_flat + (all ? 0 : B.sup_base[sup]);
+    const unsigned long long *sbox = B.sup_flat_pbox + (all ? 0 : B.sup_base[sup]);
+    __shared__ int s_q[2 * kBinTris];                     // super-list entries waiting for the certificate
+    __shared__ int s_w[4][4];
+    int qn = 0;                                           // queued (workgroup-uniform)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int base = blockIdx.x * kBinTris; base < ns; base += gridDim.x * kBinTris) {   // over the super list
+        bool pass[4];
+        unsigned long long m[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = base + r * 256 + (int)threadIdx.x;
+            pass[r] = e < ns && (all || proj_meets(sbox[e], x0, x1, y0, y1));
+            m[r] = __ballot(pass[r]);
+            if (lane == 0) s_w[r][w] = __popcll(m[r]);
+        }
+        __syncthreads();
+        int off = qn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int before = 0;
+            for (int qq = 0; qq < 4; ++qq) before += qq < w ? s_w[r][qq] : 0;
+            if (pass[r]) s_q[off + before + __popcll(m[r] & lt)] = base + r * 256 + (int)threadIdx.x;
+            for (int qq = 0; qq < 4; ++qq) off += s_w[r][qq];
+        }
+        qn = off;
+        __syncthreads();
+        if (qn >= kBinTris) {
+            bin_certify_batch(F, tc, tris, B, bin, all, slist, sbox, s_q, kBinTris, x0, x1, y0, y1);
+            const int rest = qn - kBinTris;               // < kBinTris
+            int mv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = r * 256 + (int)threadIdx.x;
+                mv[r] = k < rest ? s_q[kBinTris + k] : 0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = r * 256 + (int)threadIdx.x;
+                if (k < rest) s_q[k] = mv[r];
+            }
+            qn = rest;
+            __syncthreads();
+        }
     }
+    if (qn > 0) bin_certify_batch(F, tc, tris, B, bin, all, slist, sbox, s_q, qn, x0, x1, y0, y1);
 }
 
 // Bucket of a key within its bin: 0 without a key, else 1 + its place in the
-// bin's positive key range (the same float ops in count and scatter).
+// bin's key range, keys past the range in the last bucket (the same float
+// ops in count and scatter).  Which bucket an entry takes only orders the
+// walk: K1 skips a bucket by its smallest key, so any assignment is exact.
 __device__ __forceinline__ int depth_bucket(unsigned kbits, const BigBufs &B, int bin)
 {
     if (kbits == 0u) return 0;
     const float lo = __uint_as_float(~B.key_lo_inv[bin]), hi = __uint_as_float(B.key_hi[bin]);
     const float k = __uint_as_float(kbits);
-    int b = hi > lo ? 1 + (int)((k - lo) / (hi - lo) * (float)(kDepthBuckets - 1)) : 1;
-    return min(max(b, 1), kDepthBuckets - 1);
+    if (!(hi > lo)) return 1;
+    const float x = (k - lo) / (hi - lo) * (float)(kDepthBuckets - 1);
+    return x < (float)(kDepthBuckets - 2) ? 1 + max((int)x, 0) : kDepthBuckets - 1;
 }
 
 // Per bin: bucket sizes and each bucket's smallest key (workgroups stride
@@ -891,10 +1015,17 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
     __shared__ int s_q[kRtThreads / 64][128];
     int *q_w = s_q[wave];
     int qn = 0;                                                    // wave-uniform
+#ifdef CG_WALK_STATS
+    int st_chunks = 0, st_pass = 0, st_batches = 0, st_walked = 0, st_buckets = 0, st_all = 0, st_wide = 0;
+#endif
     auto certify_walk = [&](int cnt) {                             // the first cnt (<= 64) queued entries
         const int cand = lane < cnt ? q_w[lane] : -1;
         const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
         unsigned long long mask = __ballot(keep);
+#ifdef CG_WALK_STATS
+        ++st_batches;
+        st_walked += __popcll(mask);
+#endif
         while (mask) {
             const int b = __builtin_ctzll(mask);
             mask &= mask - 1ull;
@@ -921,6 +1052,9 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
     for (int q = 0; any && !B.bin_over[bin] && q < kDepthBuckets; ++q) {
         const int b0 = boff[q], b1 = boff[q + 1];
         if (b0 == b1 || __uint_as_float(~bmin_inv[q]) > tb) continue;
+#ifdef CG_WALK_STATS
+        ++st_buckets;
+#endif
         // the next chunk's entries are loaded while this one is scanned
         unsigned long long ent_n = b0 + lane < b1 ? list[b0 + lane] : 0ull;
         unsigned long long pb_n = b0 + lane < b1 ? pboxes[b0 + lane] : 0ull;
@@ -935,6 +1069,13 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
             const unsigned long long pm = __ballot(pass);
             if (pass) q_w[qn + __popcll(pm & ((1ull << lane) - 1ull))] = (int)(unsigned)(ent & 0xffffffffull);
             qn += __popcll(pm);
+#ifdef CG_WALK_STATS
+            ++st_chunks;
+            st_pass += __popcll(pm);
+            st_all += __popcll(__ballot(in && pb == kProjAll));
+            st_wide += __popcll(__ballot(in && pb != kProjAll &&
+                                         (short)((pb >> 16) & 0xffff) - (short)(pb & 0xffff) > 40));
+#endif
             __builtin_amdgcn_wave_barrier();
             if (qn >= 64) {
                 certify_walk(64);
@@ -952,6 +1093,12 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
             __builtin_amdgcn_wave_barrier();
         }
     }
+#ifdef CG_WALK_STATS
+    if (lane == 0 && tx % 30 == 0 && ty % 16 == 0)
+        printf("WALK tx %d ty %d sub %d list %d buckets %d chunks %d pass %d batches %d walked %d tb %g all %d wide %d\n",
+               tx, ty, sub, boff[kDepthBuckets] - boff[0], st_buckets, st_chunks, st_pass, st_batches, st_walked, tb,
+               st_all, st_wide);
+#endif
     LaneShadowBox sb;
     sb.init();
     const vec3 lmin = v3(F.lmin[0], F.lmin[1], F.lmin[2]), lmax = v3(F.lmax[0], F.lmax[1], F.lmax[2]);
@@ -1213,6 +1360,9 @@ __global__ __launch_bounds__(kRtThreads, 5) void rt_shadow_hints_kernel(RtFrame 
     const size_t npix = (size_t)F.rows_out * F.W, pix = (size_t)L * F.W + u;
     unsigned long long shadowed = 0ull, pending = 0ull;
     int last = -1, gtests = 0;
+#ifdef CG_WALK_STATS
+    int st_rays = 0, st_cheap = 0, st_grid_rays = 0, st_lit = 0;
+#endif
     for (int s = 0; s < nsu; ++s) {
         bool on;
         vec3 nd;
@@ -1252,7 +1402,16 @@ __global__ __launch_bounds__(kRtThreads, 5) void rt_shadow_hints_kernel(RtFrame 
                 if (ray && k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
             }
             if (!ray) continue;
+#ifdef CG_WALK_STATS
+            ++st_rays;
+            if (k >= 0) ++st_cheap;
+            const int g0 = gtests;
+#endif
             if (k < 0) k = grid_blocker(B.grid, tc, q, &gtests);
+#ifdef CG_WALK_STATS
+            if (gtests > g0) ++st_grid_rays;
+            if (k < 0) ++st_lit;
+#endif
             const int bitno = kLat ? l : s * F.n_lights + l;
             const unsigned long long bit = 1ull << bitno;
             if (k >= 0) {
@@ -1272,6 +1431,17 @@ __global__ __launch_bounds__(kRtThreads, 5) void rt_shadow_hints_kernel(RtFrame 
             B.pend_bits[id] = pending;
         }
     }
+#ifdef CG_WALK_STATS
+    {
+        int a = st_rays, b = st_cheap, c = st_grid_rays, d = st_lit, e = gtests;
+        for (int o = 32; o; o >>= 1) {
+            a += __shfl_xor(a, o); b += __shfl_xor(b, o); c += __shfl_xor(c, o); d += __shfl_xor(d, o);
+            e += __shfl_xor(e, o);
+        }
+        if (lane == 0 && tx % 30 == 0 && ty % 16 == 0)
+            printf("HINTS tx %d ty %d rays %d cheap %d grid_rays %d lit %d grid_tests %d\n", tx, ty, a, b, c, d, e);
+    }
+#endif
     if (!kLat && active) {
         B.sh_bits[pix] = shadowed;
         B.pend_bits[pix] = pending;
@@ -1651,7 +1821,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
     return big_counter_bytes(B) + 2 * bins * (kDepthBuckets + 1) * 4 + (tiles + bins) * sizeof(ShadowBox) +
            big_slots(B, F) * 8 + 2 * big_words(B, F) * 8 + (size_t)kMaxPend * sizeof(PendRay) +
            (size_t)F.n_tris * 4 + (sups + 2 * bins) * B.nch * sizeof(Chunk) + (sups + bins) * (B.nch + 2) * 4 +
-           (size_t)B.cap_sup * 2 * 4 + (size_t)B.cap_sbin * 4 + (size_t)B.cap_bin * 6 * 8 + (size_t)B.cap_sorted * 2 * 8 +
+           (size_t)B.cap_sup * 2 * (4 + 8) + (size_t)B.cap_sbin * 4 + (size_t)B.cap_bin * 6 * 8 + (size_t)B.cap_sorted * 2 * 8 +
            8 * 64;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
@@ -1705,6 +1875,9 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.flat_pbox2 = (unsigned long long *)p; p += (size_t)B.cap_bin * 8;
     B.sup_pool = (int *)p;                  p += (size_t)B.cap_sup * 4;
     B.sup_flat = (int *)p;                  p += (size_t)B.cap_sup * 4;
+    align();
+    B.sup_pbox_pool = (unsigned long long *)p; p += (size_t)B.cap_sup * 8;
+    B.sup_flat_pbox = (unsigned long long *)p; p += (size_t)B.cap_sup * 8;
     B.sbin_pool = (int *)p;
 }
 
@@ -1745,7 +1918,8 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const bool flags_fit = lat || 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, B.sups_x * B.sups_y), dim3(256), 0, st, F, d_tc, B);
+    hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, B.sups_x * B.sups_y), dim3(256), 0, st, F, d_tc, d_tris,
+                       B);
     const int sups = B.sups_x * B.sups_y;
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(sups), dim3(1024), 0, st, B.sup_chunk, nullptr, B.nch, B.sup_pre,
                        B.sup_tot);

@@ -511,6 +511,17 @@ extern "C" int cg_rt_scratch_info(cg_ctx *c, uint64_t *out)
     return CG_OK;
 }
 
+extern "C" int cg_rt_pool_demand(cg_ctx *c, uint64_t *out)
+{
+    if (!c || !out) return CG_E_INVALID;
+    if (c->big_ev_live) {
+        CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
+        big_observe(c, false);
+    }
+    for (int k = 0; k < 4; ++k) out[k] = c->big_last[k];
+    return CG_OK;
+}
+
 extern "C" int cg_rt_set_pool_caps(cg_ctx *c, long long sup, long long bin, long long sbin, long long sorted)
 {
     if (!c || sup < 0 || bin < 0 || sbin < 0 || sorted < 0) return CG_E_INVALID;

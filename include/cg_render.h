@@ -228,6 +228,10 @@ int cg_rt_set_pending_cap(cg_ctx *ctx, int cap);
  * bucketed and shadow lists), out[2] the pools' capacity in entries, out[3]
  * frames that overflowed a pool (rendered correctly through the fallback). */
 int cg_rt_scratch_info(cg_ctx *ctx, uint64_t *out);
+/* Large-scene list demand of the latest frame, per pool (waits for it): out[0]
+ * super-bin lists, out[1] bin lists, out[2] many-light shadow lists, out[3]
+ * bucketed (per half-bin) lists, in entries. */
+int cg_rt_pool_demand(cg_ctx *ctx, uint64_t *out);
 /* Test hook: pin the large-scene pool capacities (entries: super-bin, bin,
  * many-light shadow and bucketed lists; all 0 = automatic sizing).  Lists past a capacity take the fallback over every triangle; the
  * image is the same. */
