@@ -1979,9 +1979,53 @@ bool rt_big_shadow_lists(const RtFrame &F)
     return !rt_big_lattice(F) && 9 * F.n_lights > 64;
 }
 
-// Host build of the scene grid: cubic cells sized for ~2 triangle centroids
-// per cell, each triangle listed in every cell its bounding box touches.
-// Returns false (no grid) when the lists would exceed max_entries.
+// Does the closed triangle v meet the cell box centred at c with half-width
+// hw, widened by eps?  Separating-axis test (the box's 3 axes, the
+// triangle's normal, the 9 edge x axis products) in FP64 on the float
+// vertices; the widening and the 1e-9 relative slack make it a superset of
+// the exact overlap, which is all the certified lit search needs (a triangle
+// is listed in every cell holding a point of it).
+static bool tri_meets_cell(const double v[3][3], const double c[3], double hw, double eps)
+{
+    const double h = hw + eps;
+    double p[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) p[i][k] = v[i][k] - c[k];
+    auto beyond = [](double a, double b, double d, double r) {   // [min, max] of a, b, d misses [-r, r]
+        return std::min(a, std::min(b, d)) > r || std::max(a, std::max(b, d)) < -r;
+    };
+    for (int k = 0; k < 3; ++k)
+        if (beyond(p[0][k], p[1][k], p[2][k], h)) return false;
+    double e[3][3];
+    for (int k = 0; k < 3; ++k) {
+        e[0][k] = p[1][k] - p[0][k];
+        e[1][k] = p[2][k] - p[1][k];
+        e[2][k] = p[0][k] - p[2][k];
+    }
+    const double n[3] = {e[0][1] * e[1][2] - e[0][2] * e[1][1], e[0][2] * e[1][0] - e[0][0] * e[1][2],
+                         e[0][0] * e[1][1] - e[0][1] * e[1][0]};
+    const double nd = n[0] * p[0][0] + n[1] * p[0][1] + n[2] * p[0][2];
+    if (std::fabs(nd) > h * (std::fabs(n[0]) + std::fabs(n[1]) + std::fabs(n[2])) * (1.0 + 1e-9)) return false;
+    for (int a = 0; a < 3; ++a)
+        for (int j = 0; j < 3; ++j) {
+            double ax[3] = {0.0, 0.0, 0.0};   // unit axis a x edge j
+            const int b = (a + 1) % 3, d = (a + 2) % 3;
+            ax[b] = -e[j][d];
+            ax[d] = e[j][b];
+            const double q0 = ax[0] * p[0][0] + ax[1] * p[0][1] + ax[2] * p[0][2];
+            const double q1 = ax[0] * p[1][0] + ax[1] * p[1][1] + ax[2] * p[1][2];
+            const double q2 = ax[0] * p[2][0] + ax[1] * p[2][1] + ax[2] * p[2][2];
+            if (beyond(q0, q1, q2, h * (std::fabs(ax[0]) + std::fabs(ax[1]) + std::fabs(ax[2])) * (1.0 + 1e-9)))
+                return false;
+        }
+    return true;
+}
+
+// Host build of the scene grid: cubic cells sized for ~1/4 triangle centroid
+// per cell, each triangle listed in every cell it meets (tri_meets_cell over
+// the cells of its bounding box).  Against cells twice as wide listing whole
+// bounding boxes, C5's shadow rays test ~2.8x fewer triangles per unit
+// length.  Returns false (no grid) when the lists would exceed max_entries.
 bool rt_grid_build(const cg_tri *t, int n, RtGrid &g, std::vector<int> &start, std::vector<int> &tris,
                    size_t max_entries)
 {
@@ -2008,7 +2052,7 @@ bool rt_grid_build(const cg_tri *t, int n, RtGrid &g, std::vector<int> &start, s
         ext[a] = (double)hi[a] - lo[a];
         vol *= ext[a];
     }
-    double h = std::cbrt(vol / std::max(1.0, n / 2.0));
+    double h = 0.5 * std::cbrt(vol / std::max(1.0, n / 2.0));
     for (int a = 0; a < 3; ++a) h = std::max(h, ext[a] / 512.0);
     for (int a = 0; a < 3; ++a) {
         g.lo[a] = lo[a];
@@ -2017,36 +2061,36 @@ bool rt_grid_build(const cg_tri *t, int n, RtGrid &g, std::vector<int> &start, s
     g.h = (float)h;
     g.inv_h = (float)(1.0 / h);
     const size_t cells = (size_t)g.res[0] * g.res[1] * g.res[2];
-    auto range = [&](const cg_tri &q, int c0[3], int c1[3]) {
-        float mn[3], mx[3];
-        bb(q, mn, mx);
-        for (int a = 0; a < 3; ++a) {
-            c0[a] = std::min(std::max((int)std::floor((mn[a] - g.lo[a]) * g.inv_h), 0), g.res[a] - 1);
-            c1[a] = std::min(std::max((int)std::floor((mx[a] - g.lo[a]) * g.inv_h), 0), g.res[a] - 1);
-        }
-    };
-    std::vector<int> count(cells + 1, 0);
-    size_t total = 0;
+    const double gh = g.h, hw = 0.5 * gh, eps = 1e-4 * gh;
+    // (cell, triangle) pairs in triangle order, then a counting sort by cell
+    std::vector<std::pair<unsigned, int>> pairs;
+    pairs.reserve((size_t)n * 8);
     for (int i = 0; i < n; ++i) {
+        float mn[3], mx[3];
+        bb(t[i], mn, mx);
         int c0[3], c1[3];
-        range(t[i], c0, c1);
-        total += (size_t)(c1[0] - c0[0] + 1) * (c1[1] - c0[1] + 1) * (c1[2] - c0[2] + 1);
-        if (total > max_entries) return false;
+        for (int a = 0; a < 3; ++a) {   // the cells whose widened box meets the bounding box
+            c0[a] = std::min(std::max((int)std::floor(((double)mn[a] - g.lo[a] - 2.0 * eps) / gh), 0), g.res[a] - 1);
+            c1[a] = std::min(std::max((int)std::floor(((double)mx[a] - g.lo[a] + 2.0 * eps) / gh), 0), g.res[a] - 1);
+        }
+        const double v[3][3] = {{t[i].v0.x, t[i].v0.y, t[i].v0.z}, {t[i].v1.x, t[i].v1.y, t[i].v1.z},
+                                {t[i].v2.x, t[i].v2.y, t[i].v2.z}};
         for (int z = c0[2]; z <= c1[2]; ++z)
             for (int y = c0[1]; y <= c1[1]; ++y)
-                for (int x = c0[0]; x <= c1[0]; ++x) ++count[((size_t)z * g.res[1] + y) * g.res[0] + x];
+                for (int x = c0[0]; x <= c1[0]; ++x) {
+                    const double c[3] = {(double)g.lo[0] + (x + 0.5) * gh, (double)g.lo[1] + (y + 0.5) * gh,
+                                         (double)g.lo[2] + (z + 0.5) * gh};
+                    if (!tri_meets_cell(v, c, hw, eps)) continue;
+                    if (pairs.size() >= max_entries) return false;
+                    pairs.emplace_back((unsigned)(((size_t)z * g.res[1] + y) * g.res[0] + x), i);
+                }
     }
     start.assign(cells + 1, 0);
-    for (size_t c = 0; c < cells; ++c) start[c + 1] = start[c] + count[c];
-    tris.assign(total, 0);
+    for (const auto &pr : pairs) ++start[pr.first + 1];
+    for (size_t c = 0; c < cells; ++c) start[c + 1] += start[c];
+    tris.assign(pairs.size(), 0);
     std::vector<int> fill(start.begin(), start.end() - 1);
-    for (int i = 0; i < n; ++i) {
-        int c0[3], c1[3];
-        range(t[i], c0, c1);
-        for (int z = c0[2]; z <= c1[2]; ++z)
-            for (int y = c0[1]; y <= c1[1]; ++y)
-                for (int x = c0[0]; x <= c1[0]; ++x) tris[fill[((size_t)z * g.res[1] + y) * g.res[0] + x]++] = i;
-    }
+    for (const auto &pr : pairs) tris[fill[pr.first]++] = pr.second;
     return true;
 }
 
