@@ -360,19 +360,6 @@ __global__ __launch_bounds__(1024) void rt_list_base_kernel(const int *__restric
     }
 }
 
-// The super lists' chunks copied into one contiguous array per super-bin.
-__global__ __launch_bounds__(256) void rt_sup_compact_kernel(BigBufs B)
-{
-    const int sup = blockIdx.y, c = blockIdx.x;
-    if (B.sup_over[sup]) return;
-    const Chunk ch = B.sup_chunk[(size_t)sup * B.nch + c];
-    const size_t at = (size_t)B.sup_base[sup] + B.sup_pre[(size_t)sup * B.nch + c];
-    for (int e = (int)threadIdx.x; e < ch.n; e += 256) {
-        B.sup_flat[at + e] = B.sup_pool[ch.off + e];
-        B.sup_flat_pbox[at + e] = B.sup_pbox_pool[ch.off + e];
-    }
-}
-
 // Append the kept triangles of this workgroup to a plain list (one atomic per
 // workgroup); kept[r] is this thread's verdict on triangle base + r*256 + tid.
 __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *list, int *count)
@@ -480,6 +467,86 @@ __device__ __forceinline__ double det_abs_max(const RtTri &c, float x0, float x1
     return fmax(fabs(lo), fabs(hi)) * (1.0 + 1e-12);
 }
 
+// A super-list entry without a box (det's sign uncertain over the super-bin:
+// a plane its rays graze, typically a triangle seen nearly edge-on somewhere
+// along that line) carries instead the mask of the super-bin's 16 bins whose
+// own certificate keeps it: low word kMaskTag (x0 = 32767 > x1 = 32766:
+// neither a real box nor kProjNone), high word the mask (bit bx + 4 by).
+constexpr unsigned kMaskTag = 0x7ffe7fffu;
+__device__ __forceinline__ bool is_bin_mask(unsigned long long b) { return (unsigned)b == kMaskTag; }
+
+// cull_primary's certificate of one triangle over nb <= 64 bundles bb[k] =
+// (x0, x1, y0, y1; x0 > x1 for none) lying in the bundle [ex0, ex1] x [ey0,
+// ey1]: bit k set when bundle k keeps it.  The linear forms are formed once
+// and the error bounds taken over the enclosing bundle (its |d| maxima bound
+// every inner bundle's, and 2e-12 max |form| over it bounds the 1e-12 (|lo| +
+// |hi|) rounding term of any inner one); every test of the certificate only
+// gets harder as the error bounds grow, so each cleared bit is a bundle the
+// exact certificate culls too.  Branch-free per bundle.
+__device__ unsigned long long bundle_mask(const RtTri &c, const float (*bb)[4], int nb, float ex0, float ex1,
+                                          float ey0, float ey1, float f)
+{
+    const double eps = 5.9604644775390625e-8;   // 2^-24
+    const double g = 16.0 * eps;
+    const vec3 e1 = v3(c.e1x, c.e1y, c.e1z), e2 = v3(c.e2x, c.e2y, c.e2z), s = v3(c.sx, c.sy, c.sz);
+    const double Nx = (double)e1.y * e2.z - (double)e2.y * e1.z, Ny = (double)e1.z * e2.x - (double)e2.z * e1.x,
+                 Nz = (double)e1.x * e2.y - (double)e2.x * e1.y;
+    const double Ax = (double)s.y * e2.z - (double)e2.y * s.z, Ay = (double)s.z * e2.x - (double)e2.z * s.x,
+                 Az = (double)s.x * e2.y - (double)e2.x * s.y;
+    const double Bx = (double)e1.y * s.z - (double)s.y * e1.z, By = (double)e1.z * s.x - (double)s.z * e1.x,
+                 Bz = (double)e1.x * s.y - (double)s.x * e1.y;
+    const double Cx = Ax + Bx - Nx, Cy = Ay + By - Ny, Cz = Az + Bz - Nz;
+    const double fz = f;
+    const double hcx = 0.5 * ((double)ex0 + ex1), hcy = 0.5 * ((double)ey0 + ey1);
+    const double hhx = 0.5 * ((double)ex1 - ex0), hhy = 0.5 * ((double)ey1 - ey0);
+    const double Dx = fmax(fabs((double)ex0), fabs((double)ex1)), Dy = fmax(fabs((double)ey0), fabs((double)ey1)),
+                 Dz = fabs(fz);
+    auto amax = [&](double X, double Y, double Z) {
+        double lo, hi;
+        lin_range(hcx, hcy, hhx, hhy, fz, X, Y, Z, lo, hi);
+        return fmax(fabs(lo), fabs(hi));
+    };
+    const double Ed = g * det3_bound(Dx, Dy, Dz, e1, e2) + 2e-12 * amax(Nx, Ny, Nz);
+    const double Eu = g * det3_bound(Dx, Dy, Dz, s, e2) + 2e-12 * amax(Ax, Ay, Az);
+    const double Ev = g * det3_bound(Dx, Dy, Dz, e1, s) + 2e-12 * amax(Bx, By, Bz);
+    const double Eb = Ed + Eu + Ev + 2e-12 * amax(Cx, Cy, Cz);
+    const double dT = c.detT;
+    if (!isfinite(Ed + Eu + Ev + Eb)) return ~0ull;
+    const double four_eps = 4.0 * eps;
+    unsigned long long mask = 0ull;
+    for (int k = 0; k < nb; ++k) {
+        const float x0 = bb[k][0], x1 = bb[k][1], y0 = bb[k][2], y1 = bb[k][3];
+        const double cx = 0.5 * ((double)x0 + x1), cy = 0.5 * ((double)y0 + y1);
+        const double hx = 0.5 * ((double)x1 - x0), hy = 0.5 * ((double)y1 - y0);
+        double dlo, dhi, ulo, uhi, vlo, vhi, blo, bhi;
+        lin_range(cx, cy, hx, hy, fz, Nx, Ny, Nz, dlo, dhi);
+        lin_range(cx, cy, hx, hy, fz, Ax, Ay, Az, ulo, uhi);
+        lin_range(cx, cy, hx, hy, fz, Bx, By, Bz, vlo, vhi);
+        lin_range(cx, cy, hx, hy, fz, Cx, Cy, Cz, blo, bhi);
+        const bool pos = dlo - Ed > 0, neg = dhi + Ed < 0;
+        // det's sign certain: cull_primary's tests
+        const double dmin = pos ? dlo - Ed : -(dhi + Ed);
+        const double dmax = pos ? dhi + Ed : -(dlo - Ed);
+        const double tiny = 1e-20 * dmax;
+        const double umx = fmax(fabs(ulo), fabs(uhi)) + Eu, vmx = fmax(fabs(vlo), fabs(vhi)) + Ev;
+        const double num = pos ? blo - Eb : -(bhi + Eb);
+        const bool c_sure = (dT != 0.0 && ((dT > 0) != pos) && fabs(dT) > tiny) |
+                            (pos ? (uhi + Eu < -tiny) : (ulo - Eu > tiny)) |
+                            (pos ? (vhi + Ev < -tiny) : (vlo - Ev > tiny)) |
+                            (num > 0.0 && num * dmin > four_eps * (umx + vmx + dmin) * dmax * (1.0 + 0x1p-40));
+        // sign uncertain: sign_free_reject
+        const double dmx = fmax(fabs(dlo - Ed), fabs(dhi + Ed));
+        const double ftiny = 1e-20 * dmx;
+        const double Ew = Eb * (1.0 + four_eps) + four_eps * (umx + vmx + dmx) + ftiny;
+        const bool p_ok = !(dhi + Ed > 0.0) || (uhi + Eu < -ftiny) || (vhi + Ev < -ftiny) || (blo > Ew);
+        const bool n_ok = !(dlo - Ed < 0.0) || (ulo - Eu > ftiny) || (vlo - Ev > ftiny) || (bhi < -Ew);
+        const bool fin = isfinite(dlo) && isfinite(dhi) && isfinite(ulo + uhi + vlo + vhi + blo + bhi);
+        const bool cull = fin & ((pos | neg) ? c_sure : (p_ok & n_ok));
+        mask |= (unsigned long long)(!(x0 > x1) & !cull) << k;
+    }
+    return mask;
+}
+
 // K00: camera-ray certificate per (super-bin, triangle) -> super list; the
 // bins then certify only their super-bin's survivors (a bin's bundle lies in
 // its super-bin's, so a triangle the super-bin culls is culled for the bin).
@@ -512,6 +579,40 @@ __global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const Rt
     }
     pooled_append(kept, base, B.sup_pool, B.pool_n + kPoolSup, B.cap_sup, B.sup_chunk + (size_t)sup * B.nch + blockIdx.x,
                   B.sup_over + sup, pb, B.sup_pbox_pool);
+}
+
+// The super lists' chunks copied into one contiguous array per super-bin.
+// (An entry without a box gets its bin mask here, in a dense pass.)
+__global__ __launch_bounds__(256) void rt_sup_compact_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const int sup = blockIdx.y, c = blockIdx.x;
+    if (B.sup_over[sup]) return;
+    const Chunk ch = B.sup_chunk[(size_t)sup * B.nch + c];
+    if (ch.n == 0) return;
+    const size_t at = (size_t)B.sup_base[sup] + B.sup_pre[(size_t)sup * B.nch + c];
+    __shared__ float s_bb[kSupBins * kSupBins][4];   // the super-bin's bins' bundles
+    const int sx = sup % B.sups_x, sy = sup / B.sups_x;
+    float ex0, ex1, ey0, ey1;
+    const bool sv = sup_bundle(F, sx, sy, ex0, ex1, ey0, ey1);
+    if (threadIdx.x < kSupBins * kSupBins) {
+        const int bx = sx * kSupBins + (int)threadIdx.x % kSupBins, by = sy * kSupBins + (int)threadIdx.x / kSupBins;
+        float *q = s_bb[threadIdx.x];
+        if (!(bx < B.bins_x && by < B.bins_y && bin_bundle(F, bx, by, q[0], q[1], q[2], q[3]))) {
+            q[0] = 1.0f;
+            q[1] = 0.0f;
+        }
+    }
+    __syncthreads();
+    for (int e = (int)threadIdx.x; e < ch.n; e += 256) {
+        const int i = B.sup_pool[ch.off + e];
+        unsigned long long pb = B.sup_pbox_pool[ch.off + e];
+        if (pb == kProjAll && sv) {
+            const unsigned long long m = bundle_mask(tc[i], s_bb, kSupBins * kSupBins, ex0, ex1, ey0, ey1, F.focal);
+            pb = m ? (m << 32) | kMaskTag : kProjNone;
+        }
+        B.sup_flat[at + e] = i;
+        B.sup_flat_pbox[at + e] = pb;
+    }
 }
 
 // K0: camera-ray certificate per (bin, triangle of its super list), with the
@@ -557,7 +658,7 @@ __device__ void bin_certify_batch(const RtFrame &F, const RtTri *__restrict__ tc
             kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
             if (kept[r]) {
                 unsigned long long b = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
-                if (b == kProjAll) b = sb;
+                if (b == kProjAll && !is_bin_mask(sb)) b = sb;
                 kept[r] = proj_meets(b, x0, x1, y0, y1);
                 pbox[r] = b;
                 // the key: t = fl(detT / det_f) and an accepting ray's
@@ -652,6 +753,7 @@ __global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const
     const int ns = all ? F.n_tris : B.sup_tot[sup];
     const int *slist = B.sup_flat + (all ? 0 : B.sup_base[sup]);
     const unsigned long long *sbox = B.sup_flat_pbox + (all ? 0 : B.sup_base[sup]);
+    const int lbin = (bx % kSupBins) + kSupBins * (by % kSupBins);   // its bit in the super-bin's bin masks
     __shared__ int s_q[2 * kBinTris];                     // super-list entries waiting for the certificate
     __shared__ int s_w[4][4];
     int qn = 0;                                           // queued (workgroup-uniform)
@@ -663,7 +765,8 @@ __global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int e = base + r * 256 + (int)threadIdx.x;
-            pass[r] = e < ns && (all || proj_meets(sbox[e], x0, x1, y0, y1));
+            const unsigned long long sb = e < ns && !all ? sbox[e] : kProjAll;
+            pass[r] = e < ns && (is_bin_mask(sb) ? ((sb >> (32 + lbin)) & 1ull) != 0ull : proj_meets(sb, x0, x1, y0, y1));
             m[r] = __ballot(pass[r]);
             if (lane == 0) s_w[r][w] = __popcll(m[r]);
         }
@@ -1924,7 +2027,7 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(sups), dim3(1024), 0, st, B.sup_chunk, nullptr, B.nch, B.sup_pre,
                        B.sup_tot);
     hipLaunchKernelGGL(rt_list_base_kernel, dim3(1), dim3(1024), 0, st, B.sup_tot, sups, B.sup_base);
-    hipLaunchKernelGGL(rt_sup_compact_kernel, dim3(B.nch, sups), dim3(256), 0, st, B);
+    hipLaunchKernelGGL(rt_sup_compact_kernel, dim3(B.nch, sups), dim3(256), 0, st, F, d_tc, B);
     hipLaunchKernelGGL(rt_bin_primary_kernel, dim3(std::min(64, (int)bgrid.x), bins), dim3(256), 0, st, F, d_tc,
                        d_tris, B);
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(bins), dim3(1024), 0, st, B.bin_chunk, B.bin_nch, B.nch, B.bin_pre,
