@@ -1091,6 +1091,9 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     // folding lanes: lane = 24 k + 3 pr + comp (k = 0: the pixel whose first
     // or middle column this is, k = 1: the pixel whose last column it is)
     const int fk = lane / 24, fpr = (lane % 24) / 3, fcomp = lane % 3;
+#ifdef CG_WALK_STATS
+    int st_units = 0, st_cand = 0, st_sph = 0;
+#endif
     for (int h = 0; h * kLatHalfH < G.nv; ++h) {
         const int pr0 = h * kLatHalfH, npr = min(kLatHalfH, G.nv - pr0);
         const int lr0 = 2 * pr0, nlr = 2 * npr + 1, items = nlr * nL;
@@ -1104,6 +1107,11 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                 const int cx = step;
                 const unsigned long long um0 = uniform_u64(s_umask[h][cx]);
                 const unsigned long long um = um0 & ~(1ull << 63);
+#ifdef CG_WALK_STATS
+                st_units += 1;
+                st_cand += __popcll(um);
+                st_sph += (int)(um0 >> 63);
+#endif
                 RtFrame Fu = Fs;                      // spheres only where one may block
                 if (!(um0 >> 63)) Fu.n_sph = 0;
                 const float X = lat_x(F, G, cx);
@@ -1166,6 +1174,10 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             __syncthreads();
         }
     }
+#ifdef CG_WALK_STATS
+    if (threadIdx.x == 0 && blockIdx.z == 0 && blockIdx.x % 24 == 0 && blockIdx.y % 24 == 0)
+        printf("LIGHTS bx %d by %d units %d cand %d sph %d\n", blockIdx.x, blockIdx.y, st_units, st_cand, st_sph);
+#endif
     const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
     uint32_t px = 0u;
     if (tx < G.nu && ty < G.nv) {
