@@ -114,6 +114,7 @@ struct BigBufs {
     unsigned long long *pool_n;   // [4] demand per pool (kPool*; the sorted pool's is its total)
     long long cap_sup, cap_bin, cap_sbin, cap_sorted;  // pool capacities (entries)
     int *sup_over, *bin_over, *sbin_over;              // [n_sups], [n_bins], [n_bins]: list overflowed
+    float *tile_bb;               // [2 n_bins][32][4]: each half-bin's wave-tile bundles (rt_half_mask_kernel)
 };
 
 // ---------------------------------------------------------------------------
@@ -226,6 +227,28 @@ __device__ bool bin_half_bundle(const RtFrame &F, int bx, int by, int part, floa
     const int u0 = bx * kBinW + part * (kBinW / 2), u1 = min(F.W, u0 + kBinW / 2) - 1;
     if (u0 > u1) return false;
     const int L0 = by * kBinH, L1 = min(F.rows_out, L0 + kBinH) - 1;
+    const int v0 = shard_row(F, L0);
+    if (v0 >= F.H) return false;
+    const int v1 = min(shard_row(F, L1), F.H - 1);
+    x0 = y0 = FLT_MAX;
+    x1 = y1 = -FLT_MAX;
+    const int us[2] = {u0, u1}, vs[2] = {v0, v1};
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            vec4 d = mat4_mul(F.R, v4((float)(us[a] - F.W / 2), (float)(vs[b] - F.H / 2), F.focal, 1.0f));
+            x0 = fminf(x0, d.x); x1 = fmaxf(x1, d.x);
+            y0 = fminf(y0, d.y); y1 = fmaxf(y1, d.y);
+        }
+    x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
+    return true;
+}
+
+// The same for the 8x8-pixel wave tile (tx, ty); false without pixels.
+__device__ bool tile_bundle(const RtFrame &F, int tx, int ty, float &x0, float &x1, float &y0, float &y1)
+{
+    const int u0 = tx * 8, u1 = min(F.W, u0 + 8) - 1;
+    const int L0 = ty * 8, L1 = min(F.rows_out, L0 + 8) - 1;
+    if (u0 > u1 || L0 > L1) return false;
     const int v0 = shard_row(F, L0);
     if (v0 >= F.H) return false;
     const int v1 = min(shard_row(F, L1), F.H - 1);
@@ -473,6 +496,7 @@ __device__ __forceinline__ double det_abs_max(const RtTri &c, float x0, float x1
 // own certificate keeps it: low word kMaskTag (x0 = 32767 > x1 = 32766:
 // neither a real box nor kProjNone), high word the mask (bit bx + 4 by).
 constexpr unsigned kMaskTag = 0x7ffe7fffu;
+constexpr unsigned kNeedTag = 0x7ffd7fffu;   // a bucketed entry waiting for its tile mask (high word: half-bin)
 __device__ __forceinline__ bool is_bin_mask(unsigned long long b) { return (unsigned)b == kMaskTag; }
 
 // cull_primary's certificate of one triangle over nb <= 64 bundles bb[k] =
@@ -987,9 +1011,53 @@ __global__ __launch_bounds__(256) void rt_bin_scatter_kernel(RtFrame F, BigBufs 
                 if (loc[r][h] >= 0) {
                     const size_t at = (size_t)s_base[h][bk[r]] + loc[r][h];
                     B.bin_sorted[at] = ent[r];
-                    B.bin_spbox[at] = pb[r][h];
+                    // a box-less entry: its half-bin, for rt_half_mask_kernel
+                    B.bin_spbox[at] = pb[r][h] == kProjAll ? ((unsigned long long)(2 * bin + h) << 32) | kNeedTag : pb[r][h];
                 }
         __syncthreads();                                    // s_cnt / s_base reused by the next chunk
+    }
+}
+
+// Tile masks for the bucketed half-bin entries without a box (det's sign
+// uncertain over the half: mostly triangles seen nearly edge-on far along
+// their plane's horizon, which every wave of the half would otherwise
+// certify and cull): the mask of the half's 32 wave tiles (8 x 4, bit c +
+// 8 r) whose certificate keeps the triangle (bundle_mask), in place of the
+// box; the walk tests its tile's bit.  One flat pass over the bucketed pool
+// (the scatter tagged those entries with their half-bin), the tile bundles
+// from a table.
+__global__ __launch_bounds__(64) void rt_half_tiles_kernel(RtFrame F, BigBufs B)
+{
+    const int sub = blockIdx.x, bin = sub >> 1, h = sub & 1, t = threadIdx.x;
+    if (t >= 32) return;
+    const int tx = (bin % B.bins_x) * kBinTilesX + h * (kBinTilesX / 2) + (t & 7);
+    const int ty = (bin / B.bins_x) * kBinTilesY + (t >> 3);
+    float *q = B.tile_bb + ((size_t)sub * 32 + t) * 4;
+    float x0, x1, y0, y1;
+    if (!tile_bundle(F, tx, ty, x0, x1, y0, y1)) {
+        x0 = 1.0f;
+        x1 = 0.0f;
+        y0 = y1 = 0.0f;
+    }
+    *(float4 *)q = make_float4(x0, x1, y0, y1);
+}
+
+__global__ __launch_bounds__(256) void rt_half_mask_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+{
+    const long long total = (long long)min((unsigned long long)B.pool_n[kPoolSorted], (unsigned long long)B.cap_sorted);
+    for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
+        const unsigned long long pb = B.bin_spbox[p];
+        if ((unsigned)pb != kNeedTag) continue;
+        // (entries of an overflowed bin may be another frame's: never walked, skipped here)
+        const int sub = (int)(pb >> 32), bin = sub >> 1;
+        if (sub < 0 || sub >= 2 * B.bins_x * B.bins_y || B.bin_over[bin]) continue;
+        float hx0, hx1, hy0, hy1;
+        if (!bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, sub & 1, hx0, hx1, hy0, hy1)) continue;
+        const int i = (int)(unsigned)(B.bin_sorted[p] & 0xffffffffull);
+        if (i < 0 || i >= F.n_tris) continue;
+        const unsigned long long mk = bundle_mask(tc[i], (const float(*)[4])(B.tile_bb + (size_t)sub * 128), 32, hx0,
+                                                  hx1, hy0, hy1, F.focal);
+        B.bin_spbox[p] = mk ? (mk << 32) | kMaskTag : kProjNone;
     }
 }
 
@@ -1095,6 +1163,7 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
     const bool any = x0 <= x1;
     const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
     const int sub = 2 * bin + ((tx % kBinTilesX) < kBinTilesX / 2 ? 0 : 1);          // the wave's half-bin
+    const int tbit = 32 + (tx % (kBinTilesX / 2)) + (kBinTilesX / 2) * (ty % kBinTilesY);   // its tile-mask bit
     const unsigned long long *list = B.bin_sorted;   // global offsets (rt_bin_scan_kernel)
     const unsigned long long *pboxes = B.bin_spbox;
     const int *boff = B.bkt_off + sub * (kDepthBuckets + 1);
@@ -1168,14 +1237,15 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
             ent_n = cn < b1 ? list[cn] : 0ull;
             pb_n = cn < b1 ? pboxes[cn] : 0ull;
             // projected box first (no gather), then the key
-            const bool pass = in && proj_meets(pb, x0, x1, y0, y1) && !(__uint_as_float((unsigned)(ent >> 32)) > tb);
+            const bool pass = in && (is_bin_mask(pb) ? ((pb >> tbit) & 1ull) != 0ull : proj_meets(pb, x0, x1, y0, y1)) &&
+                              !(__uint_as_float((unsigned)(ent >> 32)) > tb);
             const unsigned long long pm = __ballot(pass);
             if (pass) q_w[qn + __popcll(pm & ((1ull << lane) - 1ull))] = (int)(unsigned)(ent & 0xffffffffull);
             qn += __popcll(pm);
 #ifdef CG_WALK_STATS
             ++st_chunks;
             st_pass += __popcll(pm);
-            st_all += __popcll(__ballot(in && pb == kProjAll));
+            st_all += __popcll(__ballot(in && is_bin_mask(pb)));
             st_wide += __popcll(__ballot(in && pb != kProjAll &&
                                          (short)((pb >> 16) & 0xffff) - (short)(pb & 0xffff) > 40));
 #endif
@@ -1921,7 +1991,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
 {
     const size_t bins = (size_t)B.bins_x * B.bins_y, sups = (size_t)B.sups_x * B.sups_y;
     const size_t tiles = (size_t)B.tiles_x * B.tiles_y;
-    return big_counter_bytes(B) + 2 * bins * (kDepthBuckets + 1) * 4 + (tiles + bins) * sizeof(ShadowBox) +
+    return big_counter_bytes(B) + 2 * bins * (kDepthBuckets + 1) * 4 + 2 * bins * 32 * 16 + (tiles + bins) * sizeof(ShadowBox) +
            big_slots(B, F) * 8 + 2 * big_words(B, F) * 8 + (size_t)kMaxPend * sizeof(PendRay) +
            (size_t)F.n_tris * 4 + (sups + 2 * bins) * B.nch * sizeof(Chunk) + (sups + bins) * (B.nch + 2) * 4 +
            (size_t)B.cap_sup * 2 * (4 + 8) + (size_t)B.cap_sbin * 4 + (size_t)B.cap_bin * 6 * 8 + (size_t)B.cap_sorted * 2 * 8 +
@@ -1946,6 +2016,8 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     B.bin_over = (int *)p;          p += bins * 4;
     B.sbin_over = (int *)p;         p += bins * 4;
     B.bkt_off = (int *)p;           p += 2 * bins * (kDepthBuckets + 1) * 4;
+    align();
+    B.tile_bb = (float *)p;         p += 2 * bins * 32 * 16;
     align();
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
@@ -2045,7 +2117,9 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         return c != hipSuccess ? c : hipGetLastError();
     };
     if (dry == 1) return demand();
+    hipLaunchKernelGGL(rt_half_tiles_kernel, dim3(2 * bins), dim3(64), 0, st, F, B);
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
+    hipLaunchKernelGGL(rt_half_mask_kernel, dim3(2048), dim3(256), 0, st, F, d_tc, B);
     if (lat && B.lat_yaw)
         hipLaunchKernelGGL(rt_big_primary_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     else if (lat)
