@@ -711,16 +711,26 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     c->slot ^= 1;
     DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k], &bum = c->pumask[k];
     const size_t tiles = rt_lattice_tiles(F);
-    CG_TRY(c, blat.ensure((size_t)nf * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
-    CG_TRY(c, btc.ensure((size_t)nf * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
-    CG_TRY(c, bsh.ensure((size_t)std::max(F.n_tris, 1) * sizeof(RtShade)), "alloc tri shading");
+    // Both slots' certificate buffers are sized together, for a full batch
+    // (kMaxFrameBatch frames; the unit masks, large at 4K, for this call's
+    // frames): a call never allocates -- hipMalloc / hipFree, the latter a
+    // device-wide wait -- in front of its kernels merely because it batches
+    // more frames than the previous one or is the first on its slot.
+    const size_t nfa = std::max(nf, kMaxFrameBatch);
+    for (int q = 0; q < 2; ++q) {
+        CG_TRY(c, c->plat[q].ensure(nfa * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
+        CG_TRY(c, c->ptc[q].ensure(nfa * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
+        CG_TRY(c, c->pshade[q].ensure((size_t)std::max(F.n_tris, 1) * sizeof(RtShade)), "alloc tri shading");
+        CG_TRY(c, c->psup[q].ensure(nfa * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
+        if (rt_lattice_unit_bytes(F, nf))
+            CG_TRY(c, c->pumask[q].ensure(rt_lattice_unit_bytes(F, nf)), "alloc lattice unit masks");
+    }
     RtFrameCams fc{};
     for (int f = 0; f < nf; ++f) {
         fc.c[f][0] = cams[f].camera.x; fc.c[f][1] = cams[f].camera.y;
         fc.c[f][2] = cams[f].camera.z; fc.c[f][3] = cams[f].camera.w;
     }
     unsigned long long *lat = (unsigned long long *)blat.p;
-    CG_TRY(c, bsup.ensure((size_t)nf * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
     unsigned long long *supm = (unsigned long long *)bsup.p;
     // certificates on aux, after the slot's previous reader, so that they run
     // beside the lattice launch still queued before them.  A cold call (every
@@ -736,7 +746,6 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     // light sets: the per-unit shadow certificates, with the other certificates
     unsigned long long *um = nullptr;
     if (rt_lattice_unit_bytes(F, nf)) {
-        CG_TRY(c, bum.ensure(rt_lattice_unit_bytes(F, nf)), "alloc lattice unit masks");
         um = (unsigned long long *)bum.p;
         CG_TRY(c, launch_rt_lattice_units(F, (const RtTri *)btc.p, (const RtShade *)bsh.p, (const RtSphere *)c->sph.p,
                                           lat, fc, nf, um, cst),
