@@ -111,6 +111,12 @@ struct cg_ctx {
     unsigned long long big_last[4] = {};
     long long big_overflows = 0;
     std::vector<cg_tri> tris_host;      // the scene as uploaded (cg_dist's column window)
+    // the latest camera's column window over tris_host (a pass over the whole
+    // scene on the host: 1M triangles take ~6 ms), reused while camera and scene
+    // stay the same -- cg_dist asks for every frame of every call
+    mutable cg_rt_camera col_cam{};
+    mutable int col_c0 = 0, col_c1 = 0;
+    mutable bool col_valid = false;
     std::vector<cg_sphere> sph_host;
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
@@ -141,6 +147,11 @@ void ctx_set_error(cg_ctx *c, const std::string &e) { c->err = e; }
 // cg_rt_frame_columns over the context's scene (the full width without one)
 void ctx_rt_columns(const cg_ctx *c, const cg_rt_camera *cam, int *c0, int *c1)
 {
+    if (c->col_valid && std::memcmp(&c->col_cam, cam, sizeof(*cam)) == 0) {
+        *c0 = c->col_c0;
+        *c1 = c->col_c1;
+        return;
+    }
     *c0 = 0;
     *c1 = cam->width;
     if (c->n_tris < 0 || cg_rt_frame_columns(c->tris_host.data(), (int)c->tris_host.size(), c->sph_host.data(),
@@ -148,6 +159,10 @@ void ctx_rt_columns(const cg_ctx *c, const cg_rt_camera *cam, int *c0, int *c1)
         *c0 = 0;
         *c1 = cam->width;
     }
+    c->col_cam = *cam;
+    c->col_c0 = *c0;
+    c->col_c1 = *c1;
+    c->col_valid = true;
 }
 // exposed to cg_rast.hip
 void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
@@ -319,6 +334,7 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
                                  hipMemcpyHostToDevice, c->stream), "upload spheres");
     c->tris_host.assign(tris, tris + n_tris);
     c->sph_host.assign(spheres, spheres + n_spheres);
+    c->col_valid = false;   // a new scene: column windows again
     c->grid = RtGrid{};
     c->big_sized = false;   // the next large-scene frame sizes the pools
     if (n_tris > 64) {   // large scene: grid for the shadow-ray blocker search
