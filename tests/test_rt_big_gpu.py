@@ -8,6 +8,10 @@ has, against the live oracle's whole frame, bit-exact (tolerance 0):
 * per-pixel mode: a pitched camera (R turns y: no lattice) with one light, and
   the many-light path (certified per-bin shadow lists) for 16 lights under the
   pitch and for 81 lights (more than a lattice word holds);
+* the camera inside the cloud (triangles behind the eye, one straddling the
+  eye plane around the eye, and one with a vertex exactly on it: the culling
+  projections' unbounded and singular cases), unrotated, yawed and pitched,
+  and over 2 x 2 super-bins;
 * each also with the pools pinned far too small (every list overflows: the
   consumers' fallback over all triangles) and with a one-entry pending queue
   (the shading kernel's per-lane lit search)."""
@@ -36,6 +40,11 @@ def _pitch(a):
 
 
 PITCH = _pitch(0.15)
+# random_scene(500, 0x5EED)'s first triangle has z in [0.0299, 0.0467] around
+# (x, y) = (-0.2249, 0.1385): an eye at z 0.04 sits inside its span; EYE_V0 puts
+# the eye plane exactly through its vertex v0 (z 0.029914677, a float)
+EYE_IN = [-0.2249, 0.1385, 0.04, 1.0]
+EYE_V0 = [-0.2249, 0.1385, float(np.float32(0.029914677)), 1.0]
 CASES = {
     "lat_1": dict(R=None, lights=[L0]),
     "lat_area16": dict(R=None, lights=[L0], area=dict(side=0.1, n=4)),
@@ -44,11 +53,18 @@ CASES = {
     "pix_pitch_1": dict(R=PITCH, lights=[L0]),
     "pix_pitch_area16": dict(R=PITCH, lights=[L0], area=dict(side=0.1, n=4)),
     "pix_area81": dict(R=None, lights=[L0], area=dict(side=0.1, n=9)),
+    "inside_lat_1": dict(R=None, lights=[L0], cam=EYE_IN),
+    "inside_yawlat_area16": dict(R=YAW, lights=[L0], area=dict(side=0.1, n=4), cam=EYE_IN),
+    "inside_pix_pitch_1": dict(R=PITCH, lights=[L0], cam=EYE_IN),
+    "vertex_plane_lat_1": dict(R=None, lights=[L0], cam=EYE_V0),
+    "vertex_plane_yawlat_1": dict(R=YAW, lights=[L0], cam=EYE_V0),
+    # 2 x 2 super-bins (512 x 128 pixels each) around the eye
+    "inside_lat_wide": dict(R=None, lights=[L0], cam=EYE_IN, width=640, height=160, focal=160.0),
 }
 
 
 def _cfg(case):
-    return dict(width=64, height=48, focal=48.0, cam=[0, 0, -3.0, 1], scene=SCENE, **CASES[case])
+    return dict(dict(width=64, height=48, focal=48.0, cam=[0, 0, -3.0, 1], scene=SCENE), **CASES[case])
 
 
 _REF = {}
