@@ -124,3 +124,53 @@ def test_big_scene_modes_match_oracle(big, case, stress):
         assert info["overflows"] >= 1, info
     elif stress == "sized":
         assert info["overflows"] == 0 and info["capacity"] <= 2 * info["listed"] + 5 * 4096, info
+
+
+def _degenerate_scene(n=500, around_eye=False):
+    """random_scene(n) with edge-case triangles written over its first ones:
+    a point, two collinear forms, a repeated vertex, a sliver, a 10 x 10
+    backdrop behind the cloud (every bin lists it, every pixel can hit it), a
+    triangle in the eye's plane z = -3 beside the eye (or around it: every
+    camera ray meets it at its origin) and one behind the eye.
+    Normals as ComputeNormal makes them (NaN for the zero-area ones, which no
+    ray can hit: their determinant is 0)."""
+    a = np.frombuffer(bytes(cgamd.random_scene(n, 0x5EED)), np.float32).reshape(n, 19).copy()
+    v = lambda k: a[k, 0:12].reshape(3, 4)                               # noqa: E731
+    p = v(1)[0].copy()
+    v(1)[1], v(1)[2] = p, p                                              # a point
+    v(2)[2, :3] = v(2)[0, :3] + np.float32(2) * (v(2)[1, :3] - v(2)[0, :3])   # collinear (float)
+    v(3)[2, :3] = v(3)[0, :3] + np.float32(0.5) * (v(3)[1, :3] - v(3)[0, :3])
+    v(4)[1] = v(4)[0]                                                    # repeated vertex
+    v(5)[2, :3] = v(5)[1, :3] + np.float32(1e-6)                         # sliver
+    v(6)[:, :3] = [[-5, -5, 1.5], [5, -5, 1.5], [0, 5, 1.5]]             # backdrop
+    v(7)[:, :3] = [[-1, -1, -3], [1, -1, -3], [0, 1, -3]] if around_eye else \
+        [[0.5, -1, -3], [2, -1, -3], [1, 1, -3]]                          # in the eye plane
+    v(8)[:, :3] = [[-1, -1, -4], [1, -1, -4], [0, 1, -4]]                # behind the eye
+    with np.errstate(invalid="ignore", divide="ignore"):
+        for k in range(1, 9):
+            t = v(k)
+            e1, e2 = t[1, :3] - t[0, :3], t[2, :3] - t[0, :3]
+            c = np.cross(e2, e1).astype(np.float32)
+            a[k, 12:15] = c / np.float32(np.sqrt(np.float32((c * c).sum())))
+            a[k, 15] = 1.0
+    raw = a.tobytes()
+    return (cgamd.Tri * n).from_buffer_copy(raw), (oracle.RtTri * n).from_buffer_copy(raw)
+
+
+@pytest.mark.parametrize("case,around_eye", [("lat_1", False), ("yawlat_area16", False), ("pix_pitch_1", False),
+                                             ("pix_area81", False), ("inside_lat_wide", False), ("lat_1", True),
+                                             ("pix_pitch_1", True)])
+@pytest.mark.parametrize("n", [40, 500])      # 40: the small-scene kernels (n_tris <= 64)
+def test_big_scene_degenerate_triangles(ctx, case, around_eye, n):
+    gtris, otris = _degenerate_scene(n, around_eye)
+    cfg = _cfg(case)
+    try:
+        ctx.rt_set_scene(gtris, n, None, 0)
+        argb = _render(ctx, cfg)
+    finally:
+        tris, n1, sph = cgamd.rt_scene()
+        ctx.rt_set_scene(tris, n1, sph, 1)
+    ref = oracle.rt_draw(mg.rt_params_of(cfg), scene=(otris, n, None, 0), threads=min(16, os.cpu_count() or 8))
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"{case}: {bad.size} pixels differ, first {bad[:6]}: gpu {argb[bad[:3]]} ref {ref[bad[:3]]}"
+    assert (ref != 0x80000000).sum() > ref.size // 2                      # the backdrop fills the frame
