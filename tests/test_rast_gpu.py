@@ -101,3 +101,39 @@ def test_rast_draw_frames_device_overlapped(ctx):
         assert np.array_equal(S[o:o + npx], rs), f"frame {k} shadow"
     with pytest.raises(RuntimeError):
         ctx.rast_draw_frames_device([cgamd.rast_params(W, H, F, colour_mode=1)], a.data_ptr())
+
+
+_f = lambda x: float(np.float32(x))   # noqa: E731
+# Camera and light poses the golden configs do not reach (TestModelH boxes: the
+# short one spans x [-0.05, 0.70], y [0.41, 1], z [-0.77, -0.02]; the tall one
+# x [-0.70, 0.05], y [-0.19, 1], z [-0.11, 0.64]): the eye inside a box, the
+# light inside a box (every shadow volume cast from inside), looking away from
+# the room, the eye behind the back wall, the eye and the light on a wall's
+# plane, the light outside the room.
+POSES = {
+    "eye_in_short_box": dict(cam=(_f(0.33), _f(0.7), _f(-0.4), 1.0)),
+    "eye_light_in_tall_box": dict(cam=(_f(-0.33), _f(0.4), _f(0.27), 1.0), light=(_f(-0.3), _f(0.2), _f(0.3), 1.0)),
+    "light_in_short_box": dict(light=(_f(0.33), _f(0.7), _f(-0.4), 1.0)),
+    "looking_back": dict(cam=(0.0, 0.0, _f(-0.5), 1.0), yaw=_f(3.14159)),
+    "behind_back_wall": dict(cam=(0.0, 0.0, _f(1.5), 1.0)),
+    "eye_on_left_wall": dict(cam=(-1.0, 0.0, _f(-0.5), 1.0)),
+    "light_on_right_wall": dict(light=(1.0, 0.0, 0.0, 1.0)),
+    "light_outside_front": dict(light=(0.0, _f(-0.5), -2.0, 1.0)),
+}
+
+
+@pytest.mark.parametrize("pose", list(POSES))
+def test_rast_edge_poses_vs_live_oracle(ctx, pose):
+    """Both Draw entry points (host geometry + device fill, whole Draw on the
+    device) against the oracle's Draw for the pose, all three planes bit-exact."""
+    c = dict(dict(cam=(0.0, 0.0, _f(-3.001), 1.0), light=(0.0, _f(-0.5), 0.0, 1.0), yaw=0.0), **POSES[pose])
+    W, H, F = 160, 120, 90.0
+    R = mg.yaw_R(np.float32(0.0) - np.float32(c["yaw"])) if c["yaw"] else None
+    ra, rd, rs = oracle.rast_draw(oracle.rast_params(W, H, F, c["cam"], R, light=c["light"], yaw=c["yaw"]))
+    p = cgamd.rast_params(W, H, F, c["cam"], (C.c_float * 16)(*R) if R else None, c["light"], yaw=c["yaw"])
+    tris, n, light = cgamd.rast_prepare(p)
+    ctx.rast_set_scene()
+    for how, (a, d, s) in (("render", ctx.rast_render(tris, n, p, light)[:3]), ("draw", ctx.rast_draw(p)[:3])):
+        for nm, x, y in (("shadow", s, rs), ("depth", d.view(np.uint32), rd.view(np.uint32)), ("argb", a, ra)):
+            bad = np.flatnonzero(x != y)
+            assert bad.size == 0, f"{pose}/{how} {nm}: {bad.size} differ, first {bad[:6]} gpu {x[bad[:3]]} ref {y[bad[:3]]}"
