@@ -530,3 +530,38 @@ def test_rt_empty_scene_is_black(ctx):
 def test_rt_errors(ctx):
     with pytest.raises(RuntimeError):
         ctx.rt_render(cgamd.rt_camera(0, 10))
+
+
+_f = lambda x: float(np.float32(x))   # noqa: E731
+_W = [14.0, 14.0, 14.0]
+# Eye and light poses the golden configs do not reach (the sphere: centre
+# (-0.45, 0.6, -0.6), radius 0.3; the short box spans x [-0.05, 0.70],
+# y [0.41, 1], z [-0.77, -0.02]): the eye at and off the sphere's centre, the
+# light inside the sphere or a box, looking away from the room, the eye behind
+# the back wall, the eye and the light on a wall's plane, the light outside.
+RT_POSES = {
+    "eye_at_sphere_centre": dict(cam=[_f(-0.45), _f(0.6), _f(-0.6), 1]),
+    "eye_in_sphere_yawed": dict(cam=[_f(-0.4), _f(0.55), _f(-0.65), 1], yaw=_f(0.5)),
+    "light_in_sphere": dict(lights=[[[_f(-0.45), _f(0.6), _f(-0.6), 1.0], _W]]),
+    "light_in_short_box_area16": dict(lights=[[[_f(0.33), _f(0.7), _f(-0.4), 1.0], _W]], area=dict(side=0.1, n=4)),
+    "eye_in_short_box": dict(cam=[_f(0.33), _f(0.7), _f(-0.4), 1]),
+    "looking_back": dict(cam=[0, 0, _f(-0.5), 1], yaw=_f(3.14159)),
+    "behind_back_wall": dict(cam=[0, 0, _f(1.5), 1]),
+    "eye_on_left_wall": dict(cam=[-1.0, 0, _f(-0.5), 1]),
+    "light_on_right_wall": dict(lights=[[[1.0, 0.0, 0.0, 1.0], _W]]),
+    "light_outside_front_area16": dict(lights=[[[0.0, _f(-0.5), -2.0, 1.0], _W]], area=dict(side=0.1, n=4)),
+}
+
+
+@pytest.mark.parametrize("pose", list(RT_POSES))
+def test_rt_edge_poses_vs_live_oracle(rt, pose):
+    """The Cornell-box frame (lattice kernels; per-pixel columns when yawed)
+    for each pose against the oracle's whole frame, bit-exact."""
+    c = dict(RT_POSES[pose])
+    yaw = c.pop("yaw", 0.0)
+    cfg = dict(dict(width=96, height=72, focal=72.0, cam=[0, 0, -3.0, 1], lights=[[[0.0, -0.5, -0.7, 1.0], _W]],
+                    R=mg.yaw_R(np.float32(0.0) - np.float32(yaw)) if yaw else None), **c)
+    argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+    ref = oracle.rt_draw(mg.rt_params_of(cfg), threads=min(16, os.cpu_count() or 8))
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"{pose}: {bad.size} differ, first {bad[:6]} gpu {argb[bad[:3]]} ref {ref[bad[:3]]}"
