@@ -1059,8 +1059,15 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     __shared__ int8_t s_bi[PITCH * kLatH];
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ float s_dl[2][kLatHalfRows][3][kLatMaxLights];         // column buffers
-    __shared__ float s_pc[kLatTileH][kLatTileW][3];                   // pixel sums
-    __shared__ uint8_t s_valid[kLatTileH][kLatTileW];
+    // pixel sums of the current part only: a part's pixels are resolved when
+    // its sweep ends, into s_px = the start of s_t, whose lattice rows of
+    // finished parts are dead (part h's pixels land in floats 80 h .. 80 h + 79,
+    // rows < 10 h + 10 for both pitches).  2.2 KB less LDS than whole-tile
+    // sums: six workgroups per CU instead of five.
+    __shared__ float s_pc[kLatHalfH][kLatTileW][3];
+    __shared__ uint8_t s_valid[kLatHalfH][kLatTileW];
+    static_assert(kLatHalfH * kLatTileW * kLatParts <= 2 * kLatHalfH * 33, "s_px overlaps a live lattice row");
+    uint32_t *s_px = (uint32_t *)s_t;
     __shared__ unsigned long long s_umask[kLatParts][PITCH];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     LatLightsTile T;
@@ -1070,7 +1077,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
     const int ay0 = G.ay0, cols = G.cols;
     {
         const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
-        if (ty < kLatTileH) {
+        if (ty < kLatHalfH) {
             s_pc[ty][tx][0] = s_pc[ty][tx][1] = s_pc[ty][tx][2] = 0.0f;
             s_valid[ty][tx] = 0;
         }
@@ -1143,7 +1150,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                 const int tx = G.yaw ? cx / 3 : (fk == 0 ? cx / 2 : cx / 2 - 1);
                 const bool use = fpr < npr && tx >= 0 && tx < G.nu && (fk == 0 || (!G.yaw && (cx & 1) == 0));
                 if (use) {
-                    const int ty = pr0 + fpr;
+                    const int ty = fpr;   // row of the part
                     float pc = s_pc[ty][tx][fcomp];
                     bool valid = false;
                     const float *buf = &s_dl[cx & 1][0][0][0];
@@ -1173,17 +1180,26 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             }
             __syncthreads();
         }
+        // the part's pixels (:160-166); their sums are then cleared for the
+        // next part, whose first fold comes after its step 0's barrier
+        const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
+        if (ty < kLatHalfH) {
+            if (ty < npr) {
+                const vec3 pc = v3(s_pc[ty][tx][0], s_pc[ty][tx][1], s_pc[ty][tx][2]);
+                s_px[(pr0 + ty) * kLatTileW + tx] =
+                    s_valid[ty][tx] ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));
+            }
+            s_pc[ty][tx][0] = s_pc[ty][tx][1] = s_pc[ty][tx][2] = 0.0f;
+            s_valid[ty][tx] = 0;
+        }
     }
 #ifdef CG_WALK_STATS
     if (threadIdx.x == 0 && blockIdx.z == 0 && blockIdx.x % 24 == 0 && blockIdx.y % 24 == 0)
         printf("LIGHTS bx %d by %d units %d cand %d sph %d\n", blockIdx.x, blockIdx.y, st_units, st_cand, st_sph);
 #endif
+    __syncthreads();
     const int tx = threadIdx.x % kLatTileW, ty = threadIdx.x / kLatTileW;
-    uint32_t px = 0u;
-    if (tx < G.nu && ty < G.nv) {
-        const vec3 pc = v3(s_pc[ty][tx][0], s_pc[ty][tx][1], s_pc[ty][tx][2]);
-        px = s_valid[ty][tx] ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
-    }
+    const uint32_t px = (tx < G.nu && ty < G.nv) ? s_px[ty * kLatTileW + tx] : 0u;
     lat_store(F, G, T.o, px, tx, ty, (uint32_t *)&s_dl[0][0][0][0]);
 }
 
@@ -1225,7 +1241,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_lattice_units_kernel(RtFrame F0
 }
 
 template <int PITCH>
-__global__ __launch_bounds__(kRtThreads, 5) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, 6) void rt_lattice_lights_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                           const RtShade *__restrict__ shade,
                                                                           const RtSphere *__restrict__ sph,
                                                                           const unsigned long long *__restrict__ lat_masks,
