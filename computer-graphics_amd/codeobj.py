@@ -4,7 +4,7 @@ The bench's executed-work roofline scales rocprofv3 SQ counters collected on
 one build of a kernel; those counters describe that machine code only.
 kernel_sha256(name) hashes the gfx950 code of every kernel whose (mangled)
 name carries `name` -- the function bytes plus its kernel descriptor (`.kd`:
-register counts, scratch, LDS) -- so a profile records what it measured and
+register counts, scratch, LDS; its code-entry offset masked, see below) -- so a profile records what it measured and
 the bench can refuse to scale a stale profile.
 
 Layout walked here: the library's `.hip_fatbin` section holds one clang
@@ -109,8 +109,14 @@ def kernel_sha256(name: str, lib_path: str = DEFAULT_LIB):
         return None
     h = hashlib.sha256()
     for s in hit:
+        b = syms[s]
+        if s.endswith(".kd") and len(b) >= 24:
+            # kernel_code_entry_byte_offset (bytes 16-23) is the distance from the
+            # descriptor to the code: layout, which moves whenever another kernel
+            # of the same code object changes size, not this kernel's machine code
+            b = b[:16] + bytes(8) + b[24:]
         h.update(s.encode() + b"\0")
-        h.update(syms[s])
+        h.update(b)
     return h.hexdigest()
 
 

@@ -306,7 +306,7 @@ __device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int c
 // The workgroup is 1 or 4 waves (blockDim.x 64 or 256): wave w takes
 // iterations w, w + waves, ... of each phase, so a call with few super-tiles
 // (one rank's band) is not bound by one wave's serial chain of certificates.
-__global__ __launch_bounds__(256) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
+__global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
                                                            RtFrame F, const RtSphere *__restrict__ sph,
                                                            const unsigned long long *__restrict__ sup_masks,
                                                            unsigned long long *__restrict__ lat_masks)

@@ -99,6 +99,24 @@ def test_kernel_hash_tracks_machine_code():
     assert codeobj.kernel_sha256("no_such_kernel", cgamd.LIB_PATH) is None
 
 
+def test_kernel_hash_ignores_descriptor_layout(monkeypatch):
+    """The descriptor's code-entry offset (bytes 16-23: where the code sits, which moves when
+    another kernel of the code object changes size) does not change the hash; the code bytes
+    and the rest of the descriptor (registers, LDS, scratch) do."""
+    import codeobj
+    kd = bytes(range(64))
+    base = {"_Z9my_kernelv": b"\x01\x02\x03\x04", "_Z9my_kernelv.kd": kd}
+
+    def h(syms):
+        monkeypatch.setattr(codeobj, "kernel_symbols", lambda lib_path=None: syms)
+        return codeobj.kernel_sha256("my_kernel")
+    moved = dict(base, **{"_Z9my_kernelv.kd": kd[:16] + b"\xff" * 8 + kd[24:]})
+    regs = dict(base, **{"_Z9my_kernelv.kd": kd[:48] + b"\xff" + kd[49:]})
+    code = dict(base, **{"_Z9my_kernelv": b"\x01\x02\x03\x05"})
+    assert h(base) == h(moved)
+    assert h(base) != h(regs) and h(base) != h(code)
+
+
 def test_r2_sample_covers_the_whole_frame():
     """C4/C5 CPU baselines sample an R2 sequence over the whole frame (not the
     central half): a short prefix already reaches every quadrant and both borders."""
