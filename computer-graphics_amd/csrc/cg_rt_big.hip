@@ -607,7 +607,7 @@ __global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const Rt
 
 // The super lists' chunks copied into one contiguous array per super-bin.
 // (An entry without a box gets its bin mask here, in a dense pass.)
-__global__ __launch_bounds__(256) void rt_sup_compact_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+__global__ __launch_bounds__(256, 6) void rt_sup_compact_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
     const int sup = blockIdx.y, c = blockIdx.x;
     if (B.sup_over[sup]) return;
@@ -1504,7 +1504,7 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
 template <int LM>
-__global__ __launch_bounds__(kRtThreads, 5) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, 6) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
 {
