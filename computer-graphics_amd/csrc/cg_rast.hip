@@ -570,9 +570,15 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         const cg_vec4 L = *A.d_light;
         A.light[0] = L.x; A.light[1] = L.y; A.light[2] = L.z;
     }
-    __shared__ int s_sh[DIRECT ? kPostSH : 1][DIRECT ? kPostSW : 1];   // colour modes 1-2: the marks
     __shared__ float s_c[9][kPostHH][kPostHW];      // sc.xyz, lo.xyz, hi.xyz
     __shared__ float s_d[kPostHH][kPostHW];
+    // The halo-2 words (colour modes 1-2: the shadow marks; mode 0: the state
+    // words) live in s_c's space: every thread takes what it needs from them
+    // (its pixels' records and darkenings) into registers before the barrier
+    // after which s_c is written.  26.4 KB instead of 29.7: six workgroups
+    // per CU instead of five.
+    static_assert(sizeof(uint32_t) * kPostSH * kPostSW <= sizeof(float) * 9 * kPostHH * kPostHW, "halo words fit");
+    int (*s_sh)[kPostSW] = reinterpret_cast<int (*)[kPostSW]>(&s_c[0][0][0]);
     const int W = A.W, H = A.H;
     static_assert(kPostTH == kXcdRows, "a post tile row is one XCD row group");
     int m;
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
     // all global loads first (shadow marks, shade state), so each thread has them in flight together
     constexpr int kShR = (kPostSH * kPostSW + 255) / 256, kStR = (kPostHH * kPostHW + 255) / 256;
     // mode 0: the state words (record + 1, mark in bit 31) of the tile + halo 2
-    __shared__ uint32_t s_st[DIRECT ? 1 : kPostSH][DIRECT ? 1 : kPostSW];
+    uint32_t (*s_st)[kPostSW] = reinterpret_cast<uint32_t (*)[kPostSW]>(&s_c[0][0][0]);
     uint32_t shv[kShR];
 #pragma unroll
     for (int r = 0; r < kShR; ++r) {
@@ -610,7 +616,19 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
         }
     }
     __syncthreads();
+    float dv[kStR];   // each pixel's darkening, from the marks before s_c is written
+#pragma unroll
+    for (int r = 0; r < kStR; ++r) {
+        const int i = threadIdx.x + 256 * r;
+        const int cy = i / kPostHW, cx = i - cy * kPostHW;
+        const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
+        dv[r] = 0.0f;
+        if (i < kPostHH * kPostHW && gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1)
+            dv[r] = DIRECT ? darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1)
+                           : darken_at(&s_st[0][0], kPostSW, cy + 1, cx + 1);
+    }
     if constexpr (DIRECT) {
+        __syncthreads();   // the marks are dead: s_c's space is free
 #pragma unroll
         for (int r = 0; r < kStR; ++r) {
             const int i = threadIdx.x + 256 * r;
@@ -618,13 +636,12 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
             const int cy = i / kPostHW, cx = i - cy * kPostHW;
             const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
             vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
-            float d = 0.0f;
+            const float d = dv[r];
             if (gx >= 0 && gy >= 0 && gx < W && gy < H) {
                 const float4 s4 = st16[(size_t)gy * W + gx];
                 const int tb = __float_as_int(s4.x);
                 const bool tri = tb >= 0 && !(tb & kStateDirect);
                 shade3c(A, s4, tri ? tris[tb & ~(1 << 30)].color : cg_vec3{0.f, 0.f, 0.f}, sc, lo, hi);
-                if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_sh[0][0], kPostSW, cy + 1, cx + 1);
             }
             s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
             s_c[3][cy][cx] = lo.x; s_c[4][cy][cx] = lo.y; s_c[5][cy][cx] = lo.z;
@@ -646,6 +663,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
             recv[r] = in ? (int)(s_st[cy + 1][cx + 1] & ~kStShadow) - 1 : -1;
             if (recv[r] >= 0) rv[r] = recs[(size_t)gy * A.n + recv[r]];
         }
+        __syncthreads();   // the state words are dead: s_c's space is free
         cg_vec4 tnv[kStR];
         cg_vec3 colv[kStR];
 #pragma unroll
@@ -662,7 +680,7 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
             const int cy = i / kPostHW, cx = i - cy * kPostHW;
             const int gx = gx0 - 1 + cx, gy = gy0 - 1 + cy;
             vec3 sc = v3(0.f, 0.f, 0.f), lo = sc, hi = sc;
-            float d = 0.0f;
+            const float d = dv[r];
             if (recv[r] >= 0) {   // a shading fragment (:580-585, rebuilt as shade_from_record does)
                 const RowRec &R = rv[r];
                 const float fi = (float)(gx - R.lx);
@@ -680,7 +698,6 @@ __global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restric
                 const float4 s4 = make_float4(__int_as_float(t | (gx == R.first_x ? (1 << 30) : 0)), D.x, D.y, D.z);
                 shade3c(A, s4, colv[r], sc, lo, hi, tex, texel);
             }
-            if (gx >= 1 && gy >= 1 && gx < W - 1 && gy < H - 1) d = darken_at(&s_st[0][0], kPostSW, cy + 1, cx + 1);
             s_c[0][cy][cx] = sc.x; s_c[1][cy][cx] = sc.y; s_c[2][cy][cx] = sc.z;
             s_c[3][cy][cx] = lo.x; s_c[4][cy][cx] = lo.y; s_c[5][cy][cx] = lo.z;
             s_c[6][cy][cx] = hi.x; s_c[7][cy][cx] = hi.y; s_c[8][cy][cx] = hi.z;
