@@ -55,7 +55,8 @@ struct HuffTable {
     uint16_t fast[512];
     int32_t maxcode[18], valoff[17];
     uint8_t vals[256];
-    // false for an over-subscribed code (libjpeg jdhuff.c: JERR_BAD_HUFF_TABLE)
+    // false for an over-subscribed code or one using an all-ones code word
+    // (libjpeg jdhuff.c jpeg_make_d_derived_tbl: code >= 2^len is JERR_BAD_HUFF_TABLE)
     bool build(const uint8_t *counts, const uint8_t *symbols, int total)
     {
         present = false;
@@ -67,7 +68,7 @@ struct HuffTable {
         int code = 0, k = 0;
         for (int len = 1; len <= 16; ++len) {
             valoff[len] = k - code;
-            if (code + counts[len - 1] > (1 << len)) return false;
+            if (counts[len - 1] && code + counts[len - 1] >= (1 << len)) return false;
             for (int i = 0; i < counts[len - 1]; ++i, ++code, ++k)
                 if (len <= 9) {
                     int lo = code << (9 - len), hi = (code + 1) << (9 - len);

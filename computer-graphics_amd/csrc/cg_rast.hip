@@ -449,23 +449,27 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
             const float lz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlz), b));
             const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msz), b));
             const int shd = __builtin_amdgcn_readlane(msh, b);
+            // every readlane sits here, where the whole wave is active: lane b
+            // holds the record, and a readlane under a per-lane condition below
+            // would read a register the compiler may have split under EXEC
+            int tex = 0, idx = 0;
+            float lX = 0.f, sX = 0.f, lY = 0.f, sY = 0.f;
+            if (TEX) {
+                tex = __builtin_amdgcn_readlane(mtex, b);
+                idx = __builtin_amdgcn_readlane(midx, b);
+                lX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlX), b));
+                sX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msX), b));
+                lY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlY), b));
+                sY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msY), b));
+            }
             const int i = x - lx;
             if (!(x < A.W && i >= 0 && x < rx)) continue;          // :504, :573
             const float zinv = lz + (sz * (float)i);               // :543
             if (!shd) {
                 if (zinv >= depth) {                               // :574
                     bool opaque = true;
-                    if (TEX) {
-                        const int tex = __builtin_amdgcn_readlane(mtex, b);
-                        if (tex >= 2) {                            // opacity-tested textures
-                            const int idx = __builtin_amdgcn_readlane(midx, b);
-                            const float lX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlX), b));
-                            const float sX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msX), b));
-                            const float lY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mlY), b));
-                            const float sY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(msY), b));
-                            opaque = rast_opaque(A, tex, idx, zinv, lX + (sX * (float)i), lY + (sY * (float)i));
-                        }
-                    }
+                    if (TEX && tex >= 2)                           // opacity-tested textures
+                        opaque = rast_opaque(A, tex, idx, zinv, lX + (sX * (float)i), lY + (sY * (float)i));
                     if (opaque) {
                         depth = zinv;                              // :665
                         win = base + b;

@@ -891,6 +891,10 @@ __device__ __forceinline__ int lat_swz(int r, int c) { return 4 * ((r * 3 + c) &
 // every needed lattice point) in s_t / s_bi (kLatNoHit: no hit).  False: the tile is done (outside the
 // RGB24 window, or certified black -- then stored black when store_black).
 constexpr int kLatNoHit = -128;   // s_bi: hit indices are -kLatMaxSph .. 62
+// A unit's sole hit object (rt_lattice_units_kernel): outside the hit-index
+// range too, since sphere q's hits are stored as -1 - q (-1 .. -kLatMaxSph).
+constexpr int kUnitNone = -128, kUnitSeveral = -127;
+static_assert(-kLatMaxSph > kUnitSeveral, "unit markers clash with sphere hit indices");
 struct LatLightsTile {
     RtFrame F, Fs;
     LatTile G;
@@ -970,7 +974,7 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
     __shared__ int8_t s_bi[PITCH * kLatH];
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ float s_ubox[kLatParts][PITCH][6];                     // the units' hit boxes
-    __shared__ int s_uone[kLatParts][PITCH];                          // sole hit triangle (-1: several, -2: none)
+    __shared__ int s_uone[kLatParts][PITCH];                          // sole hit object (kUnitSeveral / kUnitNone)
     __shared__ unsigned long long s_umask[kLatParts][PITCH];
     static_assert(kLatParts * PITCH <= kRtThreads, "a thread per unit");
     LatLightsTile T;
@@ -987,14 +991,14 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
             const int lr0 = 2 * h * kLatHalfH, nlr = 2 * min(kLatHalfH, G.nv - h * kLatHalfH) + 1;
             LanePosBox pb;
             pb.init();
-            int one = -2;
+            int one = kUnitNone;
             const float X = lat_x(F, G, cx);
             for (int r = 0; r < nlr; ++r) {
                 const int bi = s_bi[(lr0 + r) * PITCH + cx];
                 if (bi == kLatNoHit) continue;
                 const float Y = 0.5f * (float)(ay0 + lr0 + r), t = s_t[(lr0 + r) * PITCH + cx];
                 pb.add(v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal));
-                one = (one == -2 || one == bi) ? bi : -1;
+                one = (one == kUnitNone || one == bi) ? bi : kUnitSeveral;
             }
             for (int k = 0; k < 3; ++k) {
                 s_ubox[h][cx][k] = pb.lo[k];
@@ -1011,7 +1015,7 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
         const int h = unit / PITCH, cx = unit - h * PITCH;
         if (cx >= cols) continue;
         const int one = s_uone[h][cx];
-        if (one == -2) continue;   // no hit, no shadow ray
+        if (one == kUnitNone) continue;   // no hit, no shadow ray
         const int k = nth_bit(smask, ci);
         const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
         const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
@@ -1028,7 +1032,7 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
     for (int it = threadIdx.x; it < spairs; it += kRtThreads) {
         const int unit = it / F.n_lights, l = it - unit * F.n_lights;
         const int h = unit / PITCH, cx = unit - h * PITCH;
-        if (cx >= cols || s_uone[h][cx] == -2) continue;
+        if (cx >= cols || s_uone[h][cx] == kUnitNone) continue;
         const float lo[3] = {s_ubox[h][cx][0], s_ubox[h][cx][1], s_ubox[h][cx][2]};
         const float hi[3] = {s_ubox[h][cx][3], s_ubox[h][cx][4], s_ubox[h][cx][5]};
         const RtLight Lt = F.lights[l];

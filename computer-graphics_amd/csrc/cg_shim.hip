@@ -728,10 +728,11 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k], &bum = c->pumask[k];
     const size_t tiles = rt_lattice_tiles(F);
     // Both slots' certificate buffers are sized together, for a full batch
-    // (kMaxFrameBatch frames; the unit masks, large at 4K, for this call's
-    // frames): a call never allocates -- hipMalloc / hipFree, the latter a
-    // device-wide wait -- in front of its kernels merely because it batches
-    // more frames than the previous one or is the first on its slot.
+    // (kMaxFrameBatch frames; the unit masks of light sets too: 40 MB per 4K
+    // frame, 2 x 1.3 GB of the 288 GB): a call never allocates -- hipMalloc /
+    // hipFree, the latter a device-wide wait -- in front of its kernels merely
+    // because it batches more frames than the previous one or is the first on
+    // its slot.
     const size_t nfa = std::max(nf, kMaxFrameBatch);
     for (int q = 0; q < 2; ++q) {
         CG_TRY(c, c->plat[q].ensure(nfa * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
@@ -739,7 +740,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
         CG_TRY(c, c->pshade[q].ensure((size_t)std::max(F.n_tris, 1) * sizeof(RtShade)), "alloc tri shading");
         CG_TRY(c, c->psup[q].ensure(nfa * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
         if (rt_lattice_unit_bytes(F, nf))
-            CG_TRY(c, c->pumask[q].ensure(rt_lattice_unit_bytes(F, nf)), "alloc lattice unit masks");
+            CG_TRY(c, c->pumask[q].ensure(rt_lattice_unit_bytes(F, (int)nfa)), "alloc lattice unit masks");
     }
     RtFrameCams fc{};
     for (int f = 0; f < nf; ++f) {

@@ -65,6 +65,7 @@ static int malformed_jpegs()
     dht_dc_bad[17] = 20;                                                               // DC category 20 > 15
     std::vector<uint8_t> dht_ac = {0x10, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x00};
     std::vector<uint8_t> dht_over = {0x10, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 2, 3};  // 3 1-bit codes
+    std::vector<uint8_t> dht_ones = {0x10, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 2};     // '1' used
     const std::vector<uint8_t> sos1 = {1, 1, 0x00, 0, 63, 0};
     std::vector<uint8_t> dqt_short(dqt.begin(), dqt.begin() + 20);
     std::vector<uint8_t> dht_short(dht_ac.begin(), dht_ac.begin() + 10);
@@ -77,6 +78,7 @@ static int malformed_jpegs()
         crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xDA, sos1}}),                        // no AC table
         crafted({{0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_ac}, {0xDA, sos1}}),                     // no quant table
         crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_over}, {0xDA, sos1}}),      // over-subscribed
+        crafted({{0xDB, dqt}, {0xC0, sof1}, {0xC4, dht_dc}, {0xC4, dht_ones}, {0xDA, sos1}}),      // all-ones code
         crafted({{0xDB, dqt_short}, {0xC0, sof1}}),                                                // DQT past its segment
         crafted({{0xC4, dht_short}, {0xC0, sof1}}),                                                // DHT counts cut off
         crafted({{0xC4, dht_short_syms}, {0xC0, sof1}}),                                           // DHT symbols cut off

@@ -82,7 +82,10 @@ typedef struct {
     int eobrun;
 } dec;
 
-static void huff_build(huff *t)
+/* jdhuff.c (libjpeg 9) jpeg_make_d_derived_tbl: the codes of length l must
+ * fit in l bits and none may be all ones (code >= 2^l: JERR_BAD_HUFF_TABLE);
+ * returns 0 for such a table. */
+static int huff_build(huff *t)
 {
     int code = 0, k = 0;
     for (int l = 1; l <= 16; ++l) {
@@ -90,10 +93,12 @@ static void huff_build(huff *t)
         t->mincode[l] = code;
         code += t->bits[l];
         k += t->bits[l];
+        if (t->bits[l] && code >= (1 << l)) return 0;
         t->maxcode[l] = t->bits[l] ? code - 1 : -1;
         code <<= 1;
     }
     t->maxcode[17] = 0x7fffffff;
+    return 1;
 }
 
 static void fill(bits *b)
@@ -546,7 +551,7 @@ int cgo_jpeg_decode(const uint8_t *data, size_t n, uint8_t *out, size_t cap)
                 for (int l = 1; l <= 16; ++l) { t->bits[l] = q[l]; tot += q[l]; }
                 if (tot > 256) { err = -3; break; }
                 memcpy(t->vals, q + 17, (size_t)tot);
-                huff_build(t);
+                if (!huff_build(t)) { err = -3; break; }
                 t->present = 1;
                 q += 17 + tot;
             }

@@ -112,6 +112,52 @@ def test_rt_light_sets_vs_oracle(rt, case):
     assert bad.size == 0, f"{case}: {bad.size} pixels differ, first {bad[:8]}"
 
 
+def _three_spheres():
+    """LoadTestModel's sphere plus two more (TestModelH.h:275-277 shape): the
+    lattice paths store sphere q's hits as -1 - q, so sphere 1's are -2."""
+    _, _, s0 = cgamd.rt_scene()
+    sph = (cgamd.Sphere * 3)(s0, s0, s0)
+    for q, (c, r, col) in enumerate((((0.4, 0.55, -0.3), 0.25, (0.2, 0.8, 0.3)),
+                                     ((0.05, -0.15, 0.1), 0.15, (0.9, 0.4, 0.1))), 1):
+        sph[q].radius, sph[q].radiusSquared = r, np.float32(r) * np.float32(r)
+        sph[q].centre = cgamd.Vec3(*c)
+        sph[q].color = cgamd.Vec3(*col)
+    return sph
+
+
+@pytest.mark.parametrize("case", ["lattice5", "lattice64", "yaw5", "one"])
+def test_rt_three_spheres_vs_oracle(rt, case):
+    """Three spheres under light sets (rt_lattice_units_kernel's per-unit sole-hit
+    object must not confuse sphere 1's hit index -2 with 'no hit'), a yawed
+    light set and the one-light lattice, against the live oracle."""
+    tris, n, _ = cgamd.rt_scene()
+    sph = _three_spheres()
+    W, H, f = 200, 118, 150.0
+    lights = {"lattice64": oracle.rt_area_lights((0.0, -0.5, -0.7, 1.0), (14.0, 14.0, 14.0), 0.1, 8),
+              "one": _LIGHT_SET[:1]}.get(case, _LIGHT_SET)
+    R = cgamd.yaw_matrix(0.3) if case.startswith("yaw") else None
+    cam_pos = (0.05, -0.1, -2.7, 1.0)
+    osph = (oracle.Sphere * 3).from_buffer_copy(sph)
+    otris = (oracle.RtTri * len(tris)).from_buffer_copy(tris)
+    p = oracle.rt_params(W, H, f, cam_pos, list(R) if R is not None else None, lights=lights)
+    ref = oracle.rt_draw(p, threads=os.cpu_count() or 8, scene=(otris, n, osph, 3))
+    arr = (cgamd.Light * len(lights))()
+    for i, (pos, col) in enumerate(lights):
+        arr[i].position = cgamd.Vec4(*pos)
+        arr[i].colour = cgamd.Vec3(*col)
+    rc = rt.lib.cg_rt_set_scene(rt.h, tris, n, sph, 3)
+    assert rc == 0
+    try:
+        argb, _ = rt.rt_render(cgamd.rt_camera(W, H, f, cam_pos, R), arr)
+    finally:
+        _set_scene(rt, {})
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"{case}: {bad.size} pixels differ, first {bad[:8]}"
+    # the extra spheres are in view: the frame differs from the one-sphere scene's
+    ref1 = oracle.rt_draw(p, threads=os.cpu_count() or 8)
+    assert int((ref1 != ref).sum()) > 500
+
+
 @pytest.mark.parametrize("yaw", [0.1745, -0.52, 0.9, 2.0, -1.5707964, 3.1415927])
 def test_rt_yaw_lattice_vs_oracle(rt, yaw):
     """A yawed one-light camera (skeleton.cpp:233-244) takes the lattice

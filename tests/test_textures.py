@@ -45,3 +45,39 @@ def test_textured_oracle_frames_are_deterministic_and_differ():
         assert math.isfinite(float(a.mean()))
     finally:
         oracle.rast_set_textures(None)
+
+
+def _crafted_jpeg(segs):
+    """SOI, the (marker, payload) segments, 64 entropy bytes after SOS, EOI."""
+    j = bytearray(b"\xff\xd8")
+    for m, pay in segs:
+        j += bytes([0xFF, m, (len(pay) + 2) >> 8, (len(pay) + 2) & 0xFF]) + bytes(pay)
+        if m == 0xDA:
+            j += bytes(0x5A ^ k for k in range(64))
+    return bytes(j + b"\xff\xd9")
+
+
+def test_huffman_table_with_all_ones_code_is_rejected():
+    """libjpeg 9 jdhuff.c jpeg_make_d_derived_tbl rejects a table whose codes of
+    length l reach 2^l -- no code word may be all ones (JERR_BAD_HUFF_TABLE).
+    Two 1-bit codes use '1': the product's parser and the oracle both refuse it;
+    one 1-bit code is fine."""
+    sof1 = [8, 0, 16, 0, 16, 1, 1, 0x11, 0]
+    dqt = [0] + [1] * 64
+    dht_dc = [0x00, 1] + [0] * 15 + [0]
+    dht_ac = [0x10, 1] + [0] * 15 + [0]
+    dht_all_ones = [0x10, 2] + [0] * 15 + [0, 1]
+    sos1 = [1, 1, 0x00, 0, 63, 0]
+    good = _crafted_jpeg([(0xDB, dqt), (0xC0, sof1), (0xC4, dht_dc), (0xC4, dht_ac), (0xDA, sos1)])
+    bad = _crafted_jpeg([(0xDB, dqt), (0xC0, sof1), (0xC4, dht_dc), (0xC4, dht_all_ones), (0xDA, sos1)])
+    lib = cgamd.load()
+    gb, bb = np.frombuffer(good, np.uint8), np.frombuffer(bad, np.uint8)
+    assert lib.cg_image_jpeg_check(gb.ctypes.data, gb.size) == 0
+    assert lib.cg_image_jpeg_check(bb.ctypes.data, bb.size) == cgamd.CG_E_INVALID
+    oracle.jpeg_decode(good)
+    try:
+        oracle.jpeg_decode(bad)
+    except ValueError:
+        pass
+    else:
+        raise AssertionError("the oracle accepted a Huffman table with an all-ones code")
