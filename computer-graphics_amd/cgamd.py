@@ -108,6 +108,10 @@ _SIGS = {
     "cg_rt_route": (C.c_int, [C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "cg_rt_set_pool_caps": (C.c_int, [P, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
+    "cg_rt_render_frames": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int, P,
+                                      C.c_size_t, C.c_int, C.POINTER(Stats)]),
+    "cg_kernel_timing": (C.c_int, [C.c_int]),
+    "cg_kernel_time": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
                                       C.POINTER(RtShard), P, P]),
     "cg_rt_render_frames_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int,
@@ -313,6 +317,20 @@ def frame_columns(tris, n, sph, n_sph, cam):
     if rc != CG_OK:
         raise RuntimeError(f"cg_rt_frame_columns failed with {rc}")
     return c0.value, c1.value
+
+
+def kernel_timing(enable: bool):
+    """cg_kernel_timing: start (reset) or stop the live per-kernel HIP-event timing."""
+    if load().cg_kernel_timing(1 if enable else 0) != CG_OK:
+        raise RuntimeError("cg_kernel_timing failed")
+
+
+def kernel_time(kernel: str):
+    """(total ms, launches) of one timed kernel since kernel_timing(True)."""
+    ms, n = C.c_double(), C.c_longlong()
+    if load().cg_kernel_time(kernel.encode(), C.byref(ms), C.byref(n)) != CG_OK:
+        raise ValueError(f"cg_kernel_time: {kernel} is not a timed kernel")
+    return ms.value, n.value
 
 
 def rt_scene():
@@ -521,6 +539,20 @@ class Context:
         st = Stats()
         self._check(self.lib.cg_rt_render(self.h, lights, n_lights, C.byref(cam),
                                           out.ctypes.data_as(P), C.byref(st)), "cg_rt_render")
+        return out, st
+
+    def rt_render_frames(self, cams, out=None, chunk=0, lights=None):
+        """cg_rt_render_frames: len(cams) frames into host memory `out` (uint32, len(cams) * W * H;
+        pageable or pinned, allocated pageable when None), downloads overlapped with later renders."""
+        lights = default_lights() if lights is None else lights
+        arr = (RtCamera * len(cams))(*cams)
+        npx = cams[0].width * cams[0].height
+        if out is None:
+            out = np.zeros(len(cams) * npx, np.uint32)
+        ptr = out.ctypes.data if isinstance(out, np.ndarray) else out.data_ptr()
+        st = Stats()
+        self._check(self.lib.cg_rt_render_frames(self.h, lights, len(lights), arr, len(cams), P(ptr), npx, chunk,
+                                                 C.byref(st)), "cg_rt_render_frames")
         return out, st
 
     def rt_render_device(self, cam, d_out, shard=None, stream=None, lights=None):

@@ -120,6 +120,28 @@ def kernel_sha256(name: str, lib_path: str = DEFAULT_LIB):
     return h.hexdigest()
 
 
+def kernel_names(lib_path: str = DEFAULT_LIB, prefixes=("rt_", "rast_", "jpeg_", "star_")):
+    """The identifiers of the library's kernels (one per template family) whose name starts with
+    one of `prefixes`, from the mangled names of their descriptors."""
+    import re
+    out = set()
+    for s in kernel_symbols(lib_path):
+        if not s.endswith(".kd"):
+            continue
+        pos = 0
+        while True:                     # <length><identifier> runs of the mangled name
+            m = re.compile(r"\d+").search(s, pos)
+            if not m:
+                break
+            n = int(m.group(0))
+            ident = s[m.end():m.end() + n]
+            if ident.startswith(prefixes):
+                out.add(ident)
+                break
+            pos = m.end() + (n if ident[:1].isalpha() or ident[:1] == "_" else 0)
+    return sorted(out)
+
+
 if __name__ == "__main__":
     import sys
     for k in sys.argv[1:] or ["rt_lattice_kernel", "rt_lattice_lights_kernel", "rt_big_primary_kernel"]:

@@ -126,4 +126,24 @@ struct RastTriHdr {
     int pad;
 };
 
+// ---- live kernel timing (cg_ktime.hip, cg_kernel_timing) ---------------
+enum KtId {
+    KT_RT_PREPARE, KT_RT_TILE_CERT, KT_RT_LATTICE_UNITS, KT_RT_LATTICE, KT_RT_LATTICE_LIGHTS, KT_RT_PIXEL,
+    KT_RT_BIG_PRIMARY, KT_RT_SHADOW_HINTS, KT_RT_BIG_FRAME, KT_RAST_FILL, KT_RAST_POST, KT_COUNT
+};
+// HIP events on `st` around the scope's launches while timing is on (id
+// outside [0, KT_COUNT): nothing).
+class KtScope {
+  public:
+    KtScope(int id, hipStream_t st);
+    ~KtScope();
+    KtScope(const KtScope &) = delete;
+    KtScope &operator=(const KtScope &) = delete;
+
+  private:
+    int id_;
+    hipStream_t st_;
+    hipEvent_t a_ = nullptr;
+};
+
 }  // namespace cg

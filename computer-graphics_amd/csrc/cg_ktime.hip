@@ -1,0 +1,121 @@
+// cg_ktime.hip -- live device time of the hot kernels, for the bench's
+// roofline: a pair of HIP events around each timed launch, recorded on the
+// stream the kernel is launched on (the certificate kernels of a batched call
+// run on the context's auxiliary stream, the rasteriser's overlapped frames on
+// its lane streams: events on the caller's stream would time the wrong span).
+// Off by default: a disabled scope records nothing.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "cg_internal.h"
+
+namespace cg {
+
+static const char *const kKtNames[KT_COUNT] = {
+    "rt_prepare_kernel",        "rt_tile_cert_kernel",   "rt_lattice_units_kernel", "rt_lattice_kernel",
+    "rt_lattice_lights_kernel", "rt_pixel_kernel",       "rt_big_primary_kernel",   "rt_shadow_hints_kernel",
+    "rt_big_frame",             "rast_fill_kernel",      "rast_post_kernel",
+};
+
+namespace {
+struct Pending {
+    int id;
+    hipEvent_t a, b;
+};
+struct KtState {
+    std::mutex mu;
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    std::vector<Pending> pending;
+    double ms[KT_COUNT] = {};
+    long long n[KT_COUNT] = {};
+    // Settle the recorded pairs into the totals (blocks until they completed).
+    void flush()
+    {
+        for (const Pending &p : pending) {
+            float ms1 = 0.f;
+            if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms1, p.a, p.b) == hipSuccess) {
+                ms[p.id] += ms1;
+                ++n[p.id];
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+    hipEvent_t get()
+    {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+    }
+};
+KtState &kt()
+{
+    static KtState s;
+    return s;
+}
+}  // namespace
+
+KtScope::KtScope(int id, hipStream_t st) : id_(id), st_(st)
+{
+    KtState &s = kt();
+    std::lock_guard<std::mutex> g(s.mu);
+    if (!s.on || id < 0 || id >= KT_COUNT) return;
+    a_ = s.get();
+    if (a_ && hipEventRecord(a_, st) != hipSuccess) {
+        s.pool.push_back(a_);
+        a_ = nullptr;
+    }
+}
+
+KtScope::~KtScope()
+{
+    if (!a_) return;
+    KtState &s = kt();
+    std::lock_guard<std::mutex> g(s.mu);
+    hipEvent_t b = s.get();
+    if (!s.on || !b || hipEventRecord(b, st_) != hipSuccess) {
+        s.pool.push_back(a_);
+        if (b) s.pool.push_back(b);
+        return;
+    }
+    s.pending.push_back({id_, a_, b});
+}
+
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" int cg_kernel_timing(int enable)
+{
+    KtState &s = kt();
+    std::lock_guard<std::mutex> g(s.mu);
+    s.flush();
+    std::memset(s.ms, 0, sizeof(s.ms));
+    std::memset(s.n, 0, sizeof(s.n));
+    s.on = enable != 0;
+    return CG_OK;
+}
+
+extern "C" int cg_kernel_time(const char *kernel, double *total_ms, long long *launches)
+{
+    if (!kernel || !total_ms || !launches) return CG_E_INVALID;
+    KtState &s = kt();
+    std::lock_guard<std::mutex> g(s.mu);
+    s.flush();
+    for (int k = 0; k < KT_COUNT; ++k)
+        if (std::strcmp(kernel, kKtNames[k]) == 0) {
+            *total_ms = s.ms[k];
+            *launches = s.n[k];
+            return CG_OK;
+        }
+    return CG_E_INVALID;
+}

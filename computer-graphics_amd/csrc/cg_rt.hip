@@ -1439,8 +1439,11 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
     }
-    hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
-                       d_tc, d_shade, prep, Fl, d_sph, sup ? d_sup_masks : d_lat_masks, sup);
+    {
+        KtScope kt(KT_RT_PREPARE, st);
+        hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
+                           d_tc, d_shade, prep, Fl, d_sph, sup ? d_sup_masks : d_lat_masks, sup);
+    }
     if (sup && F && d_lat_masks) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -1450,6 +1453,7 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         // whole frame's 10800 units stay at one wave: 85 us vs 106 with four)
         const int units = rt_cert_units(*F, 1);
         const int threads = (size_t)units * nframes < 8192 ? 256 : 64;
+        KtScope kt(KT_RT_TILE_CERT, st);
         hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(units, nframes), dim3(threads), 0, st, d_tris, n, cams, Fl,
                            d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks);
     }
@@ -1510,6 +1514,7 @@ hipError_t launch_rt_lattice_units(const RtFrame &F, const RtTri *d_tc, const Rt
 {
     if (F.n_lights <= 1) return hipSuccess;
     const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
+    KtScope kt(KT_RT_LATTICE_UNITS, st);
     if (lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_units_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, d_umask);
@@ -1526,6 +1531,7 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
 {
     const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     if (F.n_lights > 1 && !d_umask) return hipErrorInvalidValue;
+    KtScope kt(F.n_lights == 1 ? KT_RT_LATTICE : KT_RT_LATTICE_LIGHTS, st);
     if (F.n_lights == 1 && lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, out_stride, d_out, d_done);
@@ -1553,7 +1559,9 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         if (e != hipSuccess) return e;
         return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, d_umask, cams, 1, 0, d_out, st,
                                         nullptr);
-    } else if (F.n_tris <= 64 && F.cull_primary)
+    }
+    KtScope kt(KT_RT_PIXEL, st);
+    if (F.n_tris <= 64 && F.cull_primary)
         hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     else

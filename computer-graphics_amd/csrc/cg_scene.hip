@@ -213,28 +213,19 @@ extern "C" int cg_rt_random_scene(uint64_t seed, int n, cg_tri *out)
     return n;
 }
 
-// Columns an unrotated camera can see anything in (include/cg_render.h).  A
-// ray of image x-offset X = u - W/2 + i/2 (i = -1, 0, 1) meets the plane
-// z = cz + s at x = cx + s X / f; it can reach a point of the scene's box only
-// if X lies between the extreme projections f (px - cx) / (pz - cz) of the
-// box's corners (all with pz - cz > 0).  FP64, widened by two pixels.
-extern "C" int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int n_spheres,
-                                   const cg_rt_camera *cam, int *col0, int *col1)
+namespace cg {
+// The scene's box for the column windows: every triangle vertex and every
+// sphere (radius widened by 1e-6), then widened by 0.02 (1 + max |coordinate|).
+// A scene property: computed once per uploaded scene (cg_rt_set_scene), so
+// the per-frame window below is O(1) for any camera.  Empty scene: lo > hi.
+void rt_scene_box(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int n_spheres, double lo[3],
+                  double hi[3])
 {
-    if (!cam || !col0 || !col1 || n_tris < 0 || n_spheres < 0 || (n_tris && !tris) || (n_spheres && !spheres) ||
-        cam->width <= 0)
-        return CG_E_INVALID;
-    const int W = cam->width;
-    *col0 = 0;
-    *col1 = W;
-    for (int r = 0; r < 4; ++r)
-        for (int c = 0; c < 4; ++c)
-            if (cam->R[4 * c + r] != (r == c ? 1.0f : 0.0f)) return CG_OK;   // rotated: whole width
-    if (n_tris == 0 && n_spheres == 0) {   // nothing to see
-        *col1 = 0;
-        return CG_OK;
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = 1e300;
+        hi[k] = -1e300;
     }
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    if (n_tris == 0 && n_spheres == 0) return;
     auto add = [&](double x, double y, double z, double r) {
         const double p[3] = {x, y, z};
         for (int k = 0; k < 3; ++k) {
@@ -255,8 +246,27 @@ extern "C" int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphe
         lo[k] -= m;
         hi[k] += m;
     }
+}
+
+// Columns an unrotated camera can see anything in, from the scene's box
+// (rt_scene_box).  A ray of image x-offset X = u - W/2 + i/2 (i = -1, 0, 1)
+// meets the plane z = cz + s at x = cx + s X / f; it can reach a point of the
+// box only if X lies between the extreme projections f (px - cx) / (pz - cz)
+// of the box's corners (all with pz - cz > 0).  FP64, widened by two pixels.
+void rt_box_columns(const double lo[3], const double hi[3], const cg_rt_camera *cam, int *col0, int *col1)
+{
+    const int W = cam->width;
+    *col0 = 0;
+    *col1 = W;
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c)
+            if (cam->R[4 * c + r] != (r == c ? 1.0f : 0.0f)) return;   // rotated: whole width
+    if (lo[0] > hi[0]) {   // nothing to see
+        *col1 = 0;
+        return;
+    }
     const double cx = cam->camera.x, cz = cam->camera.z, f = cam->focal;
-    if (!(lo[2] - cz > 1e-6) || !(f > 0) || !std::isfinite(f)) return CG_OK;   // box reaches behind the camera
+    if (!(lo[2] - cz > 1e-6) || !(f > 0) || !std::isfinite(f)) return;   // box reaches behind the camera
     double xmin = 1e300, xmax = -1e300;
     for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) {
@@ -264,7 +274,7 @@ extern "C" int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphe
             xmin = std::min(xmin, X);
             xmax = std::max(xmax, X);
         }
-    if (!(std::isfinite(xmin) && std::isfinite(xmax))) return CG_OK;
+    if (!(std::isfinite(xmin) && std::isfinite(xmax))) return;
     // pixel u's sub-rays have X in [u - W/2 - 0.5, u - W/2 + 0.5]
     const double u0 = std::floor(xmin + W / 2 - 0.5) - 2.0, u1 = std::ceil(xmax + W / 2 + 0.5) + 3.0;
     int a = (int)std::max(0.0, std::min((double)W, u0)), b = (int)std::max(0.0, std::min((double)W, u1));
@@ -272,9 +282,21 @@ extern "C" int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphe
     b = std::min(W, ((b + 15) / 16) * 16);
     if (a >= b) {
         *col0 = *col1 = 0;
-        return CG_OK;
+        return;
     }
     *col0 = a;
     *col1 = b;
+}
+}  // namespace cg
+
+extern "C" int cg_rt_frame_columns(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int n_spheres,
+                                   const cg_rt_camera *cam, int *col0, int *col1)
+{
+    if (!cam || !col0 || !col1 || n_tris < 0 || n_spheres < 0 || (n_tris && !tris) || (n_spheres && !spheres) ||
+        cam->width <= 0)
+        return CG_E_INVALID;
+    double lo[3], hi[3];
+    cg::rt_scene_box(tris, n_tris, spheres, n_spheres, lo, hi);
+    cg::rt_box_columns(lo, hi, cam, col0, col1);
     return CG_OK;
 }

@@ -29,6 +29,9 @@ hipError_t launch_rt_pixels(const RtFrame &, const RtTri *, const RtShade *, con
                             const unsigned long long *, unsigned long long *, uint32_t *, hipStream_t);
 bool rt_use_lattice(const RtFrame &);
 int rt_lattice_kind(const RtFrame &);
+void rt_scene_box(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int n_spheres, double lo[3],
+                  double hi[3]);
+void rt_box_columns(const double lo[3], const double hi[3], const cg_rt_camera *cam, int *col0, int *col1);
 size_t rt_lattice_tiles(const RtFrame &);
 hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
                          uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, int);
@@ -97,6 +100,11 @@ struct cg_ctx {
     hipEvent_t ev_cert[2] = {nullptr, nullptr}, ev_lat[2] = {nullptr, nullptr};
     int slot = 0;
     DevBuf ptc[2], pshade[2], plat[2], psup[2], pumask[2];
+    // cg_rt_render_frames (host output): chunks render into two device slots
+    // and download on `xfer` while the next chunk renders
+    hipStream_t xfer = nullptr;
+    hipEvent_t ev_rdone[2] = {nullptr, nullptr}, ev_cdone[2] = {nullptr, nullptr};
+    DevBuf hslot[2];
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     int pend_cap = 0;                   // cg_rt_set_pending_cap (0 = default)
     // large-scene pools (cg_rt_big.hip): capacities in entries, sized on the
@@ -110,14 +118,10 @@ struct cg_ctx {
     bool big_ev_live = false;
     unsigned long long big_last[4] = {};
     long long big_overflows = 0;
-    std::vector<cg_tri> tris_host;      // the scene as uploaded (cg_dist's column window)
-    // the latest camera's column window over tris_host (a pass over the whole
-    // scene on the host: 1M triangles take ~6 ms), reused while camera and scene
-    // stay the same -- cg_dist asks for every frame of every call
-    mutable cg_rt_camera col_cam{};
-    mutable int col_c0 = 0, col_c1 = 0;
-    mutable bool col_valid = false;
-    std::vector<cg_sphere> sph_host;
+    // the scene's box (rt_scene_box, once per cg_rt_set_scene): cg_dist's column
+    // window of any camera from it in O(1) per frame -- no per-camera pass over
+    // the scene (1M triangles: ~6 ms on the host) and no per-camera cache
+    double box_lo[3] = {1e300, 1e300, 1e300}, box_hi[3] = {-1e300, -1e300, -1e300};
     std::vector<RtLight> lights_host;   // what `lights` holds (re-uploaded only on change)
     // RAST scratch (owned by cg_rast.hip)
     DevBuf rtris, rhdr, rspan, rpix, rargb, rdepth, rshadow, rcount, rrecs, rgeo, rroom, rboxes;
@@ -147,22 +151,9 @@ void ctx_set_error(cg_ctx *c, const std::string &e) { c->err = e; }
 // cg_rt_frame_columns over the context's scene (the full width without one)
 void ctx_rt_columns(const cg_ctx *c, const cg_rt_camera *cam, int *c0, int *c1)
 {
-    if (c->col_valid && std::memcmp(&c->col_cam, cam, sizeof(*cam)) == 0) {
-        *c0 = c->col_c0;
-        *c1 = c->col_c1;
-        return;
-    }
     *c0 = 0;
     *c1 = cam->width;
-    if (c->n_tris < 0 || cg_rt_frame_columns(c->tris_host.data(), (int)c->tris_host.size(), c->sph_host.data(),
-                                             (int)c->sph_host.size(), cam, c0, c1) != CG_OK) {
-        *c0 = 0;
-        *c1 = cam->width;
-    }
-    c->col_cam = *cam;
-    c->col_c0 = *c0;
-    c->col_c1 = *c1;
-    c->col_valid = true;
+    if (c->n_tris >= 0 && cam->width > 0) rt_box_columns(c->box_lo, c->box_hi, cam, c0, c1);
 }
 // exposed to cg_rast.hip
 void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e)
@@ -297,6 +288,13 @@ extern "C" void cg_destroy(cg_ctx *c)
         if (c->ev_lat[k]) (void)hipEventDestroy(c->ev_lat[k]);
     }
     if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->xfer) (void)hipStreamSynchronize(c->xfer);
+    for (int k = 0; k < 2; ++k) {
+        c->hslot[k].release();
+        if (c->ev_rdone[k]) (void)hipEventDestroy(c->ev_rdone[k]);
+        if (c->ev_cdone[k]) (void)hipEventDestroy(c->ev_cdone[k]);
+    }
+    if (c->xfer) (void)hipStreamDestroy(c->xfer);
     rast_release(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -332,9 +330,7 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     if (n_spheres)
         CG_TRY(c, hipMemcpyAsync(c->sph.p, S.data(), S.size() * sizeof(RtSphere),
                                  hipMemcpyHostToDevice, c->stream), "upload spheres");
-    c->tris_host.assign(tris, tris + n_tris);
-    c->sph_host.assign(spheres, spheres + n_spheres);
-    c->col_valid = false;   // a new scene: column windows again
+    rt_scene_box(tris, n_tris, spheres, n_spheres, c->box_lo, c->box_hi);
     c->grid = RtGrid{};
     c->big_sized = false;   // the next large-scene frame sizes the pools
     if (n_tris > 64) {   // large scene: grid for the shadow-ray blocker search
@@ -671,6 +667,8 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
 
 static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
 {
+    // a large scene's whole frame (prepare .. shading), for the bench's frame figures
+    KtScope kt(F.n_tris > 64 && F.cull_primary && F.cull_shadow ? KT_RT_BIG_FRAME : -1, st);
     unsigned long long *lat = nullptr;
     if (rt_use_lattice(F)) {
         CG_TRY(c, c->latmask.ensure(rt_lattice_tiles(F) * 2 * sizeof(unsigned long long)), "alloc lattice masks");
@@ -911,6 +909,74 @@ extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, con
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->n_tris = c->n_tris;
         stats->n_spans = 0;
+    }
+    return CG_OK;
+}
+
+// n_frames frames into host memory: chunks of `chunk` frames render through
+// rt_render_frames into two device slots on the context's stream; each
+// chunk's download runs on `xfer` while the next chunk renders.  The download
+// of chunk j is issued after chunk j + 1's render is enqueued: a pageable
+// destination makes hipMemcpyAsync stage through the runtime's pinned buffers
+// and return only when the copy is done, so issued in the other order the
+// host would hold back the next render.
+extern "C" int cg_rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
+                                   int n_frames, uint32_t *argb, size_t frame_stride, int chunk, cg_stats *stats)
+{
+    if (!c || !argb || n_frames < 0 || (n_frames && !cams) || chunk < 0) return CG_E_INVALID;
+    if (n_frames == 0) return CG_OK;
+    auto t0 = std::chrono::steady_clock::now();
+    CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    const int W = cams[0].width, H = cams[0].height;
+    if (W <= 0 || H <= 0) return CG_E_INVALID;
+    const size_t px = (size_t)W * H;
+    const size_t stride = frame_stride ? frame_stride : px;
+    if (stride < px) return CG_E_INVALID;
+    const int ch = chunk ? std::min(chunk, 64) : 8;
+    if (!c->xfer) {
+        CG_TRY(c, hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking), "copy stream");
+        for (int k = 0; k < 2; ++k) {
+            CG_TRY(c, hipEventCreateWithFlags(&c->ev_rdone[k], hipEventDisableTiming), "copy event");
+            CG_TRY(c, hipEventCreateWithFlags(&c->ev_cdone[k], hipEventDisableTiming), "copy event");
+        }
+    }
+    for (int k = 0; k < 2; ++k) CG_TRY(c, c->hslot[k].ensure((size_t)ch * px * sizeof(uint32_t)), "alloc frame slots");
+    const int nchunks = (n_frames + ch - 1) / ch;
+    auto download = [&](int j) -> int {
+        const int s = j & 1, f0 = j * ch, nf = std::min(ch, n_frames - f0);
+        CG_TRY(c, hipStreamWaitEvent(c->xfer, c->ev_rdone[s], 0), "copy wait");
+        if (stride == px)
+            CG_TRY(c, hipMemcpyAsync(argb + (size_t)f0 * stride, c->hslot[s].p, (size_t)nf * px * sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, c->xfer), "download frames");
+        else
+            for (int f = 0; f < nf; ++f)
+                CG_TRY(c, hipMemcpyAsync(argb + (size_t)(f0 + f) * stride, (uint32_t *)c->hslot[s].p + (size_t)f * px,
+                                         px * sizeof(uint32_t), hipMemcpyDeviceToHost, c->xfer), "download frame");
+        CG_TRY(c, hipEventRecord(c->ev_cdone[s], c->xfer), "copy event");
+        return CG_OK;
+    };
+    CG_TRY(c, hipEventRecord(c->ev0, c->stream), "event");
+    for (int j = 0; j < nchunks; ++j) {
+        const int s = j & 1, f0 = j * ch, nf = std::min(ch, n_frames - f0);
+        if (j >= 2) CG_TRY(c, hipStreamWaitEvent(c->stream, c->ev_cdone[s], 0), "slot wait");   // chunk j - 2 downloaded
+        int rc = rt_render_frames(c, lights, n_lights, cams + f0, nf, nullptr, c->hslot[s].p, px, CG_PIX_ARGB8888,
+                                  c->stream, nullptr, nullptr);
+        if (rc) return rc;
+        CG_TRY(c, hipEventRecord(c->ev_rdone[s], c->stream), "render event");
+        if (j >= 1 && (rc = download(j - 1))) return rc;
+    }
+    CG_TRY(c, hipEventRecord(c->ev1, c->stream), "event");
+    if (int rc = download(nchunks - 1)) return rc;
+    CG_TRY(c, hipStreamSynchronize(c->xfer), "download frames");
+    CG_TRY(c, hipStreamSynchronize(c->stream), "rt frames");
+    if (stats) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->n_tris = c->n_tris;
+        stats->n_spans = 0;
+        stats->n_shaded = -1;
     }
     return CG_OK;
 }

@@ -144,6 +144,16 @@ int cg_rt_set_scene(cg_ctx *ctx, const cg_tri *tris, int n_tris,
  * the reference leaves in screen->buffer. */
 int cg_rt_render(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
                  uint32_t *argb, cg_stats *stats);   /* 0 <= n_lights <= 4096 */
+/* n_frames successive Draw()s into caller-owned HOST memory (pageable, as
+ * screen->buffer, or pinned): frame f with camera cams[f] at argb + f *
+ * frame_stride pixels (0 = W*H), each what cg_rt_render leaves.  The frames
+ * render `chunk` at a time (0 = 8) through cg_rt_render_frames_device into
+ * device slots while the previous chunk downloads on a second stream (the
+ * main loop of skeleton.cpp:91-94 with the D2H of frame N overlapped with
+ * the render of later frames).  Returns once every frame is in host memory;
+ * stats->kernel_ms spans the renders, total_ms the call. */
+int cg_rt_render_frames(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cams,
+                        int n_frames, uint32_t *argb, size_t frame_stride, int chunk, cg_stats *stats);
 /* Device-resident form: renders this shard's rows into the caller-owned
  * device buffer d_out (cg_rt_shard_rows() rows of W pixels), enqueued on
  * `stream`, no synchronisation.  shard may be NULL (= whole frame). */
@@ -394,6 +404,18 @@ int cg_image_decode_jpeg(cg_ctx *ctx, const uint8_t *data, size_t n, uint8_t *ou
 /* Same into device memory, enqueued on `stream` (NULL: the context's). */
 int cg_image_decode_jpeg_device(cg_ctx *ctx, const uint8_t *data, size_t n, uint8_t *d_out, size_t cap,
                                 void *stream);
+
+/* ---- measurement ----------------------------------------------------- */
+/* Live device time of the hot kernels: while on, HIP events are recorded
+ * around each launch of rt_prepare_kernel, rt_tile_cert_kernel,
+ * rt_lattice_units_kernel, rt_lattice_kernel, rt_lattice_lights_kernel,
+ * rt_pixel_kernel, rt_big_primary_kernel, rt_shadow_hints_kernel,
+ * rast_fill_kernel and rast_post_kernel, on the stream it runs on, plus
+ * "rt_big_frame" (a large scene's whole frame).  cg_kernel_timing(on)
+ * resets the totals (process-wide); cg_kernel_time waits for the recorded
+ * launches and returns the total milliseconds and launch count of one. */
+int cg_kernel_timing(int enable);
+int cg_kernel_time(const char *kernel, double *total_ms, long long *launches);
 
 /* ---- starfield (starfield/Source/skeleton.cpp) -------------------------- */
 /* n stars as (x, y, z) float triples from glibc rand() (:41-46, seed 1). */

@@ -1,6 +1,8 @@
 """One process, one rank: a workload's frames through the library's multi-GPU path
 (cg_rt_render_frames_dist via cgdist.join) against the single-GPU call, timed per call;
-run it under rocprofv3 --kernel-trace to see what the dist path launches.
+run it under rocprofv3 --kernel-trace to see what the dist path launches.  Each path runs with
+a fixed camera and with a moving one (cameraPos.z stepping 0.005 per frame, the reference's UP
+key at a twentieth of its stride, skeleton.cpp:216-218): no rate may depend on a repeated camera.
 Usage: python scripts/dist_probe.py [c5|rt] [frames]"""
 import os
 import sys
@@ -27,24 +29,26 @@ with cgamd.Context(0) as ctx:
     else:
         tris, n, sph = cgamd.rt_scene()
         ctx.rt_set_scene(tris, n, sph, 1)
-    cam = cgamd.rt_camera(W, H, F)
-    cams = (cgamd.RtCamera * NF)(*([cam] * NF))
+    fixed = [cgamd.rt_camera(W, H, F)] * NF
+    moving = [cgamd.rt_camera(W, H, F, (0.0, 0.0, -3.0 + 0.005 * k, 1.0)) for k in range(NF)]
     lights = cgamd.default_lights()
     frames = torch.zeros(NF * H * W, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     for label in ("single", "dist"):
         d = cgdist.join(ctx) if label == "dist" else None
-        times = []
-        for it in range(4):
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            if d is None:
-                ctx.rt_render_frames_device(cams, frames.data_ptr(), stream=st, lights=lights)
-            else:
-                d.render_frames(cams, frames.data_ptr(), stream=st, lights=lights)
-            torch.cuda.synchronize(dev)
-            times.append(time.perf_counter() - t0)
-        print(label, "fps per call:", [round(NF / t, 1) for t in times], flush=True)
+        for path, cl in (("fixed", fixed), ("moving", moving)):
+            cams = (cgamd.RtCamera * NF)(*cl)
+            times = []
+            for it in range(4):
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                if d is None:
+                    ctx.rt_render_frames_device(cams, frames.data_ptr(), stream=st, lights=lights)
+                else:
+                    d.render_frames(cams, frames.data_ptr(), stream=st, lights=lights)
+                torch.cuda.synchronize(dev)
+                times.append(time.perf_counter() - t0)
+            print(label, path, "fps per call:", [round(NF / t, 1) for t in times], flush=True)
         if d is not None:
             print("bands", d.bands(), "last_times", d.last_times(), flush=True)
             d.close()

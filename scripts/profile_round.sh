@@ -20,8 +20,7 @@ run() {  # name timeout cmd...
 B="python3 $ROOT/bench.py --no-cpu-baseline"
 # the machine code these counters describe (bench.py nulls roofline.frac for other code)
 python3 -c "import json, sys; sys.path.insert(0, '$ROOT/computer-graphics_amd'); import codeobj; \
-json.dump({k: codeobj.kernel_sha256(k) for k in ('rt_lattice_kernel', 'rt_lattice_lights_kernel', \
-'rt_big_primary_kernel', 'rt_pixel_kernel', 'rast_fill_kernel', 'rast_post_kernel')}, open('$OUT/code_sha256.json', 'w'), indent=1)"
+json.dump({k: codeobj.kernel_sha256(k) for k in codeobj.kernel_names()}, open('$OUT/code_sha256.json', 'w'), indent=1)"
 WLS=${WLS:-rt rast c4 c5 c5yaw yaw f256}
 has() { case " $WLS " in *" $1 "*) return 0;; esac; return 1; }
 for w in $WLS; do

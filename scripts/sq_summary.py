@@ -1,11 +1,25 @@
-"""Add executed-work figures of the RT pixel kernel to profiles/pmc_summary.json from the SQ
-counter passes of scripts/pmc_sq.sh (gpurun_out/sq_*/).
+"""Add executed-work figures to profiles/pmc_summary.json from the SQ counter passes of
+scripts/profile_round.sh (gpurun_out/sq_<workload>_*/):
+
+  python3 scripts/sq_summary.py KERNEL "gpurun_out/sq_c5_*/sq_counter_collection.csv" SECTION FPL
+
+* sq_kernels[KERNEL]: the dominant kernel's counters per launch, VALU issue fraction and
+  wave states (as before);
+* frame_sq: every library kernel the profiled frames ran (rt_* / rast_* / jpeg_*), each with
+  its executed lane-ops per launch, its launches per launch of KERNEL and its machine-code
+  hash, and their sum per frame -- bench.py's `frac_frame` (every kernel's executed VALU
+  work over the frame's time).
 
 Per MI355X_MICROARCH.md: GRBM_GUI_ACTIVE is summed over the 8 XCDs; a wave64 FP32 VALU
 instruction issues in 2 cycles on a SIMD32; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* are
 quad-cycles and WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY = WAVE_CYCLES.
 """
-import collections, csv, glob, json, os, sys
+import collections
+import csv
+import glob
+import json
+import os
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = sys.argv[1] if len(sys.argv) > 1 else "rt_lattice_kernel"
@@ -13,7 +27,11 @@ SRC = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "sq
 SECTION = sys.argv[3] if len(sys.argv) > 3 else "rt"
 FPL = int(sys.argv[4]) if len(sys.argv) > 4 else 32     # frames per launch of the profiled kernel
 SIMDS = 256 * 4
+PREFIXES = ("rt_", "rast_", "jpeg_", "star_")
 
+
+def base_name(k):
+    return k.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1].strip()
 
 
 def code_sha256(kernel):
@@ -30,11 +48,15 @@ def code_sha256(kernel):
     return codeobj.kernel_sha256(kernel)
 
 
-agg = collections.defaultdict(list)
+agg = collections.defaultdict(list)                               # dominant kernel: counter -> values
+valu = collections.defaultdict(list)                              # every kernel: SQ_INSTS_VALU per dispatch
 for f in sorted(glob.glob(SRC)):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1] == KERNEL:
+        k = base_name(r["Kernel_Name"])
+        if k == KERNEL:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == "SQ_INSTS_VALU" and k.startswith(PREFIXES):
+            valu[k].append(float(r["Counter_Value"]))
 c = {k: sum(v) / len(v) for k, v in agg.items()}
 cycles = c["GRBM_GUI_ACTIVE"] / 8.0
 wave = c["SQ_WAVE_CYCLES"]
@@ -48,9 +70,24 @@ sq = {"kernel": KERNEL, "counters_per_launch": c,
       "note": "valu_issue_frac = SQ_INSTS_VALU x 2 cyc / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
 path = os.path.join(ROOT, "profiles", "pmc_summary.json")
 out = json.load(open(path))
-sqs = out.setdefault(SECTION, {}).setdefault("sq_kernels", {})
+sec = out.setdefault(SECTION, {})
+sqs = sec.setdefault("sq_kernels", {})
 sqs[KERNEL] = sq
 if SECTION == "rt":
     out["rt"]["sq"] = sq
+# the whole frame: each kernel's mean lane-ops per dispatch x its dispatches per dispatch of
+# KERNEL (sizing passes and warm-up frames dispatch the same kernels), over KERNEL's frames
+n_dom = len(valu.get(KERNEL, [])) or 1
+kern = {}
+for k, v in sorted(valu.items()):
+    kern[k] = {"valu_lane_ops_per_launch": 64.0 * sum(v) / len(v), "launches_per_frame_launch": len(v) / n_dom,
+               "code_sha256": code_sha256(k)}
+per_frame = sum(r["valu_lane_ops_per_launch"] * r["launches_per_frame_launch"] for r in kern.values()) / FPL
+sec["frame_sq"] = {"dominant": KERNEL, "frames_per_launch": FPL, "kernels": kern,
+                   "valu_lane_ops_per_frame": per_frame,
+                   "note": "every library kernel of the profiled frames: SQ_INSTS_VALU x 64 per dispatch x "
+                           "dispatches per dispatch of the dominant kernel / frames per dominant launch"}
 json.dump(out, open(path, "w"), indent=1)
-print(json.dumps(sq, indent=1))
+print(json.dumps({"sq": sq, "frame_valu_lane_ops_per_frame": per_frame,
+                  "frame_kernels": {k: round(v["valu_lane_ops_per_launch"] * v["launches_per_frame_launch"] / FPL / 1e9, 3)
+                                    for k, v in kern.items()}}, indent=1))

@@ -117,18 +117,18 @@ def test_kernel_hash_ignores_descriptor_layout(monkeypatch):
     assert h(base) != h(regs) and h(base) != h(code)
 
 
-def test_r2_sample_covers_the_whole_frame():
-    """C4/C5 CPU baselines sample an R2 sequence over the whole frame (not the
-    central half): a short prefix already reaches every quadrant and both borders."""
+def test_stratified_sample_covers_the_whole_frame():
+    """C4/C5 CPU baselines: a fixed stratified sample -- one pixel
+    per cell of an n x n grid over the whole frame, C5's 1,024 pixels -- every cell once, inside
+    the frame, reaching both borders' cells."""
     b = _bench()
-    W, H = 3840, 2160
-    xy = b.r2_pixels(W, H, 0, 64)
-    assert xy[:, 0].min() >= 0 and xy[:, 0].max() < W and xy[:, 1].min() >= 0 and xy[:, 1].max() < H
-    q = {(x * 4 // W, y * 4 // H) for x, y in xy}
-    assert len(q) == 16
-    assert xy[:, 0].min() < W // 8 and xy[:, 0].max() > 7 * W // 8
-    assert xy[:, 1].min() < H // 8 and xy[:, 1].max() > 7 * H // 8
-    assert np.array_equal(b.r2_pixels(W, H, 16, 8), xy[16:24])      # prefixes compose
+    for W, H, n in ((1920, 1080, 32), (3840, 2160, 128)):
+        xy = b.stratified_pixels(W, H, n)
+        assert len(xy) == n * n and len({(x, y) for x, y in xy}) == n * n
+        assert xy[:, 0].min() >= 0 and xy[:, 0].max() < W and xy[:, 1].min() >= 0 and xy[:, 1].max() < H
+        cells = {(x * n // W, y * n // H) for x, y in xy}
+        assert cells == {(i, j) for i in range(n) for j in range(n)}
+    assert b.CPU_STRATA["c5"] ** 2 == 1024
 
 
 def test_cpu_info_reports_physical_cores():
