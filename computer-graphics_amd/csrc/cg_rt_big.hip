@@ -2153,13 +2153,15 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         if (dry == 2) return demand();
     } else if (F.n_lights > 0) {
         hipLaunchKernelGGL(rt_lit_class_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
-        KtScope kt(KT_RT_SHADOW_HINTS, st);
-        if (lat && B.lat_yaw)
-            hipLaunchKernelGGL(rt_shadow_hints_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-        else if (lat)
-            hipLaunchKernelGGL(rt_shadow_hints_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
-        else
-            hipLaunchKernelGGL(rt_shadow_hints_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        {
+            KtScope kt(KT_RT_SHADOW_HINTS, st);
+            if (lat && B.lat_yaw)
+                hipLaunchKernelGGL(rt_shadow_hints_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+            else if (lat)
+                hipLaunchKernelGGL(rt_shadow_hints_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+            else
+                hipLaunchKernelGGL(rt_shadow_hints_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+        }
         hipLaunchKernelGGL(rt_pending_lit_kernel, dim3(1024), dim3(256), 0, st, F, d_tc, B);
     }
     if (lat && B.lat_yaw)

@@ -5,7 +5,9 @@ per cold call, median of N, measured (a) warm: calls back to back after warm-up,
 before each; (b) post-idle: the GPU idle 100 ms, one 5-frame warm-up call, then the timed call
 (bench.py's shape).  The N = 8 estimate is the slowest band plus a modelled tail: the last
 frame's band (RGB24) over one xGMI link at 50 GB/s, the other frames' transfers overlapping the
-render (the signalled pipeline).  Usage: python scripts/band_balanced.py [N]"""
+render (the signalled pipeline).  Both with the metric's fixed camera and with a moving one
+(cameraPos.z = -3 + 0.005 k for frame k, the UP key at a twentieth of its stride): no figure
+may depend on a repeated camera.  Usage: python scripts/band_balanced.py [N] [fixed|moving]"""
 import ctypes
 import json
 import os
@@ -19,16 +21,21 @@ import cgamd  # noqa: E402
 
 W, H, F, K = 1920, 1080, 1080.0, 20
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 15
+PATH = sys.argv[2] if len(sys.argv) > 2 else "fixed"
 BANDS = [(0, 177), (177, 188), (365, 164), (529, 142), (671, 90), (761, 86), (847, 94), (941, 139)]
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 stream = torch.cuda.Stream(dev)
-res = {"K": K, "calls": N, "bands": BANDS}
+res = {"K": K, "calls": N, "bands": BANDS, "camera_path": PATH,
+       "cert_single_max": os.environ.get("CG_CERT_SINGLE_MAX", "0")}
 with cgamd.Context(0) as ctx:
     tris, n, sph = cgamd.rt_scene()
     ctx.rt_set_scene(tris, n, sph, 1)
     cam = cgamd.rt_camera(W, H, F)
-    cams = (cgamd.RtCamera * 32)(*([cam] * 32))
+    if PATH == "moving":
+        cams = (cgamd.RtCamera * 32)(*[cgamd.rt_camera(W, H, F, (0.0, 0.0, -3.0 + 0.005 * k, 1.0)) for k in range(32)])
+    else:
+        cams = (cgamd.RtCamera * 32)(*([cam] * 32))
     lights = cgamd.default_lights()
     buf = torch.zeros(32 * H * W, dtype=torch.int32, device=dev)
     lib, h = ctx.lib, ctx.h
