@@ -159,47 +159,28 @@ __device__ __forceinline__ bool unit_bundle(const RtFrame &F, int unit, int sup,
     return any;
 }
 
-__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
-                                  RtTri *__restrict__ out, RtShade *__restrict__ shade, int n_prep_blocks,
-                                  RtFrame F, const RtSphere *__restrict__ sph,
-                                  unsigned long long *__restrict__ lat_masks, int sup)
+// The certificates of one unit (a tile, or a super-tile with sup = 1) over
+// lpt = 64 / tpw lanes of the calling wave (lane sl = triangle sl, the last
+// lane takes the spheres; sub = which of the wave's tpw units): on return the
+// unit's primary mask (bit 63: a sphere may be hit) and shadow mask (bit 63:
+// a sphere may block a shadow ray), valid in every lane of the unit.  Every
+// lane of the wave calls it (ballots, butterflies).
+__device__ __forceinline__ void unit_cert(const cg_tri *__restrict__ tris, int n, const float camf[4], const RtFrame &F,
+                                          const RtSphere *__restrict__ sph, int unit, int sup, bool tv, int tpw,
+                                          unsigned long long &m_out, unsigned long long &sm_out)
 {
-    const int frame = blockIdx.y;
-    const float cx = cams.c[frame][0], cy = cams.c[frame][1], cz = cams.c[frame][2], cw = cams.c[frame][3];
-    if ((int)blockIdx.x < n_prep_blocks) {
-        const int i = blockIdx.x * blockDim.x + threadIdx.x;
-        if (i >= n) return;
-        const cg_tri T = tris[i];
-        out[(size_t)frame * n + i] = rt_tri_const(T, cx, cy, cz, cw);
-        if (frame == 0) {   // camera-independent
-            RtShade sh;
-            sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
-            sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
-            shade[i] = sh;
-        }
-        return;
-    }
-    // Tile certificates: lpt lanes per tile (lane k = triangle k; the last lane
-    // takes the spheres), two tiles per wave when the scene has <= 31 triangles.
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tiles = rt_cert_units(F, sup);
-    lat_masks += (size_t)frame * tiles * 2;
-    const int tpw = n <= 31 ? 2 : 1, lpt = 64 / tpw;
+    const int lane = threadIdx.x & 63, lpt = 64 / tpw;
     const int sub = lane / lpt, sl = lane - sub * lpt;
-    const int tile = (((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave) * tpw + sub;
-    if (__ballot(tile < tiles) == 0ull) return;   // whole wave
-    const bool tv = tile < tiles;
     float x0, x1, y0, y1;
-    const bool act = unit_bundle(F, tv ? tile : 0, sup, x0, x1, y0, y1) && tv;
-    const float camf[4] = {cx, cy, cz, cw};
+    const bool act = unit_bundle(F, tv ? unit : 0, sup, x0, x1, y0, y1) && tv;
     bool keep = false, sphere = false;
     RtTri c{};
-    LanePosBox pb;   // this lane's share of the tile's possible hit positions
+    LanePosBox pb;   // this lane's share of the unit's possible hit positions
     pb.init();
     PrimDet pd;
     double tlo = 0.0, thi = INFINITY;
     if (act && sl < n) {
-        c = rt_tri_const(tris[sl], cx, cy, cz, cw);
+        c = rt_tri_const(tris[sl], camf[0], camf[1], camf[2], camf[3]);
         keep = !cull_primary(c, x0, x1, y0, y1, F.focal, &pd);
         if (keep && !primary_t_range(c, pd, tlo, thi)) {
             tlo = 0.0;
@@ -230,7 +211,7 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     const unsigned long long half = tpw == 2 ? 0xffffffffull : ~0ull;
     const unsigned long long m = ((__ballot(keep) >> (sub * lpt)) & half) |
                                  (((__ballot(sphere) >> (sub * lpt)) & half) ? (1ull << 63) : 0ull);
-    // the tile's box of possible hit positions (reduction within its lanes)
+    // the unit's box of possible hit positions (reduction within its lanes)
     float blo[3], bhi[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -246,7 +227,7 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     bool keep_s = true;
     if (cert && act && m != 0ull && sl < n && blo[0] <= bhi[0])
         keep_s = !cull_shadow(c, v3(F.lc[0], F.lc[1], F.lc[2]), F.lrho, shadow_box_of_range(F, blo, bhi));
-    // a tile whose every hit lies on one triangle k: k never shadows its own hits
+    // a unit whose every hit lies on one triangle k: k never shadows its own hits
     if (cert && keep && keep_s && m == (1ull << sl)) {
         const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // the light set's centre
         if (own_shadow_rejects(tris[sl], c, pd, thi, camf, x0, x1, y0, y1, F.focal, Lp, F.lrho, blo, bhi))
@@ -255,7 +236,7 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     unsigned long long sm = (__ballot(keep_s && sl < n) >> (sub * lpt)) & half;
     bool sph_shadow = F.n_sph > 0;   // bit 63 of the shadow mask: a sphere may block a shadow ray
     if (m == 0ull) {
-        sm = 0ull;                   // no ray of the tile can hit anything: no shadow rays
+        sm = 0ull;                   // no ray of the unit can hit anything: no shadow rays
         sph_shadow = false;
     } else if (cert && blo[0] <= bhi[0]) {
         bool any = false;
@@ -263,9 +244,51 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
         sph_shadow = any;
     }
     sm = (sm & ~(1ull << 63)) | (sph_shadow ? (1ull << 63) : 0ull);
+    m_out = act ? m : 0ull;
+    sm_out = act ? sm : 0ull;
+}
+
+// Per-frame RtTri / RtShade of triangle i (threads of the first n_prep_blocks blocks).
+__device__ __forceinline__ void prep_tri(const cg_tri *__restrict__ tris, int n, int i, int frame, const float camf[4],
+                                         RtTri *__restrict__ out, RtShade *__restrict__ shade)
+{
+    if (i >= n) return;
+    const cg_tri T = tris[i];
+    out[(size_t)frame * n + i] = rt_tri_const(T, camf[0], camf[1], camf[2], camf[3]);
+    if (frame == 0) {   // camera-independent
+        RtShade sh;
+        sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
+        sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
+        shade[i] = sh;
+    }
+}
+
+__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
+                                  RtTri *__restrict__ out, RtShade *__restrict__ shade, int n_prep_blocks,
+                                  RtFrame F, const RtSphere *__restrict__ sph,
+                                  unsigned long long *__restrict__ lat_masks, int sup)
+{
+    const int frame = blockIdx.y;
+    const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
+    if ((int)blockIdx.x < n_prep_blocks) {
+        prep_tri(tris, n, blockIdx.x * blockDim.x + threadIdx.x, frame, camf, out, shade);
+        return;
+    }
+    // Unit certificates: lpt lanes per unit (lane k = triangle k; the last lane
+    // takes the spheres), two units per wave when the scene has <= 31 triangles.
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tiles = rt_cert_units(F, sup);
+    lat_masks += (size_t)frame * tiles * 2;
+    const int tpw = n <= 31 ? 2 : 1, lpt = 64 / tpw;
+    const int sub = lane / lpt, sl = lane - sub * lpt;
+    const int tile = (((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave) * tpw + sub;
+    if (__ballot(tile < tiles) == 0ull) return;   // whole wave
+    const bool tv = tile < tiles;
+    unsigned long long m, sm;
+    unit_cert(tris, n, camf, F, sph, tile, sup, tv, tpw, m, sm);
     if (tv && sl == 0) {
-        lat_masks[2 * tile] = act ? m : 0ull;
-        lat_masks[2 * tile + 1] = act ? sm : 0ull;
+        lat_masks[2 * tile] = m;
+        lat_masks[2 * tile + 1] = sm;
     }
 }
 
@@ -306,20 +329,48 @@ __device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int c
 // The workgroup is 1 or 4 waves (blockDim.x 64 or 256): wave w takes
 // iterations w, w + waves, ... of each phase, so a call with few super-tiles
 // (one rank's band) is not bound by one wave's serial chain of certificates.
+// Fused (sup_masks == null): one launch does the whole two-level chain -- the
+// first n_prep_blocks blocks write the frame's RtTri / RtShade (as
+// rt_prepare_kernel's), every other block first certifies its super-tile
+// (wave 0, unit_cert) into LDS and then refines it per tile; no super-tile
+// masks round-trip through memory and no second dependent launch.
 __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
                                                            RtFrame F, const RtSphere *__restrict__ sph,
                                                            const unsigned long long *__restrict__ sup_masks,
-                                                           unsigned long long *__restrict__ lat_masks)
+                                                           unsigned long long *__restrict__ lat_masks,
+                                                           RtTri *__restrict__ tc_out, RtShade *__restrict__ shade_out,
+                                                           int n_prep_blocks)
 {
     constexpr int kT = kSup * kSup;
-    const int frame = blockIdx.y, lane = threadIdx.x & 63, unit = blockIdx.x;
+    const int frame = blockIdx.y, lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
+    if ((int)blockIdx.x < n_prep_blocks) {
+        prep_tri(tris, n, blockIdx.x * blockDim.x + threadIdx.x, frame, camf, tc_out, shade_out);
+        return;
+    }
+    const int unit = blockIdx.x - n_prep_blocks;
     const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW, tiles_y = (F.rows_out + kLatTileH - 1) / kLatTileH;
     const int sx = (tiles_x + kSup - 1) / kSup;
     lat_masks += (size_t)frame * tiles_x * tiles_y * 2;
-    sup_masks += ((size_t)frame * rt_cert_units(F, 1) + unit) * 2;
-    const unsigned long long SP = sup_masks[0], SS = sup_masks[1];
+    __shared__ unsigned long long s_sup[2];
+    if (!sup_masks) {
+        if (wave == 0) {
+            unsigned long long m, sm;
+            unit_cert(tris, n, camf, F, sph, unit, 1, true, 1, m, sm);
+            if (lane == 0) {
+                s_sup[0] = m;
+                s_sup[1] = sm;
+            }
+        }
+        __syncthreads();
+    } else if (threadIdx.x == 0) {
+        const unsigned long long *sm = sup_masks + ((size_t)frame * rt_cert_units(F, 1) + unit) * 2;
+        s_sup[0] = sm[0];
+        s_sup[1] = sm[1];
+    }
+    __syncthreads();
+    const unsigned long long SP = s_sup[0], SS = s_sup[1];
     const unsigned long long SPt = SP & ~(1ull << 63), SSt = SS & ~(1ull << 63);
     const bool cert = F.cull_shadow && F.n_lights > 0;
     const double Lp[3] = {(double)F.lc[0], (double)F.lc[1], (double)F.lc[2]};   // the light set's centre
@@ -1422,8 +1473,20 @@ __global__ void rt_probe_direct_light_kernel(RtFrame F, const RtTri *__restrict_
 
 // ---------------------------------------------------------------------------
 // Launch helpers (called by the shim).
-// d_sup_masks (optional): two-level certificates -- rt_prepare_kernel certifies
-// super-tiles into d_sup_masks, rt_tile_cert_kernel refines them per tile.
+// d_sup_masks (optional): two-level certificates -- super-tiles, then their
+// tiles.  By default one fused rt_tile_cert_kernel launch does both levels and
+// the RtTri constants (the super-tile masks stay in LDS; d_sup_masks unused);
+// CG_CERT_FUSED=0 restores the two launches (rt_prepare_kernel certifies the
+// super-tiles into d_sup_masks, rt_tile_cert_kernel refines them), for A/B runs.
+static bool cert_fused()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("CG_CERT_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
                              RtShade *d_shade, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
                              unsigned long long *d_lat_masks, unsigned long long *d_sup_masks)
@@ -1433,30 +1496,45 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
     int cert = 0;
     RtFrame Fl{};
     const int sup = d_sup_masks ? 1 : 0;
-    if (F && d_lat_masks) {
-        Fl = *F;
-        const int units = rt_cert_units(*F, sup);
-        const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
-        cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
-    }
-    {
-        KtScope kt(KT_RT_PREPARE, st);
-        hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
-                           d_tc, d_shade, prep, Fl, d_sph, sup ? d_sup_masks : d_lat_masks, sup);
-    }
     if (sup && F && d_lat_masks) {
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        Fl = *F;
         // few super-tiles (a band of one rank): four waves per super-tile, so
         // the call's certificate latency is a quarter of one wave's chain
         // (C2, 1/8 band, 20 frames, cold: 53.9 -> 28.7 us; 8 waves 49 us; a
         // whole frame's 10800 units stay at one wave: 85 us vs 106 with four)
         const int units = rt_cert_units(*F, 1);
-        const int threads = (size_t)units * nframes < 8192 ? 256 : 64;
+        const int tthreads = (size_t)units * nframes < 8192 ? 256 : 64;
+        if (cert_fused()) {
+            const int tprep = (n + tthreads - 1) / tthreads;
+            KtScope kt(KT_RT_TILE_CERT, st);
+            hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(tprep + units, nframes), dim3(tthreads), 0, st, d_tris, n,
+                               cams, Fl, d_sph, (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep);
+            return hipGetLastError();
+        }
+        const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
+        cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
+        {
+            KtScope kt(KT_RT_PREPARE, st);
+            hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
+                               d_tc, d_shade, prep, Fl, d_sph, d_sup_masks, 1);
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
         KtScope kt(KT_RT_TILE_CERT, st);
-        hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(units, nframes), dim3(threads), 0, st, d_tris, n, cams, Fl,
-                           d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks);
+        hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(units, nframes), dim3(tthreads), 0, st, d_tris, n, cams, Fl,
+                           d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks, (RtTri *)nullptr,
+                           (RtShade *)nullptr, 0);
+        return hipGetLastError();
     }
+    if (F && d_lat_masks) {   // single-level: every tile certified by rt_prepare_kernel
+        Fl = *F;
+        const int units = rt_cert_units(*F, 0);
+        const int tpw = n <= 31 ? 2 : 1;
+        cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
+    }
+    KtScope kt(KT_RT_PREPARE, st);
+    hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
+                       d_tc, d_shade, prep, Fl, d_sph, d_lat_masks, 0);
     return hipGetLastError();
 }
 

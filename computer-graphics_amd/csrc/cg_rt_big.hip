@@ -117,19 +117,6 @@ struct BigBufs {
     float *tile_bb;               // [2 n_bins][32][4]: each half-bin's wave-tile bundles (rt_half_mask_kernel)
 };
 
-// Lane b's RtTri, broadcast to the wave (16 readlanes; lane b must be active).
-__device__ __forceinline__ RtTri rt_tri_readlane(const RtTri &t, int b)
-{
-    auto r = [b](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), b)); };
-    RtTri o;
-    o.e1x = r(t.e1x); o.e1y = r(t.e1y); o.e1z = r(t.e1z);
-    o.e2x = r(t.e2x); o.e2y = r(t.e2y); o.e2z = r(t.e2z);
-    o.sx = r(t.sx); o.sy = r(t.sy); o.sz = r(t.sz); o.detT = r(t.detT);
-    o.K1 = r(t.K1); o.K2 = r(t.K2); o.K3 = r(t.K3);
-    o.v0x = r(t.v0x); o.v0y = r(t.v0y); o.v0z = r(t.v0z);
-    return o;
-}
-
 // ---------------------------------------------------------------------------
 // One triangle, one camera sub-ray (camera-origin constants of RtTri):
 // lexicographic (distance, index) minimum.
@@ -1203,14 +1190,9 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
 #ifdef CG_WALK_STATS
     int st_chunks = 0, st_pass = 0, st_batches = 0, st_walked = 0, st_buckets = 0, st_all = 0, st_wide = 0;
 #endif
-    // The batch's triangles are loaded once, one per lane (coalesced 64 B
-    // rows), for the certificate; the walk then broadcasts each kept one from
-    // its lane's registers (readlane, the whole wave active) instead of a
-    // dependent scalar load per walked triangle from the 64 MB array.
     auto certify_walk = [&](int cnt) {                             // the first cnt (<= 64) queued entries
         const int cand = lane < cnt ? q_w[lane] : -1;
-        const RtTri Tl = tc[cand >= 0 ? cand : 0];
-        const bool keep = cand >= 0 && !cull_primary(Tl, x0, x1, y0, y1, F.focal);
+        const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
         unsigned long long mask = __ballot(keep);
 #ifdef CG_WALK_STATS
         ++st_batches;
@@ -1220,7 +1202,9 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
             const int b = __builtin_ctzll(mask);
             mask &= mask - 1ull;
             const int k = __builtin_amdgcn_readlane(cand, b);
-            const RtTri T = rt_tri_readlane(Tl, b);
+            // scalar loads; broadcasting the certificate's per-lane copy with
+            // 16 readlanes instead measured slower (C5 primary 3.05 -> 3.11 ms)
+            const RtTri T = tc[k];
 #pragma unroll
             for (int s = 0; s < NS; ++s)
                 if (s < nsu && on[s]) tri_closest(T, k, -slot_nd(s), len[s], best[s], bt[s], bi[s]);

@@ -706,17 +706,6 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
     return rt_enqueue(c, F, d_out, st);
 }
 
-// Tile-frames below which a batched call certifies its tiles in one level
-// (CG_CERT_SINGLE_MAX overrides, for measurements).
-static bool rt_cert_single(const RtFrame &F, int nf)
-{
-    static const long long lim = [] {
-        const char *e = std::getenv("CG_CERT_SINGLE_MAX");
-        return e ? std::atoll(e) : 0ll;
-    }();
-    return (long long)rt_lattice_tiles(F) * nf < lim;
-}
-
 // Frames f0 .. f0 + nf - 1 of a batch, one prepare + one lattice launch
 // (rt_use_lattice(F) holds for every frame; they differ only in cameraPos).
 static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
@@ -757,11 +746,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
         fc.c[f][2] = cams[f].camera.z; fc.c[f][3] = cams[f].camera.w;
     }
     unsigned long long *lat = (unsigned long long *)blat.p;
-    // Few tiles in the call (one rank's band): single-level certificates --
-    // one launch, every tile certified against the whole scene -- instead of
-    // the super-tile pass and its refinement, two dependent launches each
-    // bound by one wave's FP64 chain.
-    unsigned long long *supm = rt_cert_single(F, nf) ? nullptr : (unsigned long long *)bsup.p;
+    unsigned long long *supm = (unsigned long long *)bsup.p;
     // certificates on aux, after the slot's previous reader, so that they run
     // beside the lattice launch still queued before them.  A cold call (every
     // earlier lattice launch of this context complete: nothing to run beside)

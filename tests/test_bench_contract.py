@@ -41,6 +41,65 @@ def test_bench_line_contract(name):
     assert cb["cores"] >= 1 and cb["kind"] in ("port", "reference") and cb["value"] > 0
 
 
+def _default():
+    """The latest committed driver-shaped default line (profiles/rNN_bench_default.json)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_default.json")))
+    if not paths:
+        pytest.skip("no profiles/rNN_bench_default.json collected")
+    with open(paths[-1]) as f:
+        return os.path.basename(paths[-1])[:3], json.loads(f.read().strip().splitlines()[-1])
+
+
+def test_default_line_pins_every_config():
+    """The default line (what the driver runs) carries C2 and the C3/C4/C5 sub-records, each
+    with its roofline, its CPU baseline compared with the GPU's pixels, and its parity flags."""
+    rnd, d = _default()
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["frame_sha256_matches_golden"] is True and d["frames_identical_in_call"] is True
+    assert d["cpu_baseline"]["frame_matches_gpu"] is True
+    for name in ("c4", "c5"):
+        s = d[name]
+        assert s["value"] > 0 and s["frames_identical_in_call"] is True
+        assert s["cpu_baseline"]["sample_matches_gpu"] is True and s["cpu_baseline"]["value"] > 0
+        assert "frac" in s["roofline"]
+    assert d["rast"]["cpu_baseline"]["frame_matches_gpu"] is True and d["rast"]["frames_identical_in_batch"] is True
+
+
+def test_default_line_roofline_is_the_kernels_own():
+    """each workload's dominant-kernel fraction is its SQ lane-ops over that
+    kernel's own live HIP-event time (frac), beside the call-span figure (frac_call) and the whole
+    frame's (frac_frame); C5's CPU baseline is SURVEY 8d's 1,024-pixel stratified sample."""
+    rnd, d = _default()
+    if rnd < "r04":
+        pytest.skip("the kernel-own fractions start with round 4's bench")
+    for r, kern in ((d, "rt_lattice_kernel"), (d["c4"], "rt_lattice_lights_kernel"), (d["c5"], "rt_big_primary_kernel")):
+        ro = r["roofline"]
+        assert ro["kernel"] == kern and ro["kernel_ms"] > 0 and ro["kernel_launches"] >= 1
+        assert ro["frac"] is not None and 0 < ro["frac"] <= 1
+        assert ro["frac"] == pytest.approx(ro["achieved"] / ro["peak"])
+        assert ro["frac_frame"] is not None and 0 < ro["frac_frame"] <= 1
+        if ro.get("frac_call") is not None:
+            assert ro["frac_call"] <= ro["frac"] * 1.001      # the call's span includes the kernel's
+        live = r["kernel_ms_live"][kern]
+        assert live["total_ms"] / live["launches"] == pytest.approx(ro["kernel_ms"])
+    assert d["c5"]["cpu_baseline"]["sampled_pixels"] >= 1024
+    assert d["c5"]["cpu_baseline"]["threads"] >= 1 and d["c5"]["cpu_baseline"]["cores"] == 1
+
+
+def test_default_line_measures_the_boundary():
+    """the host-buffer Draw (cg_rt_render / cg_rt_render_frames), pageable and
+    pinned, single frame and pipelined, every frame golden."""
+    rnd, d = _default()
+    if rnd < "r04":
+        pytest.skip("the draw record starts with round 4's bench")
+    dr = d["draw"]
+    assert dr["all_frames_golden"] is True
+    assert dr["single_frame_ms"] > 0 and dr["fps_pageable"] > 0 and dr["fps_pinned"] > 0
+    assert dr["fps_pinned"] < d["value"]          # the PCIe copy is never free
+
+
 def test_headline_line_checks_parity_and_roofline():
     d = _line("rt")
     assert d["metric"].startswith("frames/sec") and d["unit"] == "frames/s"
