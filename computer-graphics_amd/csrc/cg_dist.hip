@@ -486,6 +486,22 @@ extern "C" int cg_dist_rebalance(cg_dist *d)
     return CG_OK;
 }
 
+// The signalled pipeline's chunks of a call: up to C frames each, tapering
+// at the end (half the frames left, at least one), so the transfer and the
+// assembly left after the last frame renders cover one frame, not C (20
+// frames, C = 4: 4 4 4 4 2 1 1).  Senders and rank 0 derive the same plan.
+static std::vector<std::pair<int, int>> chunk_plan(int n_frames, int C)
+{
+    std::vector<std::pair<int, int>> plan;
+    for (int f0 = 0; f0 < n_frames;) {
+        const int left = n_frames - f0;
+        const int nf = left > 2 * C ? C : std::max(1, std::min(C, left / 2));
+        plan.emplace_back(f0, nf);
+        f0 += nf;
+    }
+    return plan;
+}
+
 // One call, signalled: every rank renders its band for all the call's frames
 // in one render call (one lattice launch per 32 frames: full-size launches
 // even for a 1/8 band); ranks > 0 render into the call's send slot and their
@@ -541,8 +557,8 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
         d->last_pitch = pitch;
         d->last_frames = n_frames;
         if (d->group) return CG_OK;   // rank 0 pulls the chunks
-        for (int f0 = 0; f0 < n_frames; f0 += C) {
-            const int nf = std::min(C, n_frames - f0);
+        for (const auto &ch : chunk_plan(n_frames, C)) {
+            const int f0 = ch.first, nf = ch.second;
             for (int f = f0; f < f0 + nf; ++f)
                 if (d->target[s][f])
                     DT(d, hipStreamWaitValue32(d->xs, d->done[s] + f, d->target[s][f], hipStreamWaitValueGte,
@@ -575,8 +591,8 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
             br0[p - 1] = d->row0[p];
             brows[p - 1] = d->rows[p];
         }
-        for (int f0 = 0; f0 < n_frames; f0 += C) {
-            const int nf = std::min(C, n_frames - f0);
+        for (const auto &ch : chunk_plan(n_frames, C)) {
+            const int f0 = ch.first, nf = ch.second;
             uint8_t *cb = rb + (size_t)f0 * per_frame;   // blocks of this chunk, peers in order
             size_t off = 0;
             if (d->group) {

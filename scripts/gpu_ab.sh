@@ -3,8 +3,9 @@
 # timeout (rc not 0/1).  Outputs under gpurun_out/ab_*.  Steps: $AB_STEPS.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out
-mkdir -p $OUT
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"; export TMPDIR=/tmp
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "== $name" | tee -a $OUT/ab_steps.log
@@ -13,7 +14,7 @@ step() {  # name timeout cmd...
   echo "== $name rc=$rc" | tee -a $OUT/ab_steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 "$OUT/ab_$name.log"; exit $rc; fi
 }
-step tests 300 python -u -m pytest tests/test_rt_gpu.py tests/test_dist_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread
+step tests 300 python -u -m pytest tests/test_rt_gpu.py tests/test_dist_gpu.py tests/test_rt_big_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread
 for i in 1 2; do
   step c2_fused_$i 120 python bench.py --steps 20 --warmup 5 --no-sub --no-draw --no-cpu-baseline --no-steady
   step c2_split_$i 120 env CG_CERT_FUSED=0 python bench.py --steps 20 --warmup 5 --no-sub --no-draw --no-cpu-baseline --no-steady
@@ -23,4 +24,6 @@ step c4_split 120 env CG_CERT_FUSED=0 python bench.py --workload c4 --steps 32 -
 step band_fused 200 python scripts/band_balanced.py 15 fixed
 step band_split 200 env CG_CERT_FUSED=0 python scripts/band_balanced.py 15 fixed
 step band_fused_moving 200 python scripts/band_balanced.py 15 moving
+step c5_overlap 200 python scripts/c5_overlap.py 20
+cd /tmp && step trace_band 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_band -o band -- python3 $ROOT/scripts/band_balanced.py 5 fixed
 echo ab done

@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
   echo "== $name rc=$rc"
   [ $rc -eq 0 ] || { tail -5 "$OUT/$name.log"; exit $rc; }
 }
-B="python3 $ROOT/bench.py --no-cpu-baseline"
+B="python3 $ROOT/bench.py --no-cpu-baseline --no-draw --no-steady"
 # the machine code these counters describe (bench.py nulls roofline.frac for other code)
 python3 -c "import json, sys; sys.path.insert(0, '$ROOT/computer-graphics_amd'); import codeobj; \
 json.dump({k: codeobj.kernel_sha256(k) for k in codeobj.kernel_names()}, open('$OUT/code_sha256.json', 'w'), indent=1)"

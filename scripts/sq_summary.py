@@ -80,8 +80,10 @@ if SECTION == "rt":
 n_dom = len(valu.get(KERNEL, [])) or 1
 kern = {}
 for k, v in sorted(valu.items()):
-    kern[k] = {"valu_lane_ops_per_launch": 64.0 * sum(v) / len(v), "launches_per_frame_launch": len(v) / n_dom,
-               "code_sha256": code_sha256(k)}
+    # the median dispatch (a first frame's sizing passes repeat the list kernels on the same
+    # frame) times its dispatches per dominant launch, rounded (2 for the per-frame scans)
+    kern[k] = {"valu_lane_ops_per_launch": 64.0 * sorted(v)[len(v) // 2],
+               "launches_per_frame_launch": max(1, round(len(v) / n_dom)), "code_sha256": code_sha256(k)}
 per_frame = sum(r["valu_lane_ops_per_launch"] * r["launches_per_frame_launch"] for r in kern.values()) / FPL
 sec["frame_sq"] = {"dominant": KERNEL, "frames_per_launch": FPL, "kernels": kern,
                    "valu_lane_ops_per_frame": per_frame,

@@ -1,5 +1,6 @@
 """Summarise a rocprofv3 kernel trace of scripts/band_cost.py: median duration
-per kernel, and per call (a call starts at each rt_prepare_kernel) the span
+per kernel, and per call (a call starts at each rt_prepare_kernel, or at each
+rt_tile_cert_kernel when the certificates are fused into one launch) the span
 from its first kernel's start to its last kernel's end and the idle gaps
 between its kernels.  Usage: trace_calls.py KERNEL_TRACE_CSV"""
 import csv
@@ -14,9 +15,10 @@ for r in rows:
     by.setdefault(name(r), []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, v in by.items():
     print(f"  {k:32s} n={len(v):3d} median {statistics.median(v):8.1f} us")
+first = "rt_prepare_kernel" if "rt_prepare_kernel" in by else "rt_tile_cert_kernel"
 calls, cur = [], []
 for r in rows:
-    if name(r) == "rt_prepare_kernel" and cur:
+    if name(r) == first and cur:
         calls.append(cur)
         cur = []
     cur.append(r)
