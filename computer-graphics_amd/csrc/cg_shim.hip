@@ -118,6 +118,16 @@ struct cg_ctx {
     bool big_ev_live = false;
     unsigned long long big_last[4] = {};
     long long big_overflows = 0;
+    // Large scenes, two frames in flight (rt_render_frames): slot 1's buffers,
+    // stream and demand read-back; slot 0 is tc / shade / big / frame /
+    // big_demand / big_ev above.  A frame's list building and walks are
+    // latency-bound phases; two independent frames fill each other's gaps.
+    DevBuf tc1, shade1, big1, frame1;
+    unsigned long long *big_demand1 = nullptr;
+    hipEvent_t big_ev1 = nullptr;
+    bool big_ev_live1 = false;
+    hipStream_t bst = nullptr;
+    hipEvent_t bev_start = nullptr, bev_end = nullptr;
     // the scene's box (rt_scene_box, once per cg_rt_set_scene): cg_dist's column
     // window of any camera from it in O(1) per frame -- no per-camera pass over
     // the scene (1M triangles: ~6 ms on the host) and no per-camera cache
@@ -275,6 +285,16 @@ extern "C" void cg_destroy(cg_ctx *c)
     }
     for (DevBuf *b : bufs) b->release();
     if (c->big_demand) (void)hipHostFree(c->big_demand);
+    if (c->bst) (void)hipStreamSynchronize(c->bst);
+    if (c->big_ev1) {
+        (void)hipEventSynchronize(c->big_ev1);
+        (void)hipEventDestroy(c->big_ev1);
+    }
+    if (c->big_demand1) (void)hipHostFree(c->big_demand1);
+    c->tc1.release(); c->shade1.release(); c->big1.release(); c->frame1.release();
+    if (c->bev_start) (void)hipEventDestroy(c->bev_start);
+    if (c->bev_end) (void)hipEventDestroy(c->bev_end);
+    if (c->bst) (void)hipStreamDestroy(c->bst);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
     for (int k = 0; k < cg_ctx::kRastLanes; ++k) {
         if (c->lanes[k]) cg_destroy(c->lanes[k]);
@@ -506,17 +526,41 @@ extern "C" int cg_rt_route(const cg_rt_camera *cam, int n_tris, int n_spheres, i
     return k == 1 ? CG_RT_ROUTE_LIGHTS : CG_RT_ROUTE_LIGHTS_YAW;
 }
 
-static bool big_observe(cg_ctx *c, bool sizing);
+// A large-scene frame slot's buffers (slot 0: the context's own; slot 1: the
+// second frame in flight of rt_render_frames).
+struct BigSlot {
+    DevBuf *tc, *shade, *big, *frame;
+    unsigned long long **demand;
+    hipEvent_t *ev;
+    bool *ev_live;
+};
+static BigSlot big_slot(cg_ctx *c, int q)
+{
+    if (q) return BigSlot{&c->tc1, &c->shade1, &c->big1, &c->frame1, &c->big_demand1, &c->big_ev1, &c->big_ev_live1};
+    return BigSlot{&c->tc, &c->shade, &c->big, &c->frame, &c->big_demand, &c->big_ev, &c->big_ev_live};
+}
+
+static bool big_observe(cg_ctx *c, bool sizing, int q);
+
+// Settle both slots' outstanding pool demand (blocks on their last frames).
+static int big_observe_all(cg_ctx *c)
+{
+    for (int q = 0; q < 2; ++q) {
+        const BigSlot b = big_slot(c, q);
+        if (*b.ev_live) {
+            CG_TRY(c, hipEventSynchronize(*b.ev), "pool demand");
+            big_observe(c, false, q);
+        }
+    }
+    return CG_OK;
+}
 
 extern "C" int cg_rt_scratch_info(cg_ctx *c, uint64_t *out)
 {
     if (!c || !out) return CG_E_INVALID;
-    if (c->big_ev_live) {
-        CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
-        big_observe(c, false);
-    }
+    if (int rc = big_observe_all(c)) return rc;
     const unsigned long long *d = c->big_last;
-    out[0] = c->big.bytes;
+    out[0] = c->big.bytes + c->big1.bytes;
     out[1] = d[0] + d[1] + d[2] + d[3];
     out[2] = (uint64_t)(c->big_caps.sup + c->big_caps.bin + c->big_caps.sbin + c->big_caps.sorted);
     out[3] = (uint64_t)c->big_overflows;
@@ -526,10 +570,7 @@ extern "C" int cg_rt_scratch_info(cg_ctx *c, uint64_t *out)
 extern "C" int cg_rt_pool_demand(cg_ctx *c, uint64_t *out)
 {
     if (!c || !out) return CG_E_INVALID;
-    if (c->big_ev_live) {
-        CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
-        big_observe(c, false);
-    }
+    if (int rc = big_observe_all(c)) return rc;
     for (int k = 0; k < 4; ++k) out[k] = c->big_last[k];
     return CG_OK;
 }
@@ -565,9 +606,10 @@ extern "C" int cg_rt_shard_rows(int height, const cg_rt_shard *shard)
     return per * s->stripe_h;
 }
 
-static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st);
+static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st, int slot);
 
-static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t st)
+// slot: a large scene's frame slot (rt_render_frames' second frame in flight: 1)
+static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t st, int slot = 0)
 {
     // RGB24 output: the lattice kernel stores it directly; the other kernels
     // render ARGB into the context's scratch frame, then one pack pass
@@ -575,11 +617,12 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t 
     uint32_t *d_out = (uint32_t *)d_out_v;
     const bool pack = F.out_fmt == CG_PIX_RGB24 && !rt_use_lattice(F);
     if (pack) {
-        CG_TRY(c, c->frame.ensure((size_t)F.rows_out * F.W * sizeof(uint32_t)), "alloc frame");
-        d_out = (uint32_t *)c->frame.p;
+        DevBuf &fr = *big_slot(c, slot).frame;
+        CG_TRY(c, fr.ensure((size_t)F.rows_out * F.W * sizeof(uint32_t)), "alloc frame");
+        d_out = (uint32_t *)fr.p;
         F.out_fmt = CG_PIX_ARGB8888;
     }
-    int rc = rt_enqueue_kernels(c, F, d_out, st);
+    int rc = rt_enqueue_kernels(c, F, d_out, st, slot);
     if (rc || !pack) return rc;
     CG_TRY(c, launch_rt_pack_rgb24(d_out, F.W, F.rows_out, Fin.wcols ? Fin.wcol0 : 0, Fin.wcols ? Fin.wcols : F.W,
                                    (uint8_t *)d_out_v, st), "pack launch");
@@ -591,9 +634,10 @@ static int rt_enqueue(cg_ctx *c, const RtFrame &Fin, void *d_out_v, hipStream_t 
 // overflow nor hold more than ~1.6x what they list); a sizing frame sets them
 // to 1.25x its demand either way.  True when the frame overflowed a pool (it
 // was still right: the consumers fell back to every triangle).
-static bool big_observe(cg_ctx *c, bool sizing = false)
+static bool big_observe(cg_ctx *c, bool sizing, int q)
 {
-    std::memcpy(c->big_last, c->big_demand, sizeof(c->big_last));
+    const BigSlot b = big_slot(c, q);
+    std::memcpy(c->big_last, *b.demand, sizeof(c->big_last));
     const unsigned long long *d = c->big_last;
     long long *cap[4] = {&c->big_caps.sup, &c->big_caps.bin, &c->big_caps.sbin, &c->big_caps.sorted};
     bool over = false;
@@ -604,7 +648,7 @@ static bool big_observe(cg_ctx *c, bool sizing = false)
             *cap[k] = std::min<long long>(need + need / 4 + 4096, (1ll << 31) - 1);
     }
     if (!sizing) c->big_overflows += over;
-    c->big_ev_live = false;
+    *b.ev_live = false;
     return over;
 }
 
@@ -615,13 +659,14 @@ static bool big_observe(cg_ctx *c, bool sizing = false)
 // shades through per-bin shadow lists -- dry passes up to those lists.  Later
 // frames stay asynchronous and grow the pools for the next ones from their
 // reported demand; a frame that still overflows renders through the fallback.
-static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
+static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st, int slot)
 {
-    if (!c->big_demand) {
-        CG_TRY(c, hipHostMalloc((void **)&c->big_demand, 4 * sizeof(unsigned long long), hipHostMallocDefault),
+    const BigSlot S = big_slot(c, slot);
+    if (!*S.demand) {
+        CG_TRY(c, hipHostMalloc((void **)S.demand, 4 * sizeof(unsigned long long), hipHostMallocDefault),
                "alloc pool demand");
-        std::memset(c->big_demand, 0, 4 * sizeof(unsigned long long));
-        CG_TRY(c, hipEventCreateWithFlags(&c->big_ev, hipEventDisableTiming), "pool event");
+        std::memset(*S.demand, 0, 4 * sizeof(unsigned long long));
+        CG_TRY(c, hipEventCreateWithFlags(S.ev, hipEventDisableTiming), "pool event");
     }
     if (c->big_caps.sup == 0) {   // first guess; the first frame corrects it
         const long long g = 2ll * F.n_tris + 65536;
@@ -636,25 +681,29 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
         c->big_sized = false;
     }
     if (c->big_fixed) c->big_sized = true;
-    if (c->big_ev_live && hipEventQuery(c->big_ev) == hipSuccess) big_observe(c);
+    for (int q = 0; q < 2; ++q) {   // either slot's finished frame reports its demand
+        const BigSlot b = big_slot(c, q);
+        if (*b.ev_live && hipEventQuery(*b.ev) == hipSuccess) big_observe(c, false, q);
+    }
     int stage = c->big_sized ? 0 : 1;   // dry stage of the next pass (0: render)
+    DevBuf &big = *S.big;
     for (int pass = 0; pass < 8; ++pass) {
         const int dry = pass == 7 ? 0 : stage;
         const size_t need = rt_big_scratch_bytes(F, c->big_caps);
-        if ((need > c->big.bytes || need < c->big.bytes / 2) && c->big.p) {   // grow, or give back a sized-down half
+        if ((need > big.bytes || need < big.bytes / 2) && big.p) {   // grow, or give back a sized-down half
             CG_TRY(c, hipDeviceSynchronize(), "drain before resizing scratch");
-            c->big.release();
+            big.release();
         }
-        CG_TRY(c, c->big.ensure(need), "alloc large-scene scratch");
-        CG_TRY(c, launch_rt_big(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
-                                c->grid, c->big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap, c->big_caps,
-                                c->big_demand, dry),
+        CG_TRY(c, big.ensure(need), "alloc large-scene scratch");
+        CG_TRY(c, launch_rt_big(F, (const RtTri *)S.tc->p, (const RtShade *)S.shade->p, (const RtSphere *)c->sph.p,
+                                c->grid, big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap, c->big_caps,
+                                *S.demand, dry),
                "rt_big launch");
-        CG_TRY(c, hipEventRecord(c->big_ev, st), "pool event");
-        c->big_ev_live = true;
+        CG_TRY(c, hipEventRecord(*S.ev, st), "pool event");
+        *S.ev_live = true;
         if (!dry) break;
-        CG_TRY(c, hipEventSynchronize(c->big_ev), "pool demand");
-        if (big_observe(c, true)) continue;          // grown: the same stage again
+        CG_TRY(c, hipEventSynchronize(*S.ev), "pool demand");
+        if (big_observe(c, true, slot)) continue;          // grown: the same stage again
         if (stage == 1 && rt_big_shadow_lists(F)) {
             stage = 2;
         } else {
@@ -665,7 +714,7 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
     return CG_OK;
 }
 
-static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st)
+static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStream_t st, int slot)
 {
     // a large scene's whole frame (prepare .. shading), for the bench's frame figures
     KtScope kt(F.n_tris > 64 && F.cull_primary && F.cull_shadow ? KT_RT_BIG_FRAME : -1, st);
@@ -685,9 +734,15 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
         CG_TRY(c, c->supmask.ensure(rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
         supm = (unsigned long long *)c->supmask.p;
     }
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
-    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st);
+    const BigSlot S = big_slot(c, slot);   // slot 1 only for large scenes (rt_render_frames)
+    if (slot) {
+        const size_t nt = (size_t)std::max(c->n_tris, 1);
+        CG_TRY(c, S.tc->ensure(nt * sizeof(RtTri)), "alloc tri constants");
+        CG_TRY(c, S.shade->ensure(nt * sizeof(RtShade)), "alloc tri shading");
+    }
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)S.tc->p,
+                                (RtShade *)S.shade->p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
+    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st, slot);
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                (const RtSphere *)c->sph.p, lat, um, d_out, st), "rt_pixel launch");
     return CG_OK;
@@ -778,6 +833,16 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     return CG_OK;
 }
 
+// Two large-scene frames in flight (default); CG_BIG_SLOTS=1 keeps one, for A/B runs.
+static bool big_two_slots()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("CG_BIG_SLOTS");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 static size_t pix_bytes(int fmt) { return fmt == CG_PIX_RGB24 ? 3 : 4; }
 
 namespace cg {
@@ -826,18 +891,38 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
         batch = cams[f].focal == cams[0].focal && cams[f].indirect == cams[0].indirect &&
                 std::memcmp(cams[f].R, cams[0].R, sizeof(cams[0].R)) == 0;
     if (!batch) {
+        // Large scenes: consecutive frames alternate between two slots on two
+        // streams, two independent frames in flight (CG_BIG_SLOTS=1: one)
+        const bool two = n_frames > 1 && F.n_tris > 64 && F.cull_primary && F.cull_shadow && big_two_slots();
+        if (two) {
+            if (!c->bst) {
+                CG_TRY(c, hipStreamCreateWithFlags(&c->bst, hipStreamNonBlocking), "slot stream");
+                CG_TRY(c, hipEventCreateWithFlags(&c->bev_start, hipEventDisableTiming), "slot event");
+                CG_TRY(c, hipEventCreateWithFlags(&c->bev_end, hipEventDisableTiming), "slot event");
+            }
+            // slot 1 starts after what the caller queued before this call (the
+            // scene, the lights just uploaded on st)
+            CG_TRY(c, hipEventRecord(c->bev_start, st), "slot event");
+            CG_TRY(c, hipStreamWaitEvent(c->bst, c->bev_start, 0), "slot wait");
+        }
         for (int f = 0; f < n_frames; ++f) {
             if (f) {
                 rc = fill_frame(c, lights, n_lights, &cams[f], shard, st, F);
                 if (rc) return rc;
                 F.out_fmt = pix_format;
             }
-            rc = rt_enqueue(c, F, out + (size_t)f * fbytes, st);
+            const int q = two ? (f & 1) : 0;
+            hipStream_t fs = q ? c->bst : st;
+            rc = rt_enqueue(c, F, out + (size_t)f * fbytes, fs, q);
             if (rc) return rc;
             if (d_done) {
-                CG_TRY(c, hipStreamWriteValue32(st, d_done + f, 1u, 0), "frame signal");
+                CG_TRY(c, hipStreamWriteValue32(fs, d_done + f, 1u, 0), "frame signal");
                 target[f] = 1u;
             }
+        }
+        if (two) {   // the call ends on the caller's stream
+            CG_TRY(c, hipEventRecord(c->bev_end, c->bst), "slot event");
+            CG_TRY(c, hipStreamWaitEvent(st, c->bev_end, 0), "slot wait");
         }
         return CG_OK;
     }

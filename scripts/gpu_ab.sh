@@ -24,6 +24,10 @@ step c4_split 120 env CG_CERT_FUSED=0 python bench.py --workload c4 --steps 32 -
 step band_fused 200 python scripts/band_balanced.py 15 fixed
 step band_split 200 env CG_CERT_FUSED=0 python scripts/band_balanced.py 15 fixed
 step band_fused_moving 200 python scripts/band_balanced.py 15 moving
-step c5_overlap 200 python scripts/c5_overlap.py 20
+for i in 1 2; do
+  step c5_two_$i 150 python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline
+  step c5_one_$i 150 env CG_BIG_SLOTS=1 python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline
+done
+step dist_c5 200 python scripts/dist_probe.py c5 20
 cd /tmp && step trace_band 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_band -o band -- python3 $ROOT/scripts/band_balanced.py 5 fixed
 echo ab done

@@ -174,3 +174,34 @@ def test_big_scene_degenerate_triangles(ctx, case, around_eye, n):
     bad = np.flatnonzero(argb != ref)
     assert bad.size == 0, f"{case}: {bad.size} pixels differ, first {bad[:6]}: gpu {argb[bad[:3]]} ref {ref[bad[:3]]}"
     assert (ref != 0x80000000).sum() > ref.size // 2                      # the backdrop fills the frame
+
+
+@pytest.mark.parametrize("lights_n", [1, 16])
+def test_big_frames_two_in_flight_equal_single_frames(ctx, lights_n):
+    """cg_rt_render_frames_device over a large scene alternates consecutive frames between
+    two slots on two streams (two independent frames in flight): a dolly camera path and a
+    second call right after it (slot parity and the slots' buffers reused across calls) give
+    exactly the frames cg_rt_render renders one at a time."""
+    import torch
+    W, H, F = 160, 96, 120.0
+    n = 4000
+    ctx.rt_set_scene(cgamd.random_scene(n, 0x5EED), n, None, 0)
+    try:
+        lights = cgamd.default_lights() if lights_n == 1 else cgamd.area_lights(None, 0.1, 4)
+        cams = [cgamd.rt_camera(W, H, F, (0.0, 0.0, float(np.float32(-3.0 + 0.05 * k)), 1.0)) for k in range(5)]
+        want = [ctx.rt_render(c, lights)[0] for c in cams]
+        dev = torch.device("cuda", 0)
+        s = torch.cuda.Stream(dev)
+        for call in range(2):
+            out = torch.zeros(len(cams) * W * H, dtype=torch.int32, device=dev)
+            order = cams if call == 0 else cams[::-1]
+            ctx.rt_render_frames_device(order, out.data_ptr(), stream=s.cuda_stream, lights=lights)
+            s.synchronize()
+            got = out.cpu().numpy().view(np.uint32).reshape(len(cams), W * H)
+            exp = want if call == 0 else want[::-1]
+            for k in range(len(cams)):
+                assert np.array_equal(got[k], exp[k]), f"call {call} frame {k}"
+        assert len({w.tobytes() for w in want}) == len(want)      # the path's frames differ
+    finally:
+        tris, nt, sph = cgamd.rt_scene()
+        ctx.rt_set_scene(tris, nt, sph, 1)
