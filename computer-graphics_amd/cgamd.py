@@ -111,7 +111,7 @@ _SIGS = {
     "cg_rt_render_frames": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int, P,
                                       C.c_size_t, C.c_int, C.POINTER(Stats)]),
     "cg_kernel_timing": (C.c_int, [C.c_int]),
-    "cg_kernel_time": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
+    "cg_kernel_time": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_longlong)]),
     "cg_rt_render_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera),
                                       C.POINTER(RtShard), P, P]),
     "cg_rt_render_frames_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int,
@@ -326,11 +326,12 @@ def kernel_timing(enable: bool):
 
 
 def kernel_time(kernel: str):
-    """(total ms, launches) of one timed kernel since kernel_timing(True)."""
-    ms, n = C.c_double(), C.c_longlong()
-    if load().cg_kernel_time(kernel.encode(), C.byref(ms), C.byref(n)) != CG_OK:
+    """(total ms, busy ms, launches) of one timed kernel since kernel_timing(True); busy counts
+    overlapping launches (two frames in flight) once."""
+    ms, busy, n = C.c_double(), C.c_double(), C.c_longlong()
+    if load().cg_kernel_time(kernel.encode(), C.byref(ms), C.byref(busy), C.byref(n)) != CG_OK:
         raise ValueError(f"cg_kernel_time: {kernel} is not a timed kernel")
-    return ms.value, n.value
+    return ms.value, busy.value, n.value
 
 
 def rt_scene():

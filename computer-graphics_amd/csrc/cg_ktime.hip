@@ -6,8 +6,10 @@
 // Off by default: a disabled scope records nothing.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "cg_internal.h"
@@ -32,19 +34,45 @@ struct KtState {
     std::vector<Pending> pending;
     double ms[KT_COUNT] = {};
     long long n[KT_COUNT] = {};
+    // each launch's [start, end] in ms after `ref` (the first timed launch since
+    // timing was switched on): launches of one kernel that overlap (two frames in
+    // flight on two streams) count once in its busy time
+    hipEvent_t ref = nullptr;
+    bool ref_set = false;
+    std::vector<std::pair<double, double>> spans[KT_COUNT];
     // Settle the recorded pairs into the totals (blocks until they completed).
     void flush()
     {
         for (const Pending &p : pending) {
-            float ms1 = 0.f;
+            float ms1 = 0.f, t0 = 0.f;
             if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms1, p.a, p.b) == hipSuccess) {
                 ms[p.id] += ms1;
                 ++n[p.id];
+                if (ref_set && hipEventElapsedTime(&t0, ref, p.a) == hipSuccess)
+                    spans[p.id].emplace_back((double)t0, (double)t0 + ms1);
             }
             pool.push_back(p.a);
             pool.push_back(p.b);
         }
         pending.clear();
+    }
+    // union length of a kernel's launch spans
+    double busy(int id)
+    {
+        std::vector<std::pair<double, double>> v = spans[id];
+        std::sort(v.begin(), v.end());
+        double tot = 0.0, s = 0.0, e = -1e300;
+        for (const auto &x : v) {
+            if (x.first > e) {
+                if (e > s) tot += e - s;
+                s = x.first;
+                e = x.second;
+            } else {
+                e = std::max(e, x.second);
+            }
+        }
+        if (!v.empty() && e > s) tot += e - s;
+        return tot;
     }
     hipEvent_t get()
     {
@@ -69,6 +97,10 @@ KtScope::KtScope(int id, hipStream_t st) : id_(id), st_(st)
     KtState &s = kt();
     std::lock_guard<std::mutex> g(s.mu);
     if (!s.on || id < 0 || id >= KT_COUNT) return;
+    if (!s.ref_set) {
+        if (!s.ref && hipEventCreate(&s.ref) != hipSuccess) s.ref = nullptr;
+        s.ref_set = s.ref && hipEventRecord(s.ref, st) == hipSuccess;
+    }
     a_ = s.get();
     if (a_ && hipEventRecord(a_, st) != hipSuccess) {
         s.pool.push_back(a_);
@@ -101,19 +133,22 @@ extern "C" int cg_kernel_timing(int enable)
     s.flush();
     std::memset(s.ms, 0, sizeof(s.ms));
     std::memset(s.n, 0, sizeof(s.n));
+    for (auto &v : s.spans) v.clear();
+    s.ref_set = false;
     s.on = enable != 0;
     return CG_OK;
 }
 
-extern "C" int cg_kernel_time(const char *kernel, double *total_ms, long long *launches)
+extern "C" int cg_kernel_time(const char *kernel, double *total_ms, double *busy_ms, long long *launches)
 {
-    if (!kernel || !total_ms || !launches) return CG_E_INVALID;
+    if (!kernel || !total_ms || !busy_ms || !launches) return CG_E_INVALID;
     KtState &s = kt();
     std::lock_guard<std::mutex> g(s.mu);
     s.flush();
     for (int k = 0; k < KT_COUNT; ++k)
         if (std::strcmp(kernel, kKtNames[k]) == 0) {
             *total_ms = s.ms[k];
+            *busy_ms = s.ref_set ? s.busy(k) : s.ms[k];
             *launches = s.n[k];
             return CG_OK;
         }

@@ -422,20 +422,8 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
     const int x = x0 + lane;
     float depth = 0.0f;                                   // :247
     int shadow = 0, win = -1;                             // :259; record of the last shading fragment
-    const RowRec *rr = recs + (size_t)y * A.n;
-    // The first kFillPre batches of the row are requested beside the row's
-    // count, speculatively (inside the row's A.n slots; lanes past the count
-    // are masked below), so a row of up to 64 kFillPre records costs one
-    // dependent round trip instead of one per 64 records.
-    constexpr int kFillPre = TEX ? 1 : 4;
-    int plx[kFillPre], prx[kFillPre], psh[kFillPre];
-    float plz[kFillPre], psz[kFillPre];
-#pragma unroll
-    for (int k = 0; k < kFillPre; ++k) {   // unconditional loads (index clamped into the row): no waits until used
-        const RowRec &mr = rr[min(64 * k + lane, A.n - 1)];
-        plx[k] = mr.lx; prx[k] = mr.rx; plz[k] = mr.lz; psz[k] = mr.sz; psh[k] = rec_shadow(mr);
-    }
     const int cnt = count[y];
+    const RowRec *rr = recs + (size_t)y * A.n;
     // 64 records per round trip: lane q loads record base+q (coalesced), a
     // ballot keeps those with a fragment in this segment, and the set bits are
     // walked in ascending order (= triangle order) with readlane broadcasts.
@@ -443,13 +431,7 @@ __global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec
         const int q = base + lane;
         int mlx = 0, mrx = 0, msh = 0, mtex = 0, midx = 0;
         float mlz = 0.f, msz = 0.f, mlX = 0.f, msX = 0.f, mlY = 0.f, msY = 0.f;
-        const int kb = base >> 6;
-        if (kb < kFillPre) {
-#pragma unroll
-            for (int k = 0; k < kFillPre; ++k)
-                if (k == kb) { mlx = plx[k]; mrx = prx[k]; mlz = plz[k]; msz = psz[k]; msh = psh[k]; }
-        }
-        if (q < cnt && (TEX || kb >= kFillPre)) {
+        if (q < cnt) {
             const RowRec &mr = rr[q];
             mlx = mr.lx; mrx = mr.rx; mlz = mr.lz; msz = mr.sz; msh = rec_shadow(mr);
             if (TEX) {

@@ -413,9 +413,11 @@ int cg_image_decode_jpeg_device(cg_ctx *ctx, const uint8_t *data, size_t n, uint
  * rast_fill_kernel and rast_post_kernel, on the stream it runs on, plus
  * "rt_big_frame" (a large scene's whole frame).  cg_kernel_timing(on)
  * resets the totals (process-wide); cg_kernel_time waits for the recorded
- * launches and returns the total milliseconds and launch count of one. */
+ * launches and returns one kernel's summed launch milliseconds, its busy
+ * milliseconds (the union of its launches' spans: launches that overlap on
+ * two streams count once) and its launch count. */
 int cg_kernel_timing(int enable);
-int cg_kernel_time(const char *kernel, double *total_ms, long long *launches);
+int cg_kernel_time(const char *kernel, double *total_ms, double *busy_ms, long long *launches);
 
 /* ---- starfield (starfield/Source/skeleton.cpp) -------------------------- */
 /* n stars as (x, y, z) float triples from glibc rand() (:41-46, seed 1). */
