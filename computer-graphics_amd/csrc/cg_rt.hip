@@ -611,6 +611,9 @@ __global__ __launch_bounds__(kRtThreads, kRtPixelWaves) void rt_pixel_kernel(RtF
 // are formed exactly as the reference forms them.
 // kLatTileW x kLatTileH = 16 x 15 pixels: 33 x 31 = 1023 lattice rays = 4 passes of 256 lanes
 constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1;
+#ifndef CG_LAT_INTERLEAVE
+#define CG_LAT_INTERLEAVE 1   // rt_lattice_kernel's points dealt to waves in 64-point chunks (A/B: 0)
+#endif
 constexpr int kLatWY = 3 * kLatTileW;   // per-pixel columns (a yawed camera): 48 x 31 = 1488 rays
 
 // Shared pieces of the two lattice kernels.
@@ -727,10 +730,11 @@ __device__ __forceinline__ void lat_store(const RtFrame &F, const LatTile &G, co
 template <int PITCH, class Store>
 __device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__restrict__ tc,
                                             const RtSphere *__restrict__ sph, unsigned long long mask, bool covered,
-                                            const LatTile &G, int p_lo, int p_hi, int lane, Store store)
+                                            const LatTile &G, int p_lo, int p_hi, int lane, Store store,
+                                            int step = 128)
 {
     constexpr int NP = 2;
-    for (int p0 = p_lo; p0 < p_hi; p0 += 64 * NP) {
+    for (int p0 = p_lo; p0 < p_hi; p0 += step) {
         float X[NP], Y[NP];
         bool live[NP];
         int pp[NP];
@@ -816,7 +820,16 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     // the needed points, walked row-major at the full pitch; wave w takes the
     // w-th quarter
     const int npts = PITCH * rows;
+#if CG_LAT_INTERLEAVE
+    // 64-point chunks dealt round-robin to the four waves (pass 1: pairs of
+    // chunks): hits and shadow tests are spatially clustered, so contiguous
+    // quarters leave some waves idle at the barrier.  Pass 2 walks the same
+    // points as the wave's pass 1 (no barrier between them).
+    const int p_lo = wave * 128, p_hi = npts, step1 = 512;
+#else
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
+    const int step1 = 128;
+#endif
     if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window: whole workgroup
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
     // sphere may be hit; bit 62: covered) and shadow mask for every hit the
@@ -837,10 +850,12 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     __syncthreads();                       // s_obj
     lat_closest<PITCH>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_pt[p] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
-    });
+    }, step1);
     // Pass 2: DirectLight of each lattice ray that hit (:151-153); shading
     // attributes from the LDS table
-    for (int p0 = p_lo; p0 < p_hi; p0 += 64) {
+    for (int pc = 0; p_lo + pc < p_hi; pc += 64) {
+        const int p0 = p_lo + (pc / 128) * step1 + (pc % 128);   // the chunks of this wave's pass 1
+        if (p0 >= p_hi) break;
         const int p = p0 + lane;
         const int cy = p / PITCH, cx = p - cy * PITCH, idx = p;
         if (p < p_hi && cx < cols) {
