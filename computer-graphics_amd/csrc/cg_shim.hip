@@ -767,7 +767,15 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                                     void *d_out, size_t stride, hipStream_t st, uint32_t *d_done)
 {
     if (!c->aux) {
-        CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
+        // the certificates are short and latency-bound: at a higher priority
+        // their workgroups are dispatched ahead of a running lattice launch's
+        // remaining ones (CG_AUX_PRIO=0: default priority, for A/B runs)
+        int lo = 0, hi = 0;
+        const char *pe = std::getenv("CG_AUX_PRIO");
+        if (!(pe && pe[0] == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+            CG_TRY(c, hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi), "aux stream");
+        else
+            CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
         for (int k = 0; k < 2; ++k) {
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_cert[k], hipEventDisableTiming), "aux event");
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_lat[k], hipEventDisableTiming), "aux event");
@@ -831,6 +839,16 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
            "rt_lattice launch");
     CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
     return CG_OK;
+}
+
+// A cold call's head batch: n_frames / CG_COLD_HEAD frames (at least 4; 0: no head batch).
+static int cold_head_div()
+{
+    static const int div = [] {
+        const char *e = std::getenv("CG_COLD_HEAD");
+        return e ? std::atoi(e) : 2;
+    }();
+    return div;
 }
 
 // Two large-scene frames in flight (default); CG_BIG_SLOTS=1 keeps one, for A/B runs.
@@ -926,13 +944,26 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
         }
         return CG_OK;
     }
-    for (int f0 = 0; f0 < n_frames; f0 += kMaxFrameBatch) {
-        const int nf = std::min(kMaxFrameBatch, n_frames - f0);
+    // A cold call (no earlier lattice launch of this context still running)
+    // would wait for all its frames' certificates before its first lattice
+    // launch.  It starts instead with a head batch: the head's certificates
+    // on the caller's stream, the rest's on the auxiliary stream beside the
+    // head's lattice launch (the pipelined path of later batches).
+    int head = 0;
+    {
+        const bool cold = !c->aux || (hipEventQuery(c->ev_lat[0]) == hipSuccess &&
+                                      hipEventQuery(c->ev_lat[1]) == hipSuccess);
+        const int div = cold_head_div();
+        if (cold && div > 0 && n_frames >= 8) head = std::max(4, n_frames / div);
+    }
+    for (int f0 = 0; f0 < n_frames;) {
+        const int nf = f0 == 0 && head ? head : std::min(kMaxFrameBatch, n_frames - f0);
         rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, out + (size_t)f0 * fbytes, stride, st,
                                       d_done ? d_done + f0 : nullptr);
         if (rc) return rc;
         if (d_done)
             for (int f = f0; f < f0 + nf; ++f) target[f] = (uint32_t)rt_lattice_tiles(F);
+        f0 += nf;
     }
     return CG_OK;
 }
