@@ -118,16 +118,20 @@ struct cg_ctx {
     bool big_ev_live = false;
     unsigned long long big_last[4] = {};
     long long big_overflows = 0;
-    // Large scenes, two frames in flight (rt_render_frames): slot 1's buffers,
-    // stream and demand read-back; slot 0 is tc / shade / big / frame /
-    // big_demand / big_ev above.  A frame's list building and walks are
-    // latency-bound phases; two independent frames fill each other's gaps.
-    DevBuf tc1, shade1, big1, frame1;
-    unsigned long long *big_demand1 = nullptr;
-    hipEvent_t big_ev1 = nullptr;
-    bool big_ev_live1 = false;
-    hipStream_t bst = nullptr;
-    hipEvent_t bev_start = nullptr, bev_end = nullptr;
+    // Large scenes, several frames in flight (rt_render_frames): slots 1 ..
+    // kBigSlots - 1 with their own buffers, stream and demand read-back; slot 0
+    // is tc / shade / big / frame / big_demand / big_ev above.  A frame's list
+    // building and walks are latency-bound phases; independent frames fill
+    // each other's gaps.
+    static constexpr int kBigSlots = 4;
+    struct ExtraSlot {
+        DevBuf tc, shade, big, frame;
+        unsigned long long *demand = nullptr;
+        hipEvent_t ev = nullptr, done = nullptr;
+        bool ev_live = false;
+        hipStream_t st = nullptr;
+    } xs[kBigSlots - 1];
+    hipEvent_t bev_start = nullptr;
     // the scene's box (rt_scene_box, once per cg_rt_set_scene): cg_dist's column
     // window of any camera from it in O(1) per frame -- no per-camera pass over
     // the scene (1M triangles: ~6 ms on the host) and no per-camera cache
@@ -285,16 +289,18 @@ extern "C" void cg_destroy(cg_ctx *c)
     }
     for (DevBuf *b : bufs) b->release();
     if (c->big_demand) (void)hipHostFree(c->big_demand);
-    if (c->bst) (void)hipStreamSynchronize(c->bst);
-    if (c->big_ev1) {
-        (void)hipEventSynchronize(c->big_ev1);
-        (void)hipEventDestroy(c->big_ev1);
+    for (auto &x : c->xs) {
+        if (x.st) (void)hipStreamSynchronize(x.st);
+        if (x.ev) {
+            (void)hipEventSynchronize(x.ev);
+            (void)hipEventDestroy(x.ev);
+        }
+        if (x.done) (void)hipEventDestroy(x.done);
+        if (x.demand) (void)hipHostFree(x.demand);
+        x.tc.release(); x.shade.release(); x.big.release(); x.frame.release();
+        if (x.st) (void)hipStreamDestroy(x.st);
     }
-    if (c->big_demand1) (void)hipHostFree(c->big_demand1);
-    c->tc1.release(); c->shade1.release(); c->big1.release(); c->frame1.release();
     if (c->bev_start) (void)hipEventDestroy(c->bev_start);
-    if (c->bev_end) (void)hipEventDestroy(c->bev_end);
-    if (c->bst) (void)hipStreamDestroy(c->bst);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
     for (int k = 0; k < cg_ctx::kRastLanes; ++k) {
         if (c->lanes[k]) cg_destroy(c->lanes[k]);
@@ -536,7 +542,10 @@ struct BigSlot {
 };
 static BigSlot big_slot(cg_ctx *c, int q)
 {
-    if (q) return BigSlot{&c->tc1, &c->shade1, &c->big1, &c->frame1, &c->big_demand1, &c->big_ev1, &c->big_ev_live1};
+    if (q) {
+        cg_ctx::ExtraSlot &x = c->xs[q - 1];
+        return BigSlot{&x.tc, &x.shade, &x.big, &x.frame, &x.demand, &x.ev, &x.ev_live};
+    }
     return BigSlot{&c->tc, &c->shade, &c->big, &c->frame, &c->big_demand, &c->big_ev, &c->big_ev_live};
 }
 
@@ -545,7 +554,7 @@ static bool big_observe(cg_ctx *c, bool sizing, int q);
 // Settle both slots' outstanding pool demand (blocks on their last frames).
 static int big_observe_all(cg_ctx *c)
 {
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < cg_ctx::kBigSlots; ++q) {
         const BigSlot b = big_slot(c, q);
         if (*b.ev_live) {
             CG_TRY(c, hipEventSynchronize(*b.ev), "pool demand");
@@ -560,7 +569,8 @@ extern "C" int cg_rt_scratch_info(cg_ctx *c, uint64_t *out)
     if (!c || !out) return CG_E_INVALID;
     if (int rc = big_observe_all(c)) return rc;
     const unsigned long long *d = c->big_last;
-    out[0] = c->big.bytes + c->big1.bytes;
+    out[0] = c->big.bytes;
+    for (const auto &x : c->xs) out[0] += x.big.bytes;
     out[1] = d[0] + d[1] + d[2] + d[3];
     out[2] = (uint64_t)(c->big_caps.sup + c->big_caps.bin + c->big_caps.sbin + c->big_caps.sorted);
     out[3] = (uint64_t)c->big_overflows;
@@ -681,7 +691,7 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
         c->big_sized = false;
     }
     if (c->big_fixed) c->big_sized = true;
-    for (int q = 0; q < 2; ++q) {   // either slot's finished frame reports its demand
+    for (int q = 0; q < cg_ctx::kBigSlots; ++q) {   // any slot's finished frame reports its demand
         const BigSlot b = big_slot(c, q);
         if (*b.ev_live && hipEventQuery(*b.ev) == hipSuccess) big_observe(c, false, q);
     }
@@ -841,14 +851,15 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
     return CG_OK;
 }
 
-// Two large-scene frames in flight (default); CG_BIG_SLOTS=1 keeps one, for A/B runs.
-static bool big_two_slots()
+// Large-scene frames in flight: 2 by default; CG_BIG_SLOTS = 1 .. kBigSlots for A/B runs.
+static int big_slots()
 {
-    static const bool on = [] {
+    static const int n = [] {
         const char *e = std::getenv("CG_BIG_SLOTS");
-        return !(e && e[0] == '1');
+        const int v = e ? std::atoi(e) : 2;
+        return std::max(1, std::min(v, cg_ctx::kBigSlots));
     }();
-    return on;
+    return n;
 }
 
 static size_t pix_bytes(int fmt) { return fmt == CG_PIX_RGB24 ? 3 : 4; }
@@ -899,19 +910,23 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
         batch = cams[f].focal == cams[0].focal && cams[f].indirect == cams[0].indirect &&
                 std::memcmp(cams[f].R, cams[0].R, sizeof(cams[0].R)) == 0;
     if (!batch) {
-        // Large scenes: consecutive frames alternate between two slots on two
-        // streams, two independent frames in flight (CG_BIG_SLOTS=1: one)
-        const bool two = n_frames > 1 && F.n_tris > 64 && F.cull_primary && F.cull_shadow && big_two_slots();
-        if (two) {
-            if (!c->bst) {
-                CG_TRY(c, hipStreamCreateWithFlags(&c->bst, hipStreamNonBlocking), "slot stream");
-                CG_TRY(c, hipEventCreateWithFlags(&c->bev_start, hipEventDisableTiming), "slot event");
-                CG_TRY(c, hipEventCreateWithFlags(&c->bev_end, hipEventDisableTiming), "slot event");
-            }
-            // slot 1 starts after what the caller queued before this call (the
-            // scene, the lights just uploaded on st)
+        // Large scenes: consecutive frames are dealt round-robin to big_slots()
+        // slots, each with its own buffers and stream: independent frames in flight
+        const int ns = (n_frames > 1 && F.n_tris > 64 && F.cull_primary && F.cull_shadow)
+                           ? std::min(big_slots(), n_frames) : 1;
+        if (ns > 1) {
+            if (!c->bev_start) CG_TRY(c, hipEventCreateWithFlags(&c->bev_start, hipEventDisableTiming), "slot event");
+            // the other slots start after what the caller queued before this
+            // call (the scene, the lights just uploaded on st)
             CG_TRY(c, hipEventRecord(c->bev_start, st), "slot event");
-            CG_TRY(c, hipStreamWaitEvent(c->bst, c->bev_start, 0), "slot wait");
+            for (int q = 1; q < ns; ++q) {
+                cg_ctx::ExtraSlot &x = c->xs[q - 1];
+                if (!x.st) {
+                    CG_TRY(c, hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking), "slot stream");
+                    CG_TRY(c, hipEventCreateWithFlags(&x.done, hipEventDisableTiming), "slot event");
+                }
+                CG_TRY(c, hipStreamWaitEvent(x.st, c->bev_start, 0), "slot wait");
+            }
         }
         for (int f = 0; f < n_frames; ++f) {
             if (f) {
@@ -919,8 +934,8 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
                 if (rc) return rc;
                 F.out_fmt = pix_format;
             }
-            const int q = two ? (f & 1) : 0;
-            hipStream_t fs = q ? c->bst : st;
+            const int q = f % ns;
+            hipStream_t fs = q ? c->xs[q - 1].st : st;
             rc = rt_enqueue(c, F, out + (size_t)f * fbytes, fs, q);
             if (rc) return rc;
             if (d_done) {
@@ -928,9 +943,10 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
                 target[f] = 1u;
             }
         }
-        if (two) {   // the call ends on the caller's stream
-            CG_TRY(c, hipEventRecord(c->bev_end, c->bst), "slot event");
-            CG_TRY(c, hipStreamWaitEvent(st, c->bev_end, 0), "slot wait");
+        for (int q = 1; q < ns; ++q) {   // the call ends on the caller's stream
+            cg_ctx::ExtraSlot &x = c->xs[q - 1];
+            CG_TRY(c, hipEventRecord(x.done, x.st), "slot event");
+            CG_TRY(c, hipStreamWaitEvent(st, x.done, 0), "slot wait");
         }
         return CG_OK;
     }

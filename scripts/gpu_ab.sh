@@ -16,16 +16,13 @@ step() {  # name timeout cmd...
   echo "== $name rc=$rc" | tee -a $OUT/ab_steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 "$OUT/ab_$name.log"; exit $rc; fi
 }
-step tests 300 python -u -m pytest tests/test_rt_gpu.py tests/test_dist_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread
-B="python bench.py --steps 20 --warmup 5 --no-sub --no-draw --no-cpu-baseline"
-for i in 1 2 3; do
-  step c2_head2_$i 120 $B
-  step c2_old_$i 120 env CG_COLD_HEAD=0 CG_AUX_PRIO=0 $B
-  step c2_head4_$i 120 env CG_COLD_HEAD=4 $B
-  step c2_prio_$i 120 env CG_COLD_HEAD=0 $B
+step tests 300 python -u -m pytest tests/test_rt_big_gpu.py tests/test_dist_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread
+for i in 1 2; do
+  for n in 1 2 3 4; do
+    step c5_slots${n}_$i 150 env CG_BIG_SLOTS=$n python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline
+  done
 done
-step c2long_new 150 python bench.py --steps 800 --warmup 32 --no-sub --no-draw --no-cpu-baseline --no-steady
-step c2long_old 150 env CG_COLD_HEAD=0 CG_AUX_PRIO=0 python bench.py --steps 800 --warmup 32 --no-sub --no-draw --no-cpu-baseline --no-steady
-step band_head2 200 python scripts/band_balanced.py 15 fixed
-step band_old 200 env CG_COLD_HEAD=0 CG_AUX_PRIO=0 python scripts/band_balanced.py 15 fixed
+step c5yaw_slots1 150 env CG_BIG_SLOTS=1 python bench.py --workload c5yaw --steps 20 --warmup 3 --no-cpu-baseline
+step c5yaw_slots2 150 env CG_BIG_SLOTS=2 python bench.py --workload c5yaw --steps 20 --warmup 3 --no-cpu-baseline
+step c5yaw_slots3 150 env CG_BIG_SLOTS=3 python bench.py --workload c5yaw --steps 20 --warmup 3 --no-cpu-baseline
 echo ab done
