@@ -75,15 +75,22 @@ sqs = sec.setdefault("sq_kernels", {})
 sqs[KERNEL] = sq
 if SECTION == "rt":
     out["rt"]["sq"] = sq
-# the whole frame: each kernel's mean lane-ops per dispatch x its dispatches per dispatch of
-# KERNEL (sizing passes and warm-up frames dispatch the same kernels), over KERNEL's frames
-n_dom = len(valu.get(KERNEL, [])) or 1
+# the whole frame: each kernel's median lane-ops per dispatch (a first frame's sizing passes
+# repeat the list kernels on the same frame) x its dispatches per dispatch of KERNEL.  The
+# dispatch ratios come from the longer kernel-trace run of the same workload when there is one
+# (gpurun_out/prof_<section>/<section>_kernel_stats.csv: 20+ frames dilute the sizing passes),
+# else from the counter passes themselves.
+calls = {}
+stats = os.path.join(ROOT, "gpurun_out", f"prof_{SECTION}", f"{SECTION}_kernel_stats.csv")
+if os.path.exists(stats):
+    for r in csv.DictReader(open(stats)):
+        calls[base_name(r["Name"])] = int(r["Calls"])
+n_dom = calls.get(KERNEL) or len(valu.get(KERNEL, [])) or 1
 kern = {}
 for k, v in sorted(valu.items()):
-    # the median dispatch (a first frame's sizing passes repeat the list kernels on the same
-    # frame) times its dispatches per dominant launch, rounded (2 for the per-frame scans)
+    n_k = calls.get(k, len(v)) if calls else len(v)
     kern[k] = {"valu_lane_ops_per_launch": 64.0 * sorted(v)[len(v) // 2],
-               "launches_per_frame_launch": max(1, round(len(v) / n_dom)), "code_sha256": code_sha256(k)}
+               "launches_per_frame_launch": max(1, round(n_k / n_dom)), "code_sha256": code_sha256(k)}
 per_frame = sum(r["valu_lane_ops_per_launch"] * r["launches_per_frame_launch"] for r in kern.values()) / FPL
 sec["frame_sq"] = {"dominant": KERNEL, "frames_per_launch": FPL, "kernels": kern,
                    "valu_lane_ops_per_frame": per_frame,
