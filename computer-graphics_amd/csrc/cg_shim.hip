@@ -777,15 +777,12 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_cam
                                     void *d_out, size_t stride, hipStream_t st, uint32_t *d_done)
 {
     if (!c->aux) {
-        // the certificates are short and latency-bound: at a higher priority
-        // their workgroups are dispatched ahead of a running lattice launch's
-        // remaining ones (CG_AUX_PRIO=0: default priority, for A/B runs)
-        int lo = 0, hi = 0;
-        const char *pe = std::getenv("CG_AUX_PRIO");
-        if (!(pe && pe[0] == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
-            CG_TRY(c, hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi), "aux stream");
-        else
-            CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
+        // default priority: a high-priority auxiliary stream (certificates
+        // dispatched ahead of a running lattice launch) gained ~2 % on
+        // back-to-back calls, but left the process's later streams sharing
+        // hardware queues -- the rasteriser's overlapped frames then ran
+        // serialised (C3 10.1-11.1k instead of 21.0-21.3k frames/s)
+        CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
         for (int k = 0; k < 2; ++k) {
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_cert[k], hipEventDisableTiming), "aux event");
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_lat[k], hipEventDisableTiming), "aux event");
@@ -951,7 +948,7 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
         return CG_OK;
     }
     // (A cold call split into a head batch, whose lattice launch runs beside
-    // the rest's certificates on the high-priority auxiliary stream, measured
+    // the rest's certificates on a high-priority auxiliary stream, measured
     // slower: 16.0k against 17.2k frames/s for the driver's 20-frame C2 call --
     // the certificates beside a lattice launch took 0.56 ms instead of 0.12.)
     for (int f0 = 0; f0 < n_frames;) {
