@@ -103,6 +103,10 @@ struct RtFrame {
     float lmin[3], lmax[3], lc[3];
     double lrho;
     float nbound;   // >= |component| of every hit normal (triangle normals; spheres <= 1 + 2^-20)
+    // Batched lattice launches (cg_rt.hip): workgroups only for tile columns tx0 .. tx0 + txn - 1,
+    // the columns the scene's box can be seen in over the batch's cameras; the edge workgroups
+    // store the other columns black.  txn 0: every tile column.
+    int tx0 = 0, txn = 0;
 };
 
 // ---- RAST --------------------------------------------------------------

@@ -108,6 +108,40 @@ __device__ __forceinline__ void lat_xrange(const RtFrame &F, const LatTile &A, c
 // the Cornell frame are the costliest, so starting them first leaves the
 // cheap ceiling tiles for the launch's tail.
 __device__ __forceinline__ int lat_tile_row() { return (int)(gridDim.y - 1 - blockIdx.y); }
+// Tile column of a lattice workgroup (launches over the window RtFrame::tx0 / txn), and the
+// frame's full tile-grid width (mask and unit-mask indices).
+__device__ __forceinline__ int lat_tile_col(const RtFrame &F) { return F.tx0 + (int)blockIdx.x; }
+__host__ __device__ __forceinline__ int lat_tiles_x(const RtFrame &F) { return (F.W + kLatTileW - 1) / kLatTileW; }
+
+#ifdef CG_WG_TIMING
+// Diagnostic build only (make OUT=_build_wgt EXTRA=-DCG_WG_TIMING): per-workgroup
+// wall-clock stamps (100 MHz) of the certificate and lattice kernels, read by
+// scripts/wg_timing.py.  Record: {kind << 56 | z << 40 | y << 20 | x, t0, t1, t2, t3}; kind 1
+// (certificates) in the first half of the buffer, kind 2 (lattice) in the second, unused
+// slots zero.
+__device__ unsigned long long *g_wgt;
+__device__ unsigned int g_wgt_n, g_wgt_cap;
+__device__ __forceinline__ void wgt_record(unsigned long long kind, unsigned long long t0, unsigned long long t1,
+                                           unsigned long long t2, unsigned long long t3)
+{
+    if (threadIdx.x != 0 || !g_wgt) return;
+    // a slot per workgroup (no shared counter: its atomics serialised the launch)
+    const unsigned s = (kind == 1 ? 0u : g_wgt_cap / 2) +
+                       (unsigned)(((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+    if (s >= (kind == 1 ? g_wgt_cap / 2 : g_wgt_cap)) return;
+    unsigned long long *r = g_wgt + 5ull * s;
+    r[0] = kind << 56 | (unsigned long long)blockIdx.z << 40 | (unsigned long long)blockIdx.y << 20 | blockIdx.x;
+    r[1] = t0;
+    r[2] = t1;
+    r[3] = t2;
+    r[4] = t3;
+}
+#define WGT_STAMP(v)          \
+    __syncthreads();          \
+    const unsigned long long v = wall_clock64()
+#else
+#define WGT_STAMP(v)
+#endif
 
 // Certificate units of a frame: tiles, or super-tiles of kSup x kSup tiles.
 __host__ __device__ __forceinline__ int rt_cert_units(const RtFrame &F, int sup)
@@ -349,9 +383,14 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
         prep_tri(tris, n, blockIdx.x * blockDim.x + threadIdx.x, frame, camf, tc_out, shade_out);
         return;
     }
-    const int unit = blockIdx.x - n_prep_blocks;
+#ifdef CG_WG_TIMING
+    const unsigned long long wt0 = wall_clock64();
+#endif
     const int tiles_x = (F.W + kLatTileW - 1) / kLatTileW, tiles_y = (F.rows_out + kLatTileH - 1) / kLatTileH;
     const int sx = (tiles_x + kSup - 1) / kSup;
+    // the launch's super-tile columns: those over the window's tiles (all when F.txn = 0)
+    const int s0 = F.txn ? F.tx0 / kSup : 0, sxw = F.txn ? (F.tx0 + F.txn + kSup - 1) / kSup - s0 : sx;
+    const int uw = blockIdx.x - n_prep_blocks, unit = (uw / sxw) * sx + s0 + uw % sxw;
     lat_masks += (size_t)frame * tiles_x * tiles_y * 2;
     __shared__ unsigned long long s_sup[2];
     if (!sup_masks) {
@@ -370,6 +409,7 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
         s_sup[1] = sm[1];
     }
     __syncthreads();
+    WGT_STAMP(wt1);
     const unsigned long long SP = s_sup[0], SS = s_sup[1];
     const unsigned long long SPt = SP & ~(1ull << 63), SSt = SS & ~(1ull << 63);
     const bool cert = F.cull_shadow && F.n_lights > 0;
@@ -464,6 +504,7 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
         }
     }
     __syncthreads();
+    WGT_STAMP(wt2);
     // Phase 2: shadow candidates (triangles of SS)
     const int nts = __popcll(SSt);
     const int sp = pow2_at_least(max(nts, 1)), tpi2 = 64 / sp;
@@ -492,6 +533,10 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
             lat_masks[2 * t + 1] = (live && pm != 0ull) ? (sm | (s_sphsh[tl] ? (1ull << 63) : 0ull)) : 0ull;
         }
     }
+#ifdef CG_WG_TIMING
+    WGT_STAMP(wt3);
+    wgt_record(1, wt0, wt1, wt2, wt3);
+#endif
 }
 
 
@@ -788,6 +833,36 @@ __device__ __forceinline__ void lat_store_black(const RtFrame &F, const LatTile 
     }
 }
 
+// A windowed launch (RtFrame::txn > 0): the first and last workgroup of each
+// tile row also store the output's columns left / right of the window black
+// -- no ray there can hit the scene's box (rt_box_columns), so those pixels
+// are PutPixelSDL(0, 0, 0) -- instead of a workgroup per black tile.
+__device__ __forceinline__ void lat_store_outside(const RtFrame &F, const LatTile &G, const LatOut &o)
+{
+    if (F.txn <= 0 || G.nv <= 0) return;
+    const bool left = blockIdx.x == 0, right = blockIdx.x == gridDim.x - 1;
+    if (!left && !right) return;
+    const uint32_t px = put_pixel(v3(0.0f, 0.0f, 0.0f));
+    for (int side = 0; side < 2; ++side) {
+        if (!(side ? right : left)) continue;
+        const int c0 = side ? max(o.wc0, (F.tx0 + F.txn) * kLatTileW) : o.wc0;
+        const int c1 = side ? o.wc0 + o.pitch : min(o.wc0 + o.pitch, F.tx0 * kLatTileW);
+        const int w = c1 - c0;
+        if (w <= 0) continue;
+        for (int i = threadIdx.x; i < w * G.nv; i += blockDim.x) {
+            const int r = i / w, col = c0 + (i - r * w);
+            if (F.out_fmt == CG_PIX_ARGB8888) {
+                o.out[(size_t)(G.L0 + r) * F.W + col] = px;
+            } else {
+                uint8_t *q = o.out8 + ((size_t)(G.L0 + r) * o.pitch + (col - o.wc0)) * 3;
+                q[0] = (uint8_t)px;
+                q[1] = (uint8_t)(px >> 8);
+                q[2] = (uint8_t)(px >> 16);
+            }
+        }
+    }
+}
+
 // blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
 // tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
 // out + frame * out_stride.
@@ -804,12 +879,13 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
 #pragma unroll
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
     tc += (size_t)frame * F.n_tris;
-    lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
+    lat_masks += (size_t)frame * lat_tiles_x(F) * gridDim.y * 2;
     const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int by = lat_tile_row();
-    LatTile G = lat_tile(F, blockIdx.x, by);
+    const int by = lat_tile_row(), bx = lat_tile_col(F);
+    LatTile G = lat_tile(F, bx, by);
     G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
+    lat_store_outside(F, G, o);
     const int ay0 = G.ay0, cols = G.cols, rows = G.rows;
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
     // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
@@ -834,7 +910,7 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
     // sphere may be hit; bit 62: covered) and shadow mask for every hit the
     // tile can produce
-    const size_t tix = (size_t)by * gridDim.x + blockIdx.x;
+    const size_t tix = (size_t)by * lat_tiles_x(F) + bx;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
     const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
@@ -983,18 +1059,19 @@ __device__ __forceinline__ bool lat_lights_tile(const RtFrame &F0, const RtTri *
 #pragma unroll
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
     tc += (size_t)frame * F.n_tris;
-    lat_masks += (size_t)frame * gridDim.x * gridDim.y * 2;
+    lat_masks += (size_t)frame * lat_tiles_x(F) * gridDim.y * 2;
     T.o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int by = lat_tile_row();
+    const int by = lat_tile_row(), bx = lat_tile_col(F);
     LatTile &G = T.G;
-    G = lat_tile(F, blockIdx.x, by);
+    G = lat_tile(F, bx, by);
     G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
+    if (store_black) lat_store_outside(F, G, T.o);
     lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
     const int npts = PITCH * G.rows;
     const int q = (npts + 3) / 4, p_lo = min(npts, wave * q), p_hi = min(npts, p_lo + q);
     if (G.u0 + G.nu <= T.o.wc0 || G.u0 >= T.o.wc0 + T.o.pitch) return false;   // outside the RGB24 window
-    T.tix = (size_t)by * gridDim.x + blockIdx.x;
+    T.tix = (size_t)by * lat_tiles_x(F) + bx;
     const unsigned long long m0 = uniform_u64(lat_masks[2 * T.tix]);
     const unsigned long long s0 = uniform_u64(lat_masks[2 * T.tix + 1]);
     const unsigned long long mask = m0 & ~(3ull << 62);
@@ -1111,7 +1188,7 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
     if (threadIdx.x < kLatParts * PITCH) {
         const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
         if (h < nhalf && cx < cols)
-            umask[((size_t)blockIdx.z * gridDim.x * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x] =
+            umask[((size_t)blockIdx.z * lat_tiles_x(F) * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x] =
                 s_umask[h][cx];
     }
 }
@@ -1156,7 +1233,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
             if (h < T.nhalf && cx < cols)
                 s_umask[h][cx] =
-                    umask[((size_t)blockIdx.z * gridDim.x * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x];
+                    umask[((size_t)blockIdx.z * lat_tiles_x(F) * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x];
         }
     }
     __syncthreads();
@@ -1295,8 +1372,15 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
                                                                   RtFrameCams cams, size_t out_stride,
                                                                   uint32_t *__restrict__ out, uint32_t *frame_done)
 {
+#ifdef CG_WG_TIMING
+    const unsigned long long wt0 = wall_clock64();
+#endif
     lattice_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
     lat_signal(frame_done, blockIdx.z);
+#ifdef CG_WG_TIMING
+    WGT_STAMP(wt3);
+    wgt_record(2, wt0, wt3, wt3, wt3);
+#endif
 }
 
 template <int PITCH>
@@ -1518,14 +1602,20 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         // (C2, 1/8 band, 20 frames, cold: 53.9 -> 28.7 us; 8 waves 49 us; a
         // whole frame's 10800 units stay at one wave: 85 us vs 106 with four)
         const int units = rt_cert_units(*F, 1);
-        const int tthreads = (size_t)units * nframes < 8192 ? 256 : 64;
         if (cert_fused()) {
+            // only the super-tiles over the launch's tile-column window (RtFrame::txn)
+            const int sx = (lat_tiles_x(*F) + kSup - 1) / kSup, sy = units / sx;
+            const int sxw = F->txn ? (F->tx0 + F->txn + kSup - 1) / kSup - F->tx0 / kSup : sx;
+            const int units_w = sy * sxw;
+            const int tthreads = (size_t)units_w * nframes < 8192 ? 256 : 64;
             const int tprep = (n + tthreads - 1) / tthreads;
             KtScope kt(KT_RT_TILE_CERT, st);
-            hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(tprep + units, nframes), dim3(tthreads), 0, st, d_tris, n,
+            hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(tprep + units_w, nframes), dim3(tthreads), 0, st, d_tris, n,
                                cams, Fl, d_sph, (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep);
             return hipGetLastError();
         }
+        Fl.txn = 0;   // the split form certifies every super-tile
+        const int tthreads = (size_t)units * nframes < 8192 ? 256 : 64;
         const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
         {
@@ -1606,7 +1696,7 @@ hipError_t launch_rt_lattice_units(const RtFrame &F, const RtTri *d_tc, const Rt
                                    const RtFrameCams &cams, int nframes, unsigned long long *d_umask, hipStream_t st)
 {
     if (F.n_lights <= 1) return hipSuccess;
-    const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
+    const dim3 grid(F.txn ? F.txn : lat_tiles_x(F), (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     KtScope kt(KT_RT_LATTICE_UNITS, st);
     if (lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_units_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
@@ -1622,8 +1712,9 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
                                     const unsigned long long *d_umask, const RtFrameCams &cams, int nframes,
                                     size_t out_stride, uint32_t *d_out, hipStream_t st, uint32_t *d_done)
 {
-    const dim3 grid((F.W + kLatTileW - 1) / kLatTileW, (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
+    const dim3 grid(F.txn ? F.txn : lat_tiles_x(F), (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     if (F.n_lights > 1 && !d_umask) return hipErrorInvalidValue;
+    if (F.txn && (F.tx0 < 0 || F.tx0 + F.txn > lat_tiles_x(F))) return hipErrorInvalidValue;
     KtScope kt(F.n_lights == 1 ? KT_RT_LATTICE : KT_RT_LATTICE_LIGHTS, st);
     if (F.n_lights == 1 && lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
@@ -1717,3 +1808,19 @@ hipError_t launch_rt_probe_direct_light(const RtFrame &F, const RtTri *d_tc,
 }
 
 }  // namespace cg
+
+#ifdef CG_WG_TIMING
+extern "C" int cg_diag_wg_timing(void *buf, unsigned cap)
+{
+    unsigned long long *p = (unsigned long long *)buf;
+    const unsigned zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgt), &p, sizeof p) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgt_cap), &cap, sizeof cap) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgt_n), &zero, sizeof zero) != hipSuccess) return -1;
+    return 0;
+}
+extern "C" int cg_diag_wg_count(unsigned *n)
+{
+    return hipMemcpyFromSymbol(n, HIP_SYMBOL(cg::g_wgt_n), sizeof *n) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -773,9 +773,42 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 
 // Frames f0 .. f0 + nf - 1 of a batch, one prepare + one lattice launch
 // (rt_use_lattice(F) holds for every frame; they differ only in cameraPos).
-static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F, const cg_rt_camera *cams, int nf,
-                                    void *d_out, size_t stride, hipStream_t st, uint32_t *d_done)
+static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_camera *cams, int nf,
+                                    void *d_out, size_t stride, hipStream_t st, uint32_t *d_done,
+                                    uint32_t *tiles_per_frame)
 {
+    // Workgroups only for the tile columns the scene's box can be seen in by
+    // some camera of the batch (O(1) per camera from the box, rt_box_columns);
+    // the launch's edge workgroups store the rest black.  C2: 73 of 120 tile
+    // columns -- the other 47 cost a workgroup each (~1.6 us) per tile row.
+    RtFrame F = F0;
+    static const bool window = [] {   // CG_LAT_WINDOW=0: every tile column (A/B runs)
+        const char *e = std::getenv("CG_LAT_WINDOW");
+        return !(e && e[0] == '0');
+    }();
+    if (window) {
+        int a = F.W, b = 0;
+        for (int f = 0; f < nf; ++f) {
+            int c0, c1;
+            ctx_rt_columns(c, &cams[f], &c0, &c1);
+            if (c0 < c1) {
+                a = std::min(a, c0);
+                b = std::max(b, c1);
+            }
+        }
+        const int tx = (F.W + kLatTileW - 1) / kLatTileW;
+        int t0 = a / kLatTileW, t1 = (b + kLatTileW - 1) / kLatTileW;
+        if (t0 >= t1) {   // nothing visible: one tile column (certified black) and the edges
+            t0 = 0;
+            t1 = 1;
+        }
+        if (t0 > 0 || t1 < tx) {
+            F.tx0 = t0;
+            F.txn = t1 - t0;
+        }
+    }
+    *tiles_per_frame = (uint32_t)((F.txn ? F.txn : (F.W + kLatTileW - 1) / kLatTileW) *
+                                  ((F.rows_out + kLatTileH - 1) / kLatTileH));
     if (!c->aux) {
         // default priority: a high-priority auxiliary stream (certificates
         // dispatched ahead of a running lattice launch) gained ~2 % on
@@ -953,11 +986,12 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
     // the certificates beside a lattice launch took 0.56 ms instead of 0.12.)
     for (int f0 = 0; f0 < n_frames;) {
         const int nf = std::min(kMaxFrameBatch, n_frames - f0);
+        uint32_t wg = 0;
         rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, out + (size_t)f0 * fbytes, stride, st,
-                                      d_done ? d_done + f0 : nullptr);
+                                      d_done ? d_done + f0 : nullptr, &wg);
         if (rc) return rc;
         if (d_done)
-            for (int f = f0; f < f0 + nf; ++f) target[f] = (uint32_t)rt_lattice_tiles(F);
+            for (int f = f0; f < f0 + nf; ++f) target[f] = wg;   // the launch's workgroups per frame
         f0 += nf;
     }
     return CG_OK;
