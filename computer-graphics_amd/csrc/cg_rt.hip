@@ -116,7 +116,8 @@ __host__ __device__ __forceinline__ int lat_tiles_x(const RtFrame &F) { return (
 #ifdef CG_WG_TIMING
 // Diagnostic build only (make OUT=_build_wgt EXTRA=-DCG_WG_TIMING): per-workgroup
 // wall-clock stamps (100 MHz) of the certificate and lattice kernels, read by
-// scripts/wg_timing.py.  Record: {kind << 56 | z << 40 | y << 20 | x, t0, t1, t2, t3}; kind 1
+// scripts/wg_timing.py.  Record: {kind << 56 | z << 40 | y << 20 | x, t0, t1, t2, t3, hardware
+// slot << 24 | blockIdx.x}; kind 1
 // (certificates) in the first half of the buffer, kind 2 (lattice) in the second, unused
 // slots zero.
 __device__ unsigned long long *g_wgt;
@@ -129,12 +130,15 @@ __device__ __forceinline__ void wgt_record(unsigned long long kind, unsigned lon
     const unsigned s = (kind == 1 ? 0u : g_wgt_cap / 2) +
                        (unsigned)(((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
     if (s >= (kind == 1 ? g_wgt_cap / 2 : g_wgt_cap)) return;
-    unsigned long long *r = g_wgt + 5ull * s;
+    unsigned long long *r = g_wgt + 6ull * s;
     r[0] = kind << 56 | (unsigned long long)blockIdx.z << 40 | (unsigned long long)blockIdx.y << 20 | blockIdx.x;
     r[1] = t0;
     r[2] = t1;
     r[3] = t2;
     r[4] = t3;
+    // the hardware slot: XCC_ID (hwreg 20, bits 3:0) and HW_ID (hwreg 4: wave, SIMD, CU, SH, SE)
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20), hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    r[5] = (unsigned long long)xcc << 56 | (unsigned long long)hw << 24 | blockIdx.x;
 }
 #define WGT_STAMP(v)          \
     __syncthreads();          \
@@ -315,9 +319,12 @@ __global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFram
     lat_masks += (size_t)frame * tiles * 2;
     const int tpw = n <= 31 ? 2 : 1, lpt = 64 / tpw;
     const int sub = lane / lpt, sl = lane - sub * lpt;
-    const int tile = (((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave) * tpw + sub;
-    if (__ballot(tile < tiles) == 0ull) return;   // whole wave
-    const bool tv = tile < tiles;
+    int tile = (((int)blockIdx.x - n_prep_blocks) * (kRtThreads / 64) + wave) * tpw + sub;
+    // single-level over a tile-column window (RtFrame::txn): the window's tiles only
+    const int units = (!sup && F.txn) ? F.txn * (tiles / lat_tiles_x(F)) : tiles;
+    if (__ballot(tile < units) == 0ull) return;   // whole wave
+    const bool tv = tile < units;
+    if (!sup && F.txn) tile = (tile / F.txn) * lat_tiles_x(F) + F.tx0 + tile % F.txn;
     unsigned long long m, sm;
     unit_cert(tris, n, camf, F, sph, tile, sup, tv, tpw, m, sm);
     if (tv && sl == 0) {
@@ -1586,6 +1593,12 @@ static bool cert_fused()
     return on;
 }
 
+static int env_int(const char *name, int dflt)
+{
+    const char *e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+}
+
 hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
                              RtShade *d_shade, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
                              unsigned long long *d_lat_masks, unsigned long long *d_sup_masks)
@@ -1594,7 +1607,21 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
     const int threads = kRtThreads, prep = (n + threads - 1) / threads;
     int cert = 0;
     RtFrame Fl{};
-    const int sup = d_sup_masks ? 1 : 0;
+    // A/B knobs: CG_CERT_SINGLE_MAX = window tiles x frames below which the tiles are certified
+    // in one level (measured slower for bands too: 182-217 vs 174-191 us); CG_CERT_THREADS
+    // forces the fused kernel's threads per super-tile.
+    static const int single_max = env_int("CG_CERT_SINGLE_MAX", 0);
+    static const int force_threads = env_int("CG_CERT_THREADS", 0);
+    // resident 4-wave workgroups of rt_tile_cert_kernel (4 waves per SIMD: 128 VGPRs)
+    static const int resident4 = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return cus * 4;
+    }();
+    const size_t wtiles = F ? (size_t)(F->txn ? F->txn : lat_tiles_x(*F)) * (rt_cert_units(*F, 0) / lat_tiles_x(*F)) : 0;
+    const int sup = (d_sup_masks && !(F && wtiles * nframes < (size_t)single_max)) ? 1 : 0;
     if (sup && F && d_lat_masks) {
         Fl = *F;
         // few super-tiles (a band of one rank): four waves per super-tile, so
@@ -1607,7 +1634,16 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             const int sx = (lat_tiles_x(*F) + kSup - 1) / kSup, sy = units / sx;
             const int sxw = F->txn ? (F->tx0 + F->txn + kSup - 1) / kSup - F->tx0 / kSup : sx;
             const int units_w = sy * sxw;
-            const int tthreads = (size_t)units_w * nframes < 8192 ? 256 : 64;
+            // waves per super-tile: as many as keep the call's super-tiles in one round of
+            // resident workgroups (a band: 4 or 2 waves shorten each super-tile's chain; a whole
+            // call: one wave per super-tile, 4,096 resident).  C2, 20 frames: bands of 90-188
+            // rows have 760-1,520 super-tiles (4 or 2 waves), the whole frame 6,840 (one wave:
+            // 105-110 us against 128 with four).
+            const size_t cnt = (size_t)units_w * nframes;
+            const int tthreads = force_threads ? force_threads
+                                 : cnt <= (size_t)resident4       ? 256
+                                 : cnt <= (size_t)resident4 * 2   ? 128
+                                                                  : 64;
             const int tprep = (n + tthreads - 1) / tthreads;
             KtScope kt(KT_RT_TILE_CERT, st);
             hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(tprep + units_w, nframes), dim3(tthreads), 0, st, d_tris, n,
@@ -1615,7 +1651,7 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             return hipGetLastError();
         }
         Fl.txn = 0;   // the split form certifies every super-tile
-        const int tthreads = (size_t)units * nframes < 8192 ? 256 : 64;
+        const int tthreads = (size_t)units * nframes <= (size_t)resident4 ? 256 : 64;
         const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
         {
@@ -1631,9 +1667,9 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
                            (RtShade *)nullptr, 0);
         return hipGetLastError();
     }
-    if (F && d_lat_masks) {   // single-level: every tile certified by rt_prepare_kernel
+    if (F && d_lat_masks) {   // single-level: every tile (of the window) certified by rt_prepare_kernel
         Fl = *F;
-        const int units = rt_cert_units(*F, 0);
+        const int units = (int)wtiles;
         const int tpw = n <= 31 ? 2 : 1;
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
     }

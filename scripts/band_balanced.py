@@ -4,8 +4,9 @@ each band rendered as cg_rt_render_frames_dist renders a rank's share (RGB24 row
 per cold call, median of N, measured (a) warm: calls back to back after warm-up, synchronised
 before each; (b) post-idle: the GPU idle 100 ms, one 5-frame warm-up call, then the timed call
 (bench.py's shape).  The N = 8 estimate is the slowest band plus a modelled tail: the last
-frame's band (RGB24) over one xGMI link at 50 GB/s, the other frames' transfers overlapping the
-render (the signalled pipeline).  Both with the metric's fixed camera and with a moving one
+frame's band (RGB24, the wire's visible columns) over one xGMI link at 50 GB/s, the other frames'
+transfers overlapping the render (the signalled pipeline); then the bands the bench's warm-up
+rebalance converges to from these times (cgdist.rebalance, twice), measured again.  Both with the metric's fixed camera and with a moving one
 (cameraPos.z = -3 + 0.005 k for frame k, the UP key at a twentieth of its stride): no figure
 may depend on a repeated camera.  Usage: python scripts/band_balanced.py [N] [fixed|moving]"""
 import ctypes
@@ -18,6 +19,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "computer-graphics_amd"))
 import cgamd  # noqa: E402
+import cgdist  # noqa: E402
 
 W, H, F, K = 1920, 1080, 1080.0, 20
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 15
@@ -65,14 +67,33 @@ with cgamd.Context(0) as ctx:
             idle.append(timed(shard, fmt))
         return {"warm_us": warm, "post_idle_us": sorted(idle)[len(idle) // 2]}
 
+    # the RGB24 wire carries the columns the scene's box can be seen in (cg_rt_frame_columns)
+    c0, c1 = cgamd.frame_columns(tris, n, sph, 1, cam)
+    res["wire_columns"] = [c0, c1]
+
+    def bands_run(bands):
+        out = []
+        for r0, rows in bands:
+            sh = cgamd.RtShard(row0=r0, rows=rows)
+            m = measure(ctypes.byref(sh), cgamd.PIX_RGB24)
+            m["tail_us_model"] = rows * (c1 - c0) * 3 / 50e9 * 1e6
+            out.append(m)
+        return out
+
     res["whole"] = measure(None, cgamd.PIX_ARGB8888)
-    res["band"] = []
-    for r0, rows in BANDS:
-        sh = cgamd.RtShard(row0=r0, rows=rows)
-        m = measure(ctypes.byref(sh), cgamd.PIX_RGB24)
-        m["tail_us_model"] = rows * W * 3 / 50e9 * 1e6
-        res["band"].append(m)
+    res["band"] = bands_run(BANDS)
     for cond in ("warm_us", "post_idle_us"):
         worst = max(b[cond] + b["tail_us_model"] for b in res["band"])
         res[f"n8_ratio_{cond[:-3]}"] = res["whole"][cond] / worst
+    # the bench's warm-up rebalance (cgdist.rebalance, as cg_dist_rebalance): twice from the
+    # measured band times, then the bands it converged to
+    bands = BANDS
+    for _ in range(2):
+        bands = [tuple(int(v) for v in b) for b in cgdist.rebalance(bands, [b["warm_us"] for b in res["band"]],
+                                                                  [0.0] * len(bands), H)]
+        res["band"] = bands_run(bands)
+    res["rebalanced_bands"] = bands
+    for cond in ("warm_us", "post_idle_us"):
+        worst = max(b[cond] + b["tail_us_model"] for b in res["band"])
+        res[f"n8_ratio_{cond[:-3]}_rebalanced"] = res["whole"][cond] / worst
 print(json.dumps(res, indent=1))

@@ -3,7 +3,8 @@ CGAMD_LIB=computer-graphics_amd/_build_wgt/libcgamd.so, built with
 `make OUT=_build_wgt EXTRA=-DCG_WG_TIMING`).  For the whole frame and for the bands of
 scripts/band_balanced.py, one cold call (GPU idle 100 ms, a 5-frame warm-up call, then the
 recorded call, as bench.py) and one warm call; every workgroup of rt_tile_cert_kernel (kind 1:
-entry, super-tile masks, phase 1, end) and rt_lattice_kernel (kind 2: entry, end) is written to
+entry, super-tile masks, phase 1, end) and rt_lattice_kernel (kind 2: entry, end; per tile when the
+launch draws tiles from queues) with its workgroup id is written to
 gpurun_out/wgt/<case>.npy, 100 MHz wall-clock stamps.  scripts/wg_analyze.py reads them.
 Usage: python scripts/wg_timing.py [band indices, default all]"""
 import ctypes
@@ -37,7 +38,7 @@ with cgamd.Context(0) as ctx:
     cams = (cgamd.RtCamera * 32)(*([cgamd.rt_camera(W, H, F)] * 32))
     lights = cgamd.default_lights()
     buf = torch.zeros(32 * H * W, dtype=torch.int32, device=dev)
-    rec = torch.zeros(CAP * 5, dtype=torch.int64, device=dev)
+    rec = torch.zeros(CAP * 6, dtype=torch.int64, device=dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
 
     def call(shard, fmt, nf):
@@ -61,7 +62,7 @@ with cgamd.Context(0) as ctx:
         torch.cuda.synchronize(dev)
         wall = (time.perf_counter() - t0) * 1e6
         assert lib.cg_diag_wg_timing(None, 0) == 0
-        r = rec.view(CAP, 5).cpu().numpy().view(np.uint64)
+        r = rec.view(CAP, 6).cpu().numpy().view(np.uint64)
         r = r[r[:, 1] != 0]
         m = len(r)
         np.save(os.path.join(OUT, f"{name}.npy"), r)
