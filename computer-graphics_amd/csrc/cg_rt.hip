@@ -1634,16 +1634,13 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             const int sx = (lat_tiles_x(*F) + kSup - 1) / kSup, sy = units / sx;
             const int sxw = F->txn ? (F->tx0 + F->txn + kSup - 1) / kSup - F->tx0 / kSup : sx;
             const int units_w = sy * sxw;
-            // waves per super-tile: as many as keep the call's super-tiles in one round of
-            // resident workgroups (a band: 4 or 2 waves shorten each super-tile's chain; a whole
-            // call: one wave per super-tile, 4,096 resident).  C2, 20 frames: bands of 90-188
-            // rows have 760-1,520 super-tiles (4 or 2 waves), the whole frame 6,840 (one wave:
-            // 105-110 us against 128 with four).
+            // waves per super-tile: four while the call's super-tiles fit one round of resident
+            // workgroups (a band: the latency of each super-tile's chain is the call's), else
+            // two.  C2, 20 frames: bands of 90-188 rows have 760-1,520 super-tiles (four waves
+            // 176-185 us per band call, two 169-190), the whole frame 6,840 (two waves 100-102
+            // us, one 105-111, four 128).
             const size_t cnt = (size_t)units_w * nframes;
-            const int tthreads = force_threads ? force_threads
-                                 : cnt <= (size_t)resident4       ? 256
-                                 : cnt <= (size_t)resident4 * 2   ? 128
-                                                                  : 64;
+            const int tthreads = force_threads ? force_threads : cnt <= (size_t)resident4 ? 256 : 128;
             const int tprep = (n + tthreads - 1) / tthreads;
             KtScope kt(KT_RT_TILE_CERT, st);
             hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(tprep + units_w, nframes), dim3(tthreads), 0, st, d_tris, n,
