@@ -306,6 +306,36 @@ def test_rt_render_frames_batched(rt, golden):
             assert np.array_equal(frame, singles[k]), (S, n, k)
 
 
+@pytest.mark.parametrize("nl", [1, 4])
+def test_rt_render_frames_lateral_windows(rt, nl):
+    """A batch's lattice launches cover only the union of its cameras' column windows (the
+    scene box's projection, cg_shim.hip rt_enqueue_lattice_batch): cameraPos moving sideways
+    -- windows at either edge, one camera that sees nothing at all (an empty window), one
+    centred -- rendered as one batched launch (the edge workgroups store the columns outside
+    the union black) == each frame rendered alone (no window), one light and a light set."""
+    torch = pytest.importorskip("torch")
+    W, H = 320, 256
+    xs = [-40.0, -1.6, -0.7, 0.0, 0.35, 1.1, 2.4, 40.0]
+    cams = [cgamd.rt_camera(W, H, 256.0, (x, 0.1 * k - 0.3, -3.0, 1.0)) for k, x in enumerate(xs)]
+    lights = cgamd.default_lights() if nl == 1 else cgamd.area_lights(cgamd.default_lights()[0], 0.1, 2)
+    singles = [rt.rt_render(c, lights)[0] for c in cams]
+    tris, n, sph = cgamd.rt_scene()
+    cols = [cgamd.frame_columns(tris, n, sph, 1, c) for c in cams]
+    assert cols[0][0] >= cols[0][1] and cols[-1][0] >= cols[-1][1]     # these two see nothing
+    assert not singles[0].any() or (singles[0] == singles[0][0]).all()  # a uniform (black) frame
+    assert any(0 < c0 < c1 < W for c0, c1 in cols)                     # a window inside the frame
+    g = torch.zeros(len(cams) * W * H, dtype=torch.int32, device="cuda")
+    st = torch.cuda.Stream()
+    for sel in (list(range(len(cams))), [1, 2], [0], [3, 7]):          # whole path, narrow unions, empty
+        sub = [cams[k] for k in sel]
+        g.zero_()
+        rt.rt_render_frames_device(sub, g.data_ptr(), None, st.cuda_stream, lights=lights)
+        st.synchronize()
+        got = g.cpu().numpy().view(np.uint32).reshape(len(cams), W * H)
+        for i, k in enumerate(sel):
+            assert np.array_equal(got[i], singles[k]), (sel, k)
+
+
 @pytest.mark.parametrize("window", [False, True])
 @pytest.mark.parametrize("kind", ["lattice", "yaw", "yaw_batch", "c4", "c4yaw"])
 def test_rt_bands_rgb24_assemble(rt, kind, window):
