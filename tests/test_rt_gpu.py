@@ -480,8 +480,8 @@ C4_FULL = dict(width=3840, height=2160, focal=2160.0, cam=[0, 0, -3.0, 1], R=Non
 def test_rt_c4_4k_soft_shadows_sampled(rt):
     """C4 at full size (3840x2160, f=2160, 8x8 area light = 64 lights): the
     whole GPU frame, 65,536 of its pixels checked bit-exactly against the
-    oracle (a full 4K oracle frame takes CPU-hours; the 480x270 C4 frame is
-    checked whole in test_rt_configs_match_golden)."""
+    oracle (the whole frame: test_rt_c4_4k_whole_frame_vs_oracle; the 480x270
+    C4 frame is checked whole in test_rt_configs_match_golden)."""
     cfg = C4_FULL
     W, H = cfg["width"], cfg["height"]
     argb, st = rt.rt_render(_cam(cfg), _lights(cfg))
@@ -491,6 +491,19 @@ def test_rt_c4_4k_soft_shadows_sampled(rt):
     bad = np.flatnonzero(got != ref)
     assert bad.size == 0, f"{bad.size} differ, first at {xy[bad[:4]]}: gpu {got[bad[:4]]} ref {ref[bad[:4]]}"
     assert (got >> 24 == 0x80).all()
+
+
+def test_rt_c4_4k_whole_frame_vs_oracle(rt):
+    """C4 at full size, every one of the 8,294,400 pixels bit-exact against the oracle (about
+    5 CPU-minutes of oracle work: ~20 s on the GPU box's 16 usable cores)."""
+    cfg = C4_FULL
+    W, H = cfg["width"], cfg["height"]
+    argb, _ = rt.rt_render(_cam(cfg), _lights(cfg))
+    yy, xx = np.mgrid[0:H, 0:W]
+    xy = np.stack([xx.ravel(), yy.ravel()], 1).astype(np.int32)
+    ref = oracle.rt_draw_pixels(mg.rt_params_of(cfg), xy, threads=min(16, os.cpu_count() or 8))
+    bad = np.flatnonzero(argb != ref)
+    assert bad.size == 0, f"{bad.size} differ, first at {xy[bad[:4]]}: gpu {argb[bad[:4]]} ref {ref[bad[:4]]}"
 
 
 def test_rt_c4_sharded_matches_whole(rt):
