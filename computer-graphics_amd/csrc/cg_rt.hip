@@ -380,14 +380,17 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
                                                            const unsigned long long *__restrict__ sup_masks,
                                                            unsigned long long *__restrict__ lat_masks,
                                                            RtTri *__restrict__ tc_out, RtShade *__restrict__ shade_out,
-                                                           int n_prep_blocks)
+                                                           int n_prep_blocks, int frame_fast)
 {
     constexpr int kT = kSup * kSup;
-    const int frame = blockIdx.y, lane = threadIdx.x & 63;
+    // frame_fast: blockIdx.x = frame (dispatched fastest), blockIdx.y = prep block, then
+    // super-tile; else the other way round (grids beyond 65,535 blocks in y)
+    const int frame = frame_fast ? blockIdx.x : blockIdx.y, blk = frame_fast ? blockIdx.y : blockIdx.x;
+    const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
-    if ((int)blockIdx.x < n_prep_blocks) {
-        prep_tri(tris, n, blockIdx.x * blockDim.x + threadIdx.x, frame, camf, tc_out, shade_out);
+    if (blk < n_prep_blocks) {
+        prep_tri(tris, n, blk * blockDim.x + threadIdx.x, frame, camf, tc_out, shade_out);
         return;
     }
 #ifdef CG_WG_TIMING
@@ -397,7 +400,11 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
     const int sx = (tiles_x + kSup - 1) / kSup;
     // the launch's super-tile columns: those over the window's tiles (all when F.txn = 0)
     const int s0 = F.txn ? F.tx0 / kSup : 0, sxw = F.txn ? (F.tx0 + F.txn + kSup - 1) / kSup - s0 : sx;
-    const int uw = blockIdx.x - n_prep_blocks, unit = (uw / sxw) * sx + s0 + uw % sxw;
+    // super-tile rows bottom first, each row's super-tiles for every frame of the launch in turn:
+    // the floor and box rows carry the longest certificate chains (up to 3x the median), and
+    // dispatched last they set the launch's tail (C2, 20 frames: 107 -> 84 us simulated)
+    const int sy = (tiles_y + kSup - 1) / kSup, ud = blk - n_prep_blocks;
+    const int uw = (sy - 1 - ud / sxw) * sxw + ud % sxw, unit = (uw / sxw) * sx + s0 + uw % sxw;
     lat_masks += (size_t)frame * tiles_x * tiles_y * 2;
     __shared__ unsigned long long s_sup[2];
     if (!sup_masks) {
@@ -1635,16 +1642,19 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             const int sxw = F->txn ? (F->tx0 + F->txn + kSup - 1) / kSup - F->tx0 / kSup : sx;
             const int units_w = sy * sxw;
             // waves per super-tile: four while the call's super-tiles fit one round of resident
-            // workgroups (a band: the latency of each super-tile's chain is the call's), else
-            // two.  C2, 20 frames: bands of 90-188 rows have 760-1,520 super-tiles (four waves
-            // 176-185 us per band call, two 169-190), the whole frame 6,840 (two waves 100-102
-            // us, one 105-111, four 128).
+            // workgroups (a band: the latency of each super-tile's chain is the call's), else one
+            // (throughput: the bottom-first order keeps the long chains off the tail).  C2, 20
+            // frames: bands of 90-188 rows have 760-1,520 super-tiles (four waves 176-185 us per
+            // band call, two 169-190), the whole frame 6,840 (one wave 77-78 us, two 88, four
+            // 128; in the raster order one wave took 105-111, two 100-105).
             const size_t cnt = (size_t)units_w * nframes;
-            const int tthreads = force_threads ? force_threads : cnt <= (size_t)resident4 ? 256 : 128;
+            const int tthreads = force_threads ? force_threads : cnt <= (size_t)resident4 ? 256 : 64;
             const int tprep = (n + tthreads - 1) / tthreads;
             KtScope kt(KT_RT_TILE_CERT, st);
-            hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(tprep + units_w, nframes), dim3(tthreads), 0, st, d_tris, n,
-                               cams, Fl, d_sph, (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep);
+            const int ff = tprep + units_w <= 65535;
+            const dim3 cg = ff ? dim3(nframes, tprep + units_w) : dim3(tprep + units_w, nframes);
+            hipLaunchKernelGGL(rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, n, cams, Fl, d_sph,
+                               (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep, ff);
             return hipGetLastError();
         }
         Fl.txn = 0;   // the split form certifies every super-tile
@@ -1659,9 +1669,10 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         KtScope kt(KT_RT_TILE_CERT, st);
-        hipLaunchKernelGGL(rt_tile_cert_kernel, dim3(units, nframes), dim3(tthreads), 0, st, d_tris, n, cams, Fl,
-                           d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks, (RtTri *)nullptr,
-                           (RtShade *)nullptr, 0);
+        const int ff = units <= 65535;
+        hipLaunchKernelGGL(rt_tile_cert_kernel, ff ? dim3(nframes, units) : dim3(units, nframes), dim3(tthreads), 0, st,
+                           d_tris, n, cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks,
+                           (RtTri *)nullptr, (RtShade *)nullptr, 0, ff);
         return hipGetLastError();
     }
     if (F && d_lat_masks) {   // single-level: every tile (of the window) certified by rt_prepare_kernel
