@@ -1107,11 +1107,41 @@ __device__ __forceinline__ float lat_y(const RtFrame &F, int Yi)
 }
 
 // K1: closest hits of every ray slot of the tile.
+#ifdef CG_WG_TIMING
+// Diagnostic build only: per-wave wall-clock stamps (100 MHz) of the walk (kind 3) and the
+// shadow hints (kind 4), read by scripts/wg_timing_c5.py.  Record as cg_rt.hip's wgt_record,
+// one per wave.
+__device__ unsigned long long *g_wgtb;
+__device__ unsigned int g_wgtb_cap;
+__device__ __forceinline__ void wgtb_record(unsigned long long kind, unsigned long long t0)
+{
+    const unsigned long long t1 = wall_clock64();
+    if ((threadIdx.x & 63) || !g_wgtb) return;
+    const unsigned long long s = (kind == 3 ? 0ull : g_wgtb_cap / 2) +
+                                 ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (s >= (kind == 3 ? g_wgtb_cap / 2 : g_wgtb_cap)) return;
+    unsigned long long *r = g_wgtb + 6ull * s;
+    r[0] = kind << 56 | (unsigned long long)blockIdx.y << 20 | ((unsigned long long)blockIdx.x * 4 + (threadIdx.x >> 6));
+    r[1] = t0;
+    r[2] = t1;
+    r[3] = t1;
+    r[4] = t1;
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20), hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    r[5] = (unsigned long long)xcc << 56 | (unsigned long long)hw << 24 | blockIdx.x;
+}
+#define WGTB_T0 const unsigned long long wgtb_t0 = wall_clock64()
+#define WGTB_END(k) wgtb_record(k, wgtb_t0)
+#else
+#define WGTB_T0
+#define WGTB_END(k)
+#endif
+
 template <int LM>   // 0: per-pixel mode, 1: lattice, 2: lattice with per-pixel columns
 __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                     const RtShade *__restrict__ shade,
                                                                     const RtSphere *__restrict__ sph, BigBufs B)
 {
+    WGTB_T0;
     constexpr bool kLat = LM > 0;
     constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1319,6 +1349,7 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
         W.pn = wave_max(sb.pn);
         if (lane == 0) B.wave_box[(size_t)ty * B.tiles_x + tx] = W;
     }
+    WGTB_END(3);
 }
 
 // K2: union of the wave boxes of each bin (one wave tile per lane).
@@ -1510,6 +1541,7 @@ __global__ __launch_bounds__(kRtThreads, 6) void rt_shadow_hints_kernel(RtFrame 
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
 {
+    WGTB_T0;
     constexpr bool kLat = LM > 0;
     constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1621,6 +1653,7 @@ __global__ __launch_bounds__(kRtThreads, 6) void rt_shadow_hints_kernel(RtFrame 
         B.sh_bits[pix] = shadowed;
         B.pend_bits[pix] = pending;
     }
+    WGTB_END(4);
 }
 
 // ---------------------------------------------------------------------------
@@ -2286,3 +2319,13 @@ size_t rt_big_scratch_bytes(const RtFrame &F, const BigCaps &caps)
 }
 
 }  // namespace cg
+
+#ifdef CG_WG_TIMING
+extern "C" int cg_diag_wg_timing_big(void *buf, unsigned cap)
+{
+    unsigned long long *p = (unsigned long long *)buf;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgtb), &p, sizeof p) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgtb_cap), &cap, sizeof cap) != hipSuccess) return -1;
+    return 0;
+}
+#endif
