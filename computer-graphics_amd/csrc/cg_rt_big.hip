@@ -115,6 +115,7 @@ struct BigBufs {
     long long cap_sup, cap_bin, cap_sbin, cap_sorted;  // pool capacities (entries)
     int *sup_over, *bin_over, *sbin_over;              // [n_sups], [n_bins], [n_bins]: list overflowed
     float *tile_bb;               // [2 n_bins][32][4]: each half-bin's wave-tile bundles (rt_half_mask_kernel)
+    int *walk_order;              // [tiles]: the walk's workgroups, longest half-bin list first (null: grid order)
 };
 
 // ---------------------------------------------------------------------------
@@ -1136,6 +1137,45 @@ __device__ __forceinline__ void wgtb_record(unsigned long long kind, unsigned lo
 #define WGTB_END(k)
 #endif
 
+// The walk's workgroup order: a workgroup (4 wave tiles of one half-bin) is
+// keyed by its half-bin's sorted list length, the walk's work per ray slot;
+// one workgroup counting-sorts the gx * gy keys, longest first (64 classes
+// linear in the longest list; ties in any order -- the order only schedules
+// the walk, every workgroup's pixels are its own).
+__global__ __launch_bounds__(1024) void rt_walk_order_kernel(BigBufs B, int gx, int gy)
+{
+    __shared__ int s_cnt[64], s_max;
+    const int n = gx * gy, t = threadIdx.x;
+    auto key = [&](int w) {
+        const int tx = (w % gx) * (kRtTileW / 8), ty = w / gx;
+        const int bin = (tx / kBinTilesX) + (ty / kBinTilesY) * B.bins_x;
+        const int sub = 2 * bin + ((tx % kBinTilesX) < kBinTilesX / 2 ? 0 : 1);
+        const int *o = B.bkt_off + sub * (kDepthBuckets + 1);
+        return o[kDepthBuckets] - o[0];
+    };
+    if (t < 64) s_cnt[t] = 0;
+    if (t == 0) s_max = 0;
+    __syncthreads();
+    int mx = 0;
+    for (int w = t; w < n; w += 1024) mx = max(mx, key(w));
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    const long long top = (long long)s_max + 1;
+    auto cls = [&](int w) { return 63 - (int)((long long)key(w) * 64 / top); };   // 0 = longest
+    for (int w = t; w < n; w += 1024) atomicAdd(&s_cnt[cls(w)], 1);
+    __syncthreads();
+    if (t == 0) {
+        int a = 0;
+        for (int c = 0; c < 64; ++c) {
+            const int x = s_cnt[c];
+            s_cnt[c] = a;
+            a += x;
+        }
+    }
+    __syncthreads();
+    for (int w = t; w < n; w += 1024) B.walk_order[atomicAdd(&s_cnt[cls(w)], 1)] = w;
+}
+
 template <int LM>   // 0: per-pixel mode, 1: lattice, 2: lattice with per-pixel columns
 __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                     const RtShade *__restrict__ shade,
@@ -1145,7 +1185,13 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
     constexpr bool kLat = LM > 0;
     constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (B.walk_order) {   // heavy-first (rt_walk_order_kernel): the long lists start early, not in the tail
+        const int w = __builtin_amdgcn_readfirstlane(B.walk_order[blockIdx.y * gridDim.x + blockIdx.x]);
+        bx = w % (int)gridDim.x;
+        by = w / (int)gridDim.x;
+    }
+    const int tx = bx * (kRtTileW / 8) + wave, ty = by;
     if (tx >= B.tiles_x) return;
     const float m = 0.5f;
     // slot directions: per-pixel mode dir +- m (i, j); lattice mode rx / ry
@@ -2030,7 +2076,7 @@ size_t big_scratch_bytes(const BigBufs &B, const RtFrame &F)
            big_slots(B, F) * 8 + 2 * big_words(B, F) * 8 + (size_t)kMaxPend * sizeof(PendRay) +
            (size_t)F.n_tris * 4 + (sups + 2 * bins) * B.nch * sizeof(Chunk) + (sups + bins) * (B.nch + 2) * 4 +
            (size_t)B.cap_sup * 2 * (4 + 8) + (size_t)B.cap_sbin * 4 + (size_t)B.cap_bin * 6 * 8 + (size_t)B.cap_sorted * 2 * 8 +
-           8 * 64;
+           tiles * 4 + 9 * 64;
 }
 void big_carve(BigBufs &B, const RtFrame &F, void *base)
 {
@@ -2056,6 +2102,8 @@ void big_carve(BigBufs &B, const RtFrame &F, void *base)
     align();
     B.wave_box = (ShadowBox *)p; p += tiles * sizeof(ShadowBox);
     B.bin_box = (ShadowBox *)p;  p += bins * sizeof(ShadowBox);
+    align();
+    B.walk_order = (int *)p;     p += tiles * 4;
     align();
     B.hit_bi = (int *)p;   p += slots * 4;
     B.hit_t = (float *)p;  p += slots * 4;
@@ -2155,6 +2203,11 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     hipLaunchKernelGGL(rt_half_tiles_kernel, dim3(2 * bins), dim3(64), 0, st, F, B);
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
     hipLaunchKernelGGL(rt_half_mask_kernel, dim3(2048), dim3(256), 0, st, F, d_tc, B);
+    {
+        const char *wo = std::getenv("CG_WALK_ORDER");
+        if (wo && wo[0] == '0') B.walk_order = nullptr;
+        else hipLaunchKernelGGL(rt_walk_order_kernel, dim3(1), dim3(1024), 0, st, B, (int)pgrid.x, (int)pgrid.y);
+    }
     {
         KtScope kt(KT_RT_BIG_PRIMARY, st);
         if (lat && B.lat_yaw)

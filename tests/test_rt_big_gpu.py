@@ -126,6 +126,19 @@ def test_big_scene_modes_match_oracle(big, case, stress):
         assert info["overflows"] == 0 and info["capacity"] <= 2 * info["listed"] + 5 * 4096, info
 
 
+@pytest.mark.parametrize("case", ["lat_1", "pix_pitch_1", "inside_lat_wide"])
+def test_big_walk_order_does_not_change_pixels(big, case, monkeypatch):
+    """The walk's heavy-first workgroup order (rt_walk_order_kernel) only
+    schedules it: grid order (CG_WALK_ORDER=0) renders the same frame, and
+    both equal the oracle."""
+    cfg = _cfg(case)
+    ordered = _render(big, cfg)
+    monkeypatch.setenv("CG_WALK_ORDER", "0")
+    grid = _render(big, cfg)
+    assert np.array_equal(ordered, grid)
+    assert np.array_equal(ordered, _oracle(case))
+
+
 def _degenerate_scene(n=500, around_eye=False):
     """random_scene(n) with edge-case triangles written over its first ones:
     a point, two collinear forms, a repeated vertex, a sliver, a 10 x 10
