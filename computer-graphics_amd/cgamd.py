@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGAMD_LIB") or os.path.join(HERE, "_build", "libcgamd.so")
 
-CG_OK, CG_E_INVALID, CG_E_NODEVICE, CG_E_HIP, CG_E_NOSCENE, CG_E_CAPACITY = 0, -1, -2, -3, -4, -5
+CG_OK, CG_E_INVALID, CG_E_NODEVICE, CG_E_HIP, CG_E_NOSCENE, CG_E_CAPACITY, CG_E_TIMEOUT = 0, -1, -2, -3, -4, -5, -6
 
 
 class Vec3(C.Structure):
@@ -142,6 +142,9 @@ _SIGS = {
     "cg_rast_draw_frames_device": (C.c_int, [P, C.POINTER(RastParams), C.c_int, P, P, P, C.c_size_t, P]),
     "cg_dist_unique_id": (C.c_int, [P]),
     "cg_dist_create": (C.c_int, [P, C.c_int, C.c_int, P, C.POINTER(P)]),
+    "cg_dist_create_timed": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.POINTER(P)]),
+    "cg_dist_set_timeout": (C.c_int, [P, C.c_int]),
+    "cg_dist_wait": (C.c_int, [P, P]),
     "cg_dist_create_local": (C.c_int, [C.POINTER(P), C.c_int, C.POINTER(P)]),
     "cg_dist_destroy": (None, [P]),
     "cg_dist_set_bands": (C.c_int, [P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
@@ -409,20 +412,42 @@ def band_partition_native(row_cost, nranks, overhead=None):
     return [(r0[r], rs[r]) for r in range(nranks)]
 
 
+class DistTimeout(RuntimeError):
+    """A multi-GPU wait passed its deadline (CG_E_TIMEOUT); the communicator was aborted."""
+
+
 class Dist:
     """Multi-GPU raytracer frames (cg_dist_*): one rank's handle.  Dist(ctx,
     nranks, rank, id) joins an RCCL communicator; Dist.local(ctxs) builds an
     in-process group (tests) and returns one handle per rank."""
 
-    def __init__(self, ctx, nranks=1, rank=0, uid: bytes = None, _handle=None):
+    def __init__(self, ctx, nranks=1, rank=0, uid: bytes = None, _handle=None, timeout_ms=0):
+        """timeout_ms: deadline of every host wait on this handle, init included (0: the
+        library's default, CG_DIST_TIMEOUT_MS or 60 s); a passed deadline raises
+        DistTimeout after the library aborted the communicator."""
         self.ctx, self.lib, self.nranks, self.rank = ctx, ctx.lib, nranks, rank
         if _handle is not None:
             self.h = _handle
             return
         h = P()
         idb = (C.c_char * DIST_ID_BYTES).from_buffer_copy(uid)
-        ctx._check(self.lib.cg_dist_create(ctx.h, nranks, rank, idb, C.byref(h)), "cg_dist_create")
+        self._check(self.lib.cg_dist_create_timed(ctx.h, nranks, rank, idb, int(timeout_ms), C.byref(h)),
+                    "cg_dist_create")
         self.h = h
+
+    def _check(self, rc, what):
+        if rc == CG_E_TIMEOUT:
+            msg = self.lib.cg_last_error(self.ctx.h)
+            raise DistTimeout(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        self.ctx._check(rc, what)
+
+    def set_timeout(self, ms):
+        self._check(self.lib.cg_dist_set_timeout(self.h, int(ms)), "cg_dist_set_timeout")
+
+    def wait(self, stream=None):
+        """cg_dist_wait: bounded host wait for this rank's enqueued work (raises on a
+        timeout or an RCCL error, after the library aborted the communicator)."""
+        self._check(self.lib.cg_dist_wait(self.h, P(stream) if stream else None), "cg_dist_wait")
 
     @classmethod
     def local(cls, ctxs):
@@ -456,19 +481,19 @@ class Dist:
         self.ctx._check(self.lib.cg_dist_set_pipeline(self.h, mode), "cg_dist_set_pipeline")
 
     def rebalance(self):
-        self.ctx._check(self.lib.cg_dist_rebalance(self.h), "cg_dist_rebalance")
+        self._check(self.lib.cg_dist_rebalance(self.h), "cg_dist_rebalance")
 
     def last_times(self):
         """(render ms per frame, assembly ms per frame) of this rank's last call."""
         a, b = C.c_double(), C.c_double()
-        self.ctx._check(self.lib.cg_dist_last_times(self.h, C.byref(a), C.byref(b)), "cg_dist_last_times")
+        self._check(self.lib.cg_dist_last_times(self.h, C.byref(a), C.byref(b)), "cg_dist_last_times")
         return a.value, b.value
 
     def render_frames(self, cams, d_frames, stream=None, lights=None, frame_stride=0):
         """cg_rt_render_frames_dist: len(cams) frames, assembled on rank 0 at d_frames."""
         lights = default_lights() if lights is None else lights
         arr = (RtCamera * len(cams))(*cams)
-        self.ctx._check(self.lib.cg_rt_render_frames_dist(self.h, lights, len(lights), arr, len(cams),
+        self._check(self.lib.cg_rt_render_frames_dist(self.h, lights, len(lights), arr, len(cams),
                                                           P(d_frames) if d_frames else None, frame_stride,
                                                           P(stream) if stream else None),
                         "cg_rt_render_frames_dist")
@@ -542,17 +567,19 @@ class Context:
                                           out.ctypes.data_as(P), C.byref(st)), "cg_rt_render")
         return out, st
 
-    def rt_render_frames(self, cams, out=None, chunk=0, lights=None):
-        """cg_rt_render_frames: len(cams) frames into host memory `out` (uint32, len(cams) * W * H;
-        pageable or pinned, allocated pageable when None), downloads overlapped with later renders."""
+    def rt_render_frames(self, cams, out=None, chunk=0, lights=None, frame_stride=0):
+        """cg_rt_render_frames: len(cams) frames into host memory `out` at f * frame_stride pixels
+        (uint32; pageable or pinned, allocated pageable when None; frame_stride 0 = W * H),
+        downloads overlapped with later renders."""
         lights = default_lights() if lights is None else lights
         arr = (RtCamera * len(cams))(*cams)
         npx = cams[0].width * cams[0].height
+        stride = frame_stride or npx
         if out is None:
-            out = np.zeros(len(cams) * npx, np.uint32)
+            out = np.zeros(len(cams) * stride, np.uint32)
         ptr = out.ctypes.data if isinstance(out, np.ndarray) else out.data_ptr()
         st = Stats()
-        self._check(self.lib.cg_rt_render_frames(self.h, lights, len(lights), arr, len(cams), P(ptr), npx, chunk,
+        self._check(self.lib.cg_rt_render_frames(self.h, lights, len(lights), arr, len(cams), P(ptr), stride, chunk,
                                                  C.byref(st)), "cg_rt_render_frames")
         return out, st
 

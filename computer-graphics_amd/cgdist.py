@@ -106,11 +106,12 @@ def rebalance(bands, render_s, overhead_s, height: int):
     return band_partition(cost, len(bands), overhead_s)
 
 
-def join(ctx, group=None, chunk=None):
+def join(ctx, group=None, chunk=None, timeout_ms=0):
     """This process's cgamd.Dist in the torch.distributed world (one process
     per GPU): rank 0 creates the RCCL id (cg_dist_unique_id) and it travels
-    over the existing process group; cg_dist_create then joins the library's
-    own RCCL communicator on ctx's device."""
+    over the existing process group; cg_dist_create_timed then joins the
+    library's own RCCL communicator on ctx's device (non-blocking, every host
+    wait bounded by timeout_ms; 0 = the library's default)."""
     import torch
     import torch.distributed as dist
 
@@ -121,7 +122,7 @@ def join(ctx, group=None, chunk=None):
     if rank == 0:
         t.copy_(torch.tensor(list(cgamd.dist_unique_id()), dtype=torch.uint8))
     dist.broadcast(t, src=0, group=group)
-    d = cgamd.Dist(ctx, world, rank, bytes(t.cpu().tolist()))
+    d = cgamd.Dist(ctx, world, rank, bytes(t.cpu().tolist()), timeout_ms=timeout_ms)
     if chunk:
         d.set_chunk(chunk)
     return d

@@ -24,12 +24,27 @@
 //
 // Transports: RCCL (cg_dist_create) or, for tests, an in-process group of
 // contexts whose bands move by device-to-device copies (cg_dist_create_local).
+//
+// Bounded failure: the communicator is non-blocking (ncclConfig_t.blocking =
+// 0), so no RCCL call blocks the host; every host wait of this file (init,
+// the rebalance's collectives, cg_dist_wait, destroy) polls completion and
+// ncclCommGetAsyncError against a deadline (cg_dist_set_timeout, default
+// CG_DIST_TIMEOUT_MS or 60 s).  On an RCCL error or a passed deadline the
+// communicator is aborted (ncclCommAbort: RCCL kernels still waiting on a
+// peer exit), the call returns CG_E_HIP / CG_E_TIMEOUT, and every later call
+// on the handle fails -- a missing peer ends the job with an error code
+// instead of hanging it.
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cg_internal.h"
@@ -108,6 +123,11 @@ struct cg_dist {
     hipEvent_t ev_zero[2] = {};       // ranks > 0: the slot's counts zeroed for this call (on st)
     hipEvent_t ev_start = nullptr;    // rank 0: the caller's stream at the start of the call
     int cur = 0;                      // slot of the last call
+    // bounded waits
+    int timeout_ms = 60000;           // deadline of every host wait
+    bool aborted = false;             // communicator aborted after an error / timeout
+    hipStream_t last_st = nullptr;    // render stream of the last call
+    hipEvent_t ev_wait[2] = {};       // cg_dist_wait: render stream, transfer stream
 };
 
 namespace {
@@ -126,11 +146,117 @@ int fail(cg_dist *d, int code, const std::string &what)
         hipError_t e_ = (call);                                                                    \
         if (e_ != hipSuccess) return fail((d), CG_E_HIP, std::string(what) + ": " + hipGetErrorString(e_)); \
     } while (0)
-#define DN(d, call, what)                                                                              \
-    do {                                                                                               \
-        ncclResult_t r_ = (call);                                                                      \
-        if (r_ != ncclSuccess) return fail((d), CG_E_HIP, std::string(what) + ": " + ncclGetErrorString(r_)); \
+
+using Clock = std::chrono::steady_clock;
+
+int default_timeout_ms()
+{
+    const char *e = std::getenv("CG_DIST_TIMEOUT_MS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return v > 0 && v < (1L << 30) ? (int)v : 60000;
+}
+
+void poll_pause() { std::this_thread::sleep_for(std::chrono::microseconds(20)); }
+
+// ncclCommAbort on a helper thread, joined for at most 10 s: an abort that
+// itself stalls (a peer's socket never answering) must not turn the error
+// return into the hang it reports.
+void abort_comm(cg_dist *d)
+{
+    d->aborted = true;
+    ncclComm_t c = d->comm;
+    d->comm = nullptr;
+    if (!c) return;
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    std::thread t([c, done] {
+        (void)ncclCommAbort(c);
+        done->store(true);
+    });
+    const auto end = Clock::now() + std::chrono::seconds(10);
+    while (!done->load() && Clock::now() < end) poll_pause();
+    if (done->load()) t.join();
+    else t.detach();
+}
+
+// The communicator's state after an RCCL call: ncclInProgress (non-blocking
+// mode) is polled through ncclCommGetAsyncError until it settles or the
+// deadline passes.  Errors and timeouts abort the communicator.
+int nccl_settle(cg_dist *d, ncclResult_t r, const char *what)
+{
+    if (r == ncclInProgress && d->comm) {
+        const auto end = Clock::now() + std::chrono::milliseconds(d->timeout_ms);
+        for (;;) {
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t q = ncclCommGetAsyncError(d->comm, &st);
+            r = q == ncclSuccess ? st : q;
+            if (r != ncclInProgress) break;
+            if (Clock::now() >= end) {
+                abort_comm(d);
+                return fail(d, CG_E_TIMEOUT, std::string(what) + ": no progress within " + std::to_string(d->timeout_ms) +
+                                                 " ms (a peer missing?); communicator aborted");
+            }
+            poll_pause();
+        }
+    }
+    if (r == ncclSuccess) return CG_OK;
+    abort_comm(d);
+    return fail(d, CG_E_HIP, std::string(what) + ": " + ncclGetErrorString(r) + "; communicator aborted");
+}
+#define DN(d, call, what)                                      \
+    do {                                                       \
+        if ((d)->aborted) return fail((d), CG_E_HIP, "communicator was aborted by an earlier error"); \
+        int rc_ = nccl_settle((d), (call), (what));            \
+        if (rc_) return rc_;                                   \
     } while (0)
+
+// Host wait for events (nullptr entries skipped) against the deadline, polling
+// the communicator's asynchronous error meanwhile.
+int wait_events(cg_dist *d, const hipEvent_t *ev, int n, const char *what)
+{
+    const auto end = Clock::now() + std::chrono::milliseconds(d->timeout_ms);
+    for (int i = 0; i < n;) {
+        if (!ev[i]) {
+            ++i;
+            continue;
+        }
+        const hipError_t q = hipEventQuery(ev[i]);
+        if (q == hipSuccess) {
+            ++i;
+            continue;
+        }
+        if (q != hipErrorNotReady) return fail(d, CG_E_HIP, std::string(what) + ": " + hipGetErrorString(q));
+        if (d->comm) {
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t r = ncclCommGetAsyncError(d->comm, &st);
+            const ncclResult_t e = r == ncclSuccess ? st : r;
+            if (e != ncclSuccess && e != ncclInProgress) {
+                abort_comm(d);
+                return fail(d, CG_E_HIP, std::string(what) + ": " + ncclGetErrorString(e) + "; communicator aborted");
+            }
+        }
+        if (Clock::now() >= end) {
+            abort_comm(d);
+            return fail(d, CG_E_TIMEOUT, std::string(what) + ": not done within " + std::to_string(d->timeout_ms) +
+                                             " ms; communicator aborted");
+        }
+        poll_pause();
+    }
+    return CG_OK;
+}
+
+// Bounded host wait for everything this rank enqueued: the last call's render
+// stream and the transfer stream.
+int drain(cg_dist *d, hipStream_t st, const char *what)
+{
+    if (!d->ev_done) return CG_OK;   // nothing enqueued yet
+    DT(d, hipSetDevice(ctx_device(d->ctx)), "hipSetDevice");
+    for (int k = 0; k < 2; ++k)
+        if (!d->ev_wait[k]) DT(d, hipEventCreateWithFlags(&d->ev_wait[k], hipEventDisableTiming), "event");
+    if (!st) st = d->last_st ? d->last_st : ctx_stream(d->ctx);
+    DT(d, hipEventRecord(d->ev_wait[0], st), "event");
+    DT(d, hipEventRecord(d->ev_wait[1], d->xs), "event");
+    return wait_events(d, d->ev_wait, 2, what);
+}
 
 void equal_bands(int H, int n, std::vector<int> &row0, std::vector<int> &rows)
 {
@@ -287,28 +413,53 @@ extern "C" int cg_dist_unique_id(cg_dist_id *id)
     return CG_OK;
 }
 
-extern "C" int cg_dist_create(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, cg_dist **out)
+extern "C" int cg_dist_create_timed(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, int timeout_ms,
+                                    cg_dist **out)
 {
-    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return CG_E_INVALID;
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms < 0) return CG_E_INVALID;
     *out = nullptr;
     cg_dist *d = new cg_dist;
     d->ctx = ctx;
     d->nranks = nranks;
     d->rank = rank;
+    d->timeout_ms = timeout_ms ? timeout_ms : default_timeout_ms();
     ncclUniqueId u;
     std::memcpy(u.internal, id->bytes, sizeof(u.internal));
     if (hipSetDevice(ctx_device(ctx)) != hipSuccess) {
         delete d;
         return fail(nullptr, CG_E_HIP, "hipSetDevice");
     }
-    const ncclResult_t r = ncclCommInitRank(&d->comm, nranks, u, rank);
-    if (r != ncclSuccess) {
-        ctx_set_error(ctx, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-        delete d;
-        return CG_E_HIP;
+    // non-blocking: the init (every rank meeting at the id's bootstrap root)
+    // runs in the background and is polled against the deadline
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t r = ncclCommInitRankConfig(&d->comm, nranks, u, rank, &cfg);
+    const int rc = nccl_settle(d, r, "ncclCommInitRankConfig");
+    if (rc) {
+        delete d;   // nccl_settle aborted the communicator
+        return rc;
     }
     *out = d;
     return CG_OK;
+}
+
+extern "C" int cg_dist_create(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, cg_dist **out)
+{
+    return cg_dist_create_timed(ctx, nranks, rank, id, 0, out);
+}
+
+extern "C" int cg_dist_set_timeout(cg_dist *d, int timeout_ms)
+{
+    if (!d || timeout_ms <= 0) return CG_E_INVALID;
+    d->timeout_ms = timeout_ms;
+    return CG_OK;
+}
+
+extern "C" int cg_dist_wait(cg_dist *d, void *stream)
+{
+    if (!d) return CG_E_INVALID;
+    if (d->aborted) return fail(d, CG_E_HIP, "communicator was aborted by an earlier error");
+    return drain(d, (hipStream_t)stream, "cg_dist_wait");
 }
 
 extern "C" int cg_dist_create_local(cg_ctx *const *ctxs, int nranks, cg_dist **outs)
@@ -333,8 +484,16 @@ extern "C" void cg_dist_destroy(cg_dist *d)
 {
     if (!d) return;
     (void)hipSetDevice(ctx_device(d->ctx));
-    if (d->xs) (void)hipStreamSynchronize(d->xs);
-    if (d->comm) (void)ncclCommDestroy(d->comm);
+    // bounded: a peer that never answers ends in ncclCommAbort, not a hang
+    if (!d->aborted && drain(d, nullptr, "cg_dist_destroy") == CG_OK && d->comm) {
+        if (nccl_settle(d, ncclCommFinalize(d->comm), "ncclCommFinalize") == CG_OK) {
+            (void)ncclCommDestroy(d->comm);
+            d->comm = nullptr;
+        }
+    }
+    if (d->comm) abort_comm(d);
+    for (hipEvent_t e : d->ev_wait)
+        if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < 2; ++k)
         for (hipEvent_t e : {d->ev_rend[k], d->ev_sent[k], d->ev_recv[k], d->ev_asm[k]})
             if (e) (void)hipEventDestroy(e);
@@ -404,6 +563,10 @@ extern "C" int cg_dist_set_chunk(cg_dist *d, int frames)
 extern "C" int cg_dist_last_times(cg_dist *d, double *render_ms_per_frame, double *assemble_ms_per_frame)
 {
     if (!d) return CG_E_INVALID;
+    if (!d->group) {   // the timing events sit behind the transfers: bounded wait first
+        const int rc = drain(d, nullptr, "cg_dist_last_times");
+        if (rc) return rc;
+    }
     if (render_ms_per_frame) *render_ms_per_frame = pool_ms_per_frame(d->t_rend, d->n_rend);
     if (assemble_ms_per_frame) *assemble_ms_per_frame = pool_ms_per_frame(d->t_asm, d->n_asm);
     return CG_OK;
@@ -457,6 +620,8 @@ extern "C" int cg_dist_rebalance(cg_dist *d)
     }
     int rc = ensure_events(d);
     if (rc) return rc;
+    rc = drain(d, nullptr, "cg_dist_rebalance");   // the last call's timing events, bounded
+    if (rc) return rc;
     const double mine[2] = {pool_ms_per_frame(d->t_rend, d->n_rend), pool_ms_per_frame(d->t_asm, d->n_asm)};
     DT(d, d->stats.ensure((size_t)(2 * n + 2) * sizeof(double) + (size_t)2 * n * sizeof(int)), "alloc stats");
     double *dt = (double *)d->stats.p;
@@ -465,7 +630,9 @@ extern "C" int cg_dist_rebalance(cg_dist *d)
     DN(d, ncclAllGather(dt + 2 * n, dt, 2, ncclFloat64, d->comm, d->xs), "ncclAllGather");
     std::vector<double> t(2 * n);
     DT(d, hipMemcpyAsync(t.data(), dt, 2 * n * sizeof(double), hipMemcpyDeviceToHost, d->xs), "stats download");
-    DT(d, hipStreamSynchronize(d->xs), "stats sync");
+    DT(d, hipEventRecord(d->ev_wait[1], d->xs), "event");
+    rc = wait_events(d, &d->ev_wait[1], 1, "cg_dist_rebalance: ncclAllGather");
+    if (rc) return rc;
     // rank 0 decides; every rank adopts its boundaries
     std::vector<int> band(2 * n);
     if (d->rank == 0) {
@@ -478,7 +645,9 @@ extern "C" int cg_dist_rebalance(cg_dist *d)
     }
     DN(d, ncclBroadcast(dband, dband, 2 * n, ncclInt32, 0, d->comm, d->xs), "ncclBroadcast");
     DT(d, hipMemcpyAsync(band.data(), dband, band.size() * sizeof(int), hipMemcpyDeviceToHost, d->xs), "bands");
-    DT(d, hipStreamSynchronize(d->xs), "bands sync");
+    DT(d, hipEventRecord(d->ev_wait[1], d->xs), "event");
+    rc = wait_events(d, &d->ev_wait[1], 1, "cg_dist_rebalance: ncclBroadcast");
+    if (rc) return rc;
     for (int r = 0; r < n; ++r) {
         d->row0[r] = band[2 * r];
         d->rows[r] = band[2 * r + 1];
@@ -529,7 +698,9 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
         Mem &out = d->sbuf[s];   // the whole call's band (rank 0 pulls from it in the local transport)
         DT(d, out.ensure(std::max<size_t>(bytes, 1)), "alloc send buffer");
         if (d->done_cap[s] < (size_t)n_frames) {
-            DT(d, hipStreamSynchronize(st), "sync");
+            // bounded: st may wait on the slot's previous sends
+            rc = drain(d, st, "grow signals");
+            if (rc) return rc;
             if (d->done[s]) DT(d, hipFree(d->done[s]), "free signals");
             d->done[s] = nullptr;
             // uncached fine-grained device memory: the kernels' atomics land in
@@ -650,6 +821,7 @@ extern "C" int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int 
                                         int n_frames, uint32_t *d_frames, size_t frame_stride, void *stream)
 {
     if (!d || n_frames < 0 || (n_frames && !cams)) return CG_E_INVALID;
+    if (d->aborted) return fail(d, CG_E_HIP, "communicator was aborted by an earlier error");
     if (n_frames == 0) return CG_OK;
     const int W = cams[0].width, H = cams[0].height;
     if (W <= 0 || H <= 0) return CG_E_INVALID;
@@ -666,6 +838,7 @@ extern "C" int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int 
         equal_bands(H, d->nranks, d->row0, d->rows);
     }
     hipStream_t st = stream ? (hipStream_t)stream : ctx_stream(d->ctx);
+    d->last_st = st;
     const int n = d->nranks, me = d->rank;
     int c0, cols;
     call_window(d, cams, n_frames, c0, cols);

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <utility>
@@ -30,6 +31,7 @@ struct Pending {
 struct KtState {
     std::mutex mu;
     bool on = false;
+    std::atomic<bool> on_fast{false};   // read without the lock: a disabled scope costs one load
     std::vector<hipEvent_t> pool;
     std::vector<Pending> pending;
     double ms[KT_COUNT] = {};
@@ -40,21 +42,37 @@ struct KtState {
     hipEvent_t ref = nullptr;
     bool ref_set = false;
     std::vector<std::pair<double, double>> spans[KT_COUNT];
+    void settle(const Pending &p)
+    {
+        float ms1 = 0.f, t0 = 0.f;
+        if (hipEventElapsedTime(&ms1, p.a, p.b) == hipSuccess) {
+            ms[p.id] += ms1;
+            ++n[p.id];
+            if (ref_set && hipEventElapsedTime(&t0, ref, p.a) == hipSuccess)
+                spans[p.id].emplace_back((double)t0, (double)t0 + ms1);
+        }
+        pool.push_back(p.a);
+        pool.push_back(p.b);
+    }
     // Settle the recorded pairs into the totals (blocks until they completed).
     void flush()
     {
         for (const Pending &p : pending) {
-            float ms1 = 0.f, t0 = 0.f;
-            if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms1, p.a, p.b) == hipSuccess) {
-                ms[p.id] += ms1;
-                ++n[p.id];
-                if (ref_set && hipEventElapsedTime(&t0, ref, p.a) == hipSuccess)
-                    spans[p.id].emplace_back((double)t0, (double)t0 + ms1);
-            }
-            pool.push_back(p.a);
-            pool.push_back(p.b);
+            (void)hipEventSynchronize(p.b);
+            settle(p);
         }
         pending.clear();
+    }
+    // Settle the pairs that already completed, without blocking (keeps
+    // `pending` bounded in long timed runs).
+    void settle_completed()
+    {
+        size_t k = 0;
+        for (const Pending &p : pending) {
+            if (hipEventQuery(p.b) == hipSuccess) settle(p);
+            else pending[k++] = p;
+        }
+        pending.resize(k);
     }
     // union length of a kernel's launch spans
     double busy(int id)
@@ -95,6 +113,7 @@ KtState &kt()
 KtScope::KtScope(int id, hipStream_t st) : id_(id), st_(st)
 {
     KtState &s = kt();
+    if (!s.on_fast.load(std::memory_order_relaxed)) return;
     std::lock_guard<std::mutex> g(s.mu);
     if (!s.on || id < 0 || id >= KT_COUNT) return;
     if (!s.ref_set) {
@@ -120,6 +139,7 @@ KtScope::~KtScope()
         return;
     }
     s.pending.push_back({id_, a_, b});
+    if (s.pending.size() >= 2048) s.settle_completed();
 }
 
 }  // namespace cg
@@ -136,6 +156,7 @@ extern "C" int cg_kernel_timing(int enable)
     for (auto &v : s.spans) v.clear();
     s.ref_set = false;
     s.on = enable != 0;
+    s.on_fast.store(s.on);
     return CG_OK;
 }
 

@@ -1074,6 +1074,8 @@ extern "C" int cg_rt_render_frames(cg_ctx *c, const cg_light *lights, int n_ligh
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     const int W = cams[0].width, H = cams[0].height;
     if (W <= 0 || H <= 0) return CG_E_INVALID;
+    for (int f = 1; f < n_frames; ++f)   // the slots hold chunks of W x H frames
+        if (cams[f].width != W || cams[f].height != H) return CG_E_INVALID;
     const size_t px = (size_t)W * H;
     const size_t stride = frame_stride ? frame_stride : px;
     if (stride < px) return CG_E_INVALID;
@@ -1085,6 +1087,17 @@ extern "C" int cg_rt_render_frames(cg_ctx *c, const cg_light *lights, int n_ligh
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_cdone[k], hipEventDisableTiming), "copy event");
         }
     }
+    // Every return below, error or not, leaves nothing of this call running:
+    // earlier chunks' downloads may still be writing into argb (asynchronous
+    // when it is pinned), and the stream may wait on their events.
+    struct Drain {
+        cg_ctx *c;
+        ~Drain()
+        {
+            (void)hipStreamSynchronize(c->xfer);
+            (void)hipStreamSynchronize(c->stream);
+        }
+    } drain_on_exit{c};
     for (int k = 0; k < 2; ++k) CG_TRY(c, c->hslot[k].ensure((size_t)ch * px * sizeof(uint32_t)), "alloc frame slots");
     const int nchunks = (n_frames + ch - 1) / ch;
     auto download = [&](int j) -> int {

@@ -34,6 +34,7 @@ extern "C" {
 #define CG_E_HIP (-3)         /* HIP runtime error (see cg_last_error) */
 #define CG_E_NOSCENE (-4)     /* render before cg_rt_set_scene */
 #define CG_E_CAPACITY (-5)    /* output capacity too small */
+#define CG_E_TIMEOUT (-6)     /* multi-GPU: a peer did not answer within the deadline (communicator aborted) */
 
 typedef struct cg_ctx cg_ctx;
 
@@ -262,8 +263,25 @@ typedef struct cg_dist cg_dist;
 typedef struct { char bytes[128]; } cg_dist_id;    /* an RCCL unique id (ncclUniqueId) */
 /* Rank 0 creates the id and hands it to every rank (MPI, sockets, ...). */
 int cg_dist_unique_id(cg_dist_id *id);
-/* Collective over the nranks processes: RCCL communicator on ctx's device. */
+/* Collective over the nranks processes: RCCL communicator on ctx's device.
+ * Every host wait of the multi-GPU path is bounded: the communicator is
+ * non-blocking, and init, cg_dist_rebalance, cg_dist_last_times, cg_dist_wait
+ * and cg_dist_destroy poll completion and the communicator's asynchronous
+ * error against a deadline (default: CG_DIST_TIMEOUT_MS from the environment,
+ * else 60000 ms).  An RCCL error returns CG_E_HIP and a passed deadline
+ * CG_E_TIMEOUT; either aborts the communicator (ncclCommAbort: kernels still
+ * waiting on a peer exit) and every later call on the handle fails CG_E_HIP.
+ * A missing peer therefore ends the job with an error instead of a hang. */
 int cg_dist_create(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, cg_dist **out);
+/* cg_dist_create with an explicit deadline in ms (0: the default above). */
+int cg_dist_create_timed(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, int timeout_ms, cg_dist **out);
+/* Deadline (ms, > 0) of every later host wait on this handle. */
+int cg_dist_set_timeout(cg_dist *d, int timeout_ms);
+/* Bounded host wait until this rank's work of its calls so far has drained:
+ * `stream` (NULL: the last call's stream) and the transfer stream.  0, or
+ * CG_E_TIMEOUT / CG_E_HIP after aborting the communicator.  Use it instead of
+ * an unbounded device synchronise after cg_rt_render_frames_dist. */
+int cg_dist_wait(cg_dist *d, void *stream);
 /* In-process transport for tests: nranks contexts (any devices, possibly one)
  * in one process and thread, one cg_dist per rank in outs[]; bands move by
  * device-to-device copies.  Each render call must be made on ranks

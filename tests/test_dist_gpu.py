@@ -179,3 +179,77 @@ def test_dist_errors():
             d.close()
         for c in ctxs:
             c.close()
+
+
+_MISSING_PEER = r"""
+import json, os, sys, time
+sys.path.insert(0, os.path.join(os.environ["CG_ROOT"], "computer-graphics_amd"))
+import cgamd
+ctx = cgamd.Context(0)
+uid = cgamd.dist_unique_id()
+t0 = time.monotonic()
+res = {}
+try:
+    cgamd.Dist(ctx, 2, 0, uid, timeout_ms=int(os.environ["CG_T_MS"]))
+    res["raised"] = None
+except cgamd.DistTimeout as e:
+    res["raised"], res["msg"] = "timeout", str(e)
+except RuntimeError as e:
+    res["raised"], res["msg"] = "other", str(e)
+res["elapsed"] = time.monotonic() - t0
+# the context itself stays usable after the aborted communicator
+tris, n, sph = cgamd.rt_scene()
+ctx.rt_set_scene(tris, n, sph, 1)
+argb, _ = ctx.rt_render(cgamd.rt_camera(64, 48, 48.0))
+res["frame_ok"] = bool(argb.any())
+print("RESULT " + json.dumps(res), flush=True)
+ctx.close()
+"""
+
+
+def test_dist_rccl_missing_peer_fails_within_deadline():
+    """rank 0 of a world of two calls cg_dist_create alone (its peer
+    never joins).  The non-blocking init is polled against the deadline; past it the
+    communicator is aborted and the call returns CG_E_TIMEOUT (cgamd.DistTimeout) instead
+    of blocking the job forever.  Run in a child process under its own time limit, so a
+    regression fails this test rather than hanging the suite."""
+    import json
+    import os
+    import subprocess
+    import sys
+    t_ms = 3000
+    env = dict(os.environ, CG_ROOT=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), CG_T_MS=str(t_ms))
+    r = subprocess.run([sys.executable, "-c", _MISSING_PEER], capture_output=True, text=True, timeout=100, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert r.returncode == 0 and lines, f"rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+    res = json.loads(lines[-1][7:])
+    assert res["raised"] == "timeout", res
+    # the deadline, plus at most the 10 s the library gives ncclCommAbort
+    assert t_ms / 1e3 * 0.9 <= res["elapsed"] <= t_ms / 1e3 + 12.0, res
+    assert res["frame_ok"], res
+
+
+def test_dist_rccl_one_rank_bounded_waits():
+    """The bounded host waits on a healthy communicator: cg_dist_wait, a short deadline,
+    rebalance and last_times all succeed, and the frames are the single-GPU render."""
+    W, H = 320, 256
+    cams = _cams(W, H, 256.0, 4)
+    (ctx,) = _ctxs(1)
+    d = cgamd.Dist(ctx, 1, 0, cgamd.dist_unique_id(), timeout_ms=20000)
+    try:
+        d.set_timeout(5000)
+        want = _single(ctx, cams, cgamd.default_lights())
+        frames = torch.zeros(len(cams) * W * H, dtype=torch.int32, device="cuda")
+        for _ in range(3):
+            d.render_frames(cams, frames.data_ptr(), lights=cgamd.default_lights())
+        d.wait()
+        got = frames.cpu().numpy().view(np.uint32).reshape(len(cams), H * W)
+        assert np.array_equal(got, want)
+        d.rebalance()
+        r, _ = d.last_times()
+        assert r > 0
+        with pytest.raises(RuntimeError):
+            d.set_timeout(0)
+    finally:
+        d.close()
+        ctx.close()
