@@ -52,7 +52,7 @@
 namespace cg {
 int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
                      const cg_rt_shard *shard, void *d_out, size_t frame_stride, int pix_format, void *stream,
-                     uint32_t *d_done, uint32_t *target);
+                     uint32_t *d_done, uint32_t *target, const int *group_starts, int ngroups);
 int ctx_device(const cg_ctx *c);
 hipStream_t ctx_stream(const cg_ctx *c);
 void ctx_set_error(cg_ctx *c, const std::string &e);
@@ -387,7 +387,7 @@ void call_window(const cg_dist *d, const cg_rt_camera *cams, int n, int &c0, int
 
 int render_band(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int nf, int r0, int nr,
                 int c0, int cols, void *dst, size_t stride, int fmt, hipStream_t st, uint32_t *d_done = nullptr,
-                uint32_t *target = nullptr)
+                uint32_t *target = nullptr, const std::vector<int> *groups = nullptr)
 {
     cg_rt_shard sh{0, 1, kLatTileH, r0, nr, fmt == CG_PIX_RGB24 ? c0 : 0, fmt == CG_PIX_RGB24 ? cols : 0};
     TimedPair *t;
@@ -395,7 +395,8 @@ int render_band(cg_dist *d, const cg_light *lights, int n_lights, const cg_rt_ca
     if (rc) return rc;
     t->frames = nf;
     DT(d, hipEventRecord(t->a, st), "event");
-    rc = rt_render_frames(d->ctx, lights, n_lights, cams, nf, &sh, dst, stride, fmt, st, d_done, target);
+    rc = rt_render_frames(d->ctx, lights, n_lights, cams, nf, &sh, dst, stride, fmt, st, d_done, target,
+                          groups ? groups->data() : nullptr, groups ? (int)groups->size() - 1 : 0);
     if (rc) return rc;
     DT(d, hipEventRecord(t->b, st), "event");
     return CG_OK;
@@ -719,8 +720,13 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
         DT(d, hipEventRecord(d->ev_zero[s], st), "event");
         if (!d->group) DT(d, hipStreamWaitEvent(d->xs, d->ev_zero[s], 0), "wait");
         if (nr > 0) {
+            // the lattice dispatches the chunks' frames in turn (heavy tiles first
+            // inside each), so chunk j's frames complete before chunk j + 1's
+            std::vector<int> gs;
+            for (const auto &ch : chunk_plan(n_frames, C)) gs.push_back(ch.first);
+            gs.push_back(n_frames);
             rc = render_band(d, lights, n_lights, cams, n_frames, r0, nr, c0, cols, out.p, (size_t)nr * pitch,
-                             CG_PIX_RGB24, st, d->done[s], d->target[s].data());
+                             CG_PIX_RGB24, st, d->done[s], d->target[s].data(), &gs);
             if (rc) return rc;
         } else {
             for (int f = 0; f < n_frames; ++f) d->target[s][f] = 0u;   // nothing to wait for

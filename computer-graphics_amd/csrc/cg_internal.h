@@ -19,6 +19,30 @@ constexpr int kMaxFrameBatch = 32;   // frames per batched RT launch (cg_rt_rend
 
 constexpr int kMaxBlocks = 64;       // row blocks of one assembly launch (cg_rt_assemble_device)
 
+// Measured-cost dispatch order of the lattice launch (cg_rt.hip rt_lattice_kernel).
+// A launch's frame-0 workgroups record each tile's duration as a cost class
+// (heavy first); the next call's certificate launch counting-sorts that
+// recording into `flat` (LatFlatten, its first block) and the lattice
+// workgroups take tiles in that order -- every frame's heaviest tile first,
+// the cheap tiles last, so the launch ends on short workgroups instead of a
+// heavy tile's tail.  Only the schedule changes: each workgroup still renders
+// one whole (frame, tile), and `flat` is always a permutation of the launch's
+// tiles (a counting sort of any recording is), so the image cannot depend on it.
+constexpr int kLatClasses = 64;
+constexpr int kLatMaxGroups = 32;
+struct LatOrder {
+    const uint32_t *flat;    // the launch's tiles heavy first (window-relative: by * gx + bx); null: default order
+    uint8_t *cost;           // this launch's recording (class per tile of frame 0); null: none
+    int ngroups;             // < 0: frame-major (each frame heavy first, frames in turn); >= 0: frames dispatched
+                             // in groups (cg_dist chunks), every frame of a group at each tile, heavy first; 0: one group
+    uint8_t gs[kLatMaxGroups + 1];   // group starts (frames of the launch), gs[ngroups] = frames
+};
+struct LatFlatten {
+    const uint8_t *cost;     // a recording of the launch's tile geometry
+    uint32_t *flat;          // out: its counting sort
+    int n;                   // tiles (gx * gy); 0: nothing to do
+};
+
 // Row blocks of frames for rt_assemble_kernel: block b is rows[b] rows that
 // land at frame rows row0[b] ..; cum = prefix sums of rows.
 struct RtBlocks {

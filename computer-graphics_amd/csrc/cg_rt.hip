@@ -375,12 +375,14 @@ __device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int c
 // rt_prepare_kernel's), every other block first certifies its super-tile
 // (wave 0, unit_cert) into LDS and then refines it per tile; no super-tile
 // masks round-trip through memory and no second dependent launch.
+__device__ __forceinline__ void lat_flatten(const LatFlatten &Z);   // below, with the lattice kernel
+
 __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
                                                            RtFrame F, const RtSphere *__restrict__ sph,
                                                            const unsigned long long *__restrict__ sup_masks,
                                                            unsigned long long *__restrict__ lat_masks,
                                                            RtTri *__restrict__ tc_out, RtShade *__restrict__ shade_out,
-                                                           int n_prep_blocks, int frame_fast)
+                                                           int n_prep_blocks, int frame_fast, LatFlatten Z)
 {
     constexpr int kT = kSup * kSup;
     // frame_fast: blockIdx.x = frame (dispatched fastest), blockIdx.y = prep block, then
@@ -391,6 +393,8 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
     const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
     if (blk < n_prep_blocks) {
         prep_tri(tris, n, blk * blockDim.x + threadIdx.x, frame, camf, tc_out, shade_out);
+        // the first block (dispatched first) also sorts the lattice launch's order
+        if (Z.n > 0 && blk == 0 && frame == 0) lat_flatten(Z);
         return;
     }
 #ifdef CG_WG_TIMING
@@ -850,10 +854,12 @@ __device__ __forceinline__ void lat_store_black(const RtFrame &F, const LatTile 
 // tile row also store the output's columns left / right of the window black
 // -- no ray there can hit the scene's box (rt_box_columns), so those pixels
 // are PutPixelSDL(0, 0, 0) -- instead of a workgroup per black tile.
-__device__ __forceinline__ void lat_store_outside(const RtFrame &F, const LatTile &G, const LatOut &o)
+__device__ __forceinline__ void lat_store_outside(const RtFrame &F, const LatTile &G, const LatOut &o,
+                                                  int bxw = -1)
 {
     if (F.txn <= 0 || G.nv <= 0) return;
-    const bool left = blockIdx.x == 0, right = blockIdx.x == gridDim.x - 1;
+    if (bxw < 0) bxw = (int)blockIdx.x;   // the workgroup's column within the launch's window
+    const bool left = bxw == 0, right = bxw == (int)gridDim.x - 1;
     if (!left && !right) return;
     const uint32_t px = put_pixel(v3(0.0f, 0.0f, 0.0f));
     for (int side = 0; side < 2; ++side) {
@@ -876,7 +882,104 @@ __device__ __forceinline__ void lat_store_outside(const RtFrame &F, const LatTil
     }
 }
 
-// blockIdx.z = frame of a batched launch: camera cams.c[frame], RtTri at
+// The (frame, tile) of a lattice workgroup.  Default: blockIdx.z = frame, tile
+// rows bottom first (lat_tile_row), bx = blockIdx.x.  With a measured order
+// (LatOrder::flat, cg_internal.h), by the workgroup's dispatch rank (blockIdx
+// linear: workgroups are dispatched in that order): frame-major (ngroups < 0)
+// takes each frame's tiles heavy first, frame after frame -- a CU's
+// consecutive workgroups keep one frame's triangle constants in its scalar
+// cache; interleaved (ngroups >= 0) walks frame groups in turn and, inside a
+// group, the tiles heavy first with every frame of the group at each tile:
+// rank r of a group of nfg frames is tile flat[r / nfg] of frame r % nfg.
+// flat is a permutation of the window's gx * gy tiles, so every (frame, tile)
+// is still rendered exactly once.
+struct LatSlot {
+    int frame, bx, by;   // bx: column within the launch's window (tile column F.tx0 + bx)
+};
+__device__ __forceinline__ LatSlot lat_slot_of(const LatOrder &O)
+{
+    LatSlot S;
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y, n = gx * gy;
+    if (!O.flat) {
+        S.frame = (int)blockIdx.z;
+        S.by = lat_tile_row();
+        S.bx = (int)blockIdx.x;
+        return S;
+    }
+    const int id = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+    if (O.ngroups < 0) {   // frame-major: each frame's tiles heavy first, frames in turn
+        S.frame = (int)blockIdx.z;
+        const int t = (int)O.flat[id - S.frame * n];
+        S.by = t / gx;
+        S.bx = t - S.by * gx;
+        return S;
+    }
+    int g0 = 0, g1 = (int)gridDim.z;
+    if (O.ngroups > 0) {
+        int g = 0;
+        while (g + 1 < O.ngroups && id >= (int)O.gs[g + 1] * n) ++g;
+        g0 = O.gs[g];
+        g1 = O.gs[g + 1];
+    }
+    const int local = id - g0 * n, nfg = g1 - g0, r = local / nfg;
+    S.frame = g0 + (local - r * nfg);
+    const int t = (int)O.flat[r];   // uniform: a scalar load
+    S.by = t / gx;
+    S.bx = t - S.by * gx;
+    return S;
+}
+// Heavy-first cost class of a workgroup's duration (wall_clock64 ticks, 100 MHz):
+// four classes per octave, class 0 the longest.
+__device__ __forceinline__ int lat_cost_class(unsigned long long d)
+{
+    const unsigned v = (unsigned)(d < 0xffffffffull ? d : 0xffffffffull) | 1u;
+    const int lg = 31 - __clz(v);
+    const int q = lg >= 2 ? (int)((v >> (lg - 2)) & 3u) : 0;
+    return kLatClasses - 1 - min(kLatClasses - 1, max(0, 4 * lg + q - 16));
+}
+// rt_tile_cert_kernel's first block: counting sort of the recording Z.cost
+// (class per tile) into Z.flat, heavy first.  Any recording gives a
+// permutation of the n tiles.
+__device__ __forceinline__ void lat_flatten(const LatFlatten &Z)
+{
+    __shared__ uint32_t s_cnt[kLatClasses], s_off[kLatClasses];
+    const int t = threadIdx.x, nt = blockDim.x;
+    if (t < kLatClasses) s_cnt[t] = 0u;
+    __syncthreads();
+    for (int j0 = 0; j0 < Z.n; j0 += 8 * nt) {
+        int c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u * nt + t;
+            c[u] = j < Z.n ? min((int)Z.cost[j], kLatClasses - 1) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (c[u] >= 0) atomicAdd(&s_cnt[c[u]], 1u);
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t a = 0u;
+        for (int k = 0; k < kLatClasses; ++k) {
+            s_off[k] = a;
+            a += s_cnt[k];
+        }
+    }
+    __syncthreads();
+    for (int j0 = 0; j0 < Z.n; j0 += 8 * nt) {
+        int c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u * nt + t;
+            c[u] = j < Z.n ? min((int)Z.cost[j], kLatClasses - 1) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (c[u] >= 0) Z.flat[atomicAdd(&s_off[c[u]], 1u)] = (uint32_t)(j0 + u * nt + t);
+    }
+}
+
+// Frame S.frame of a batched launch: camera cams.c[frame], RtTri at
 // tc + frame * n_tris, masks at lat_masks + frame * tiles, output at
 // out + frame * out_stride.
 // PITCH: the LDS row pitch of the lattice, kLatW (shared columns) or kLatWY
@@ -885,9 +988,9 @@ template <int PITCH>
 __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__restrict__ tc,
                                              const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
                                              const unsigned long long *__restrict__ lat_masks, const RtFrameCams &cams,
-                                             size_t out_stride, uint32_t *__restrict__ out)
+                                             size_t out_stride, uint32_t *__restrict__ out, const LatSlot &S)
 {
-    const int frame = blockIdx.z;
+    const int frame = S.frame;
     RtFrame F = F0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) F.cam[c] = cams.c[frame][c];
@@ -895,10 +998,10 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     lat_masks += (size_t)frame * lat_tiles_x(F) * gridDim.y * 2;
     const LatOut o = lat_out(F, frame, out_stride, out);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int by = lat_tile_row(), bx = lat_tile_col(F);
+    const int by = S.by, bx = F.tx0 + S.bx;
     LatTile G = lat_tile(F, bx, by);
     G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
-    lat_store_outside(F, G, o);
+    lat_store_outside(F, G, o, S.bx);
     const int ay0 = G.ay0, cols = G.cols, rows = G.rows;
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
     // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
@@ -1392,13 +1495,19 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
                                                                   const RtSphere *__restrict__ sph,
                                                                   const unsigned long long *__restrict__ lat_masks,
                                                                   RtFrameCams cams, size_t out_stride,
-                                                                  uint32_t *__restrict__ out, uint32_t *frame_done)
+                                                                  uint32_t *__restrict__ out, uint32_t *frame_done,
+                                                                  LatOrder O)
 {
 #ifdef CG_WG_TIMING
     const unsigned long long wt0 = wall_clock64();
 #endif
-    lattice_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out);
-    lat_signal(frame_done, blockIdx.z);
+    const unsigned long long t_start = wall_clock64();
+    const LatSlot S = lat_slot_of(O);
+    lattice_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out, S);
+    // the recording for the next call's order: frame 0's tiles, one class each
+    if (O.cost && S.frame == 0 && threadIdx.x == 0)
+        O.cost[S.by * (int)gridDim.x + S.bx] = (uint8_t)lat_cost_class(wall_clock64() - t_start);
+    lat_signal(frame_done, S.frame);
 #ifdef CG_WG_TIMING
     WGT_STAMP(wt3);
     wgt_record(2, wt0, wt3, wt3, wt3);
@@ -1614,9 +1723,11 @@ static int env_int(const char *name, int dflt)
     return e && *e ? std::atoi(e) : dflt;
 }
 
+// Z (optional): a measured lattice order to sort in the fused certificate
+// launch; on return Z->n < 0 iff it was (the other certificate paths skip it).
 hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
                              RtShade *d_shade, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
-                             unsigned long long *d_lat_masks, unsigned long long *d_sup_masks)
+                             unsigned long long *d_lat_masks, unsigned long long *d_sup_masks, LatFlatten *Z)
 {
     if (n <= 0) return hipSuccess;
     const int threads = kRtThreads, prep = (n + threads - 1) / threads;
@@ -1662,7 +1773,9 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             const int ff = tprep + units_w <= 65535;
             const dim3 cg = ff ? dim3(nframes, tprep + units_w) : dim3(tprep + units_w, nframes);
             hipLaunchKernelGGL(rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, n, cams, Fl, d_sph,
-                               (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep, ff);
+                               (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep, ff,
+                               Z ? *Z : LatFlatten{});
+            if (Z) Z->n = -Z->n;   // done (the caller's flag: the lattice launch may use the order)
             return hipGetLastError();
         }
         Fl.txn = 0;   // the split form certifies every super-tile
@@ -1680,7 +1793,7 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         const int ff = units <= 65535;
         hipLaunchKernelGGL(rt_tile_cert_kernel, ff ? dim3(nframes, units) : dim3(units, nframes), dim3(tthreads), 0, st,
                            d_tris, n, cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks,
-                           (RtTri *)nullptr, (RtShade *)nullptr, 0, ff);
+                           (RtTri *)nullptr, (RtShade *)nullptr, 0, ff, LatFlatten{});
         return hipGetLastError();
     }
     if (F && d_lat_masks) {   // single-level: every tile (of the window) certified by rt_prepare_kernel
@@ -1762,18 +1875,20 @@ hipError_t launch_rt_lattice_units(const RtFrame &F, const RtTri *d_tc, const Rt
 hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
                                     const RtSphere *d_sph, const unsigned long long *d_lat_masks,
                                     const unsigned long long *d_umask, const RtFrameCams &cams, int nframes,
-                                    size_t out_stride, uint32_t *d_out, hipStream_t st, uint32_t *d_done)
+                                    size_t out_stride, uint32_t *d_out, hipStream_t st, uint32_t *d_done,
+                                    const LatOrder *order)
 {
+    const LatOrder O = order ? *order : LatOrder{};
     const dim3 grid(F.txn ? F.txn : lat_tiles_x(F), (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     if (F.n_lights > 1 && !d_umask) return hipErrorInvalidValue;
     if (F.txn && (F.tx0 < 0 || F.tx0 + F.txn > lat_tiles_x(F))) return hipErrorInvalidValue;
     KtScope kt(F.n_lights == 1 ? KT_RT_LATTICE : KT_RT_LATTICE_LIGHTS, st);
     if (F.n_lights == 1 && lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                           d_lat_masks, cams, out_stride, d_out, d_done);
+                           d_lat_masks, cams, out_stride, d_out, d_done, O);
     else if (F.n_lights == 1)
         hipLaunchKernelGGL(rt_lattice_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
-                           cams, out_stride, d_out, d_done);
+                           cams, out_stride, d_out, d_done, O);
     else if (lat_yaw(F))
         hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, d_umask, cams, out_stride, d_out, d_done);
@@ -1794,7 +1909,7 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         hipError_t e = launch_rt_lattice_units(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, d_umask, st);
         if (e != hipSuccess) return e;
         return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, d_umask, cams, 1, 0, d_out, st,
-                                        nullptr);
+                                        nullptr, nullptr);
     }
     KtScope kt(KT_RT_PIXEL, st);
     if (F.n_tris <= 64 && F.cull_primary)

@@ -16,11 +16,12 @@
 
 namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTri *, RtShade *, hipStream_t,
-                             const RtFrame *, const RtSphere *, unsigned long long *, unsigned long long *);
+                             const RtFrame *, const RtSphere *, unsigned long long *, unsigned long long *,
+                             LatFlatten * = nullptr);
 size_t rt_sup_units(const RtFrame &);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                     const unsigned long long *, const unsigned long long *, const RtFrameCams &,
-                                    int, size_t, uint32_t *, hipStream_t, uint32_t *);
+                                    int, size_t, uint32_t *, hipStream_t, uint32_t *, const LatOrder *);
 hipError_t launch_rt_lattice_units(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                    const unsigned long long *, const RtFrameCams &, int, unsigned long long *,
                                    hipStream_t);
@@ -100,6 +101,11 @@ struct cg_ctx {
     hipEvent_t ev_cert[2] = {nullptr, nullptr}, ev_lat[2] = {nullptr, nullptr};
     int slot = 0;
     DevBuf ptc[2], pshade[2], plat[2], psup[2], pumask[2];
+    // measured lattice order (LatOrder, cg_internal.h): per slot, the recording
+    // of its last lattice launch (class per tile) and the order sorted for it
+    DevBuf lcost[2], lflat[2];
+    unsigned long long lrec_key[2] = {0ull, 0ull};   // geometry key of the slot's recording (0: none)
+    unsigned rt_scene_gen = 0;                       // cg_rt_set_scene count (part of the key)
     // cg_rt_render_frames (host output): chunks render into two device slots
     // and download on `xfer` while the next chunk renders
     hipStream_t xfer = nullptr;
@@ -339,6 +345,7 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     if (!c || n_tris < 0 || n_spheres < 0 || (n_tris && !tris) || (n_spheres && !spheres))
         return CG_E_INVALID;
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    ++c->rt_scene_gen;
     size_t nt = n_tris > 0 ? (size_t)n_tris : 1;
     CG_TRY(c, c->tris.ensure(nt * sizeof(cg_tri)), "alloc tris");
     CG_TRY(c, c->tc.ensure(nt * sizeof(RtTri)), "alloc tri constants");
@@ -773,9 +780,54 @@ extern "C" int cg_rt_render_device(cg_ctx *c, const cg_light *lights, int n_ligh
 
 // Frames f0 .. f0 + nf - 1 of a batch, one prepare + one lattice launch
 // (rt_use_lattice(F) holds for every frame; they differ only in cameraPos).
+static int lat_tiles_x_host(const RtFrame &F) { return (F.W + kLatTileW - 1) / kLatTileW; }
+
+// The launch geometry a lattice order is recorded for (0 never occurs): the
+// same key means the same tiles in the same window, so the recording predicts
+// the next launch's per-tile cost.  (A different key would still give a valid
+// permutation -- the key only avoids a useless order.)
+static unsigned long long lat_order_key(const cg_ctx *c, const RtFrame &F)
+{
+    unsigned long long h = 1469598103934665603ull;
+    auto mix = [&h](long long v) { h = (h ^ (unsigned long long)v) * 1099511628211ull; };
+    mix(F.W); mix(F.H); mix(F.rows_out); mix(F.row0); mix(F.rank); mix(F.nranks); mix(F.stripe_h);
+    mix(F.tx0); mix(F.txn); mix(F.n_lights); mix(F.n_tris); mix(F.n_sph); mix(c->rt_scene_gen);
+    uint32_t b;
+    std::memcpy(&b, &F.focal, 4); mix(b);
+    for (int k : {0, 8, 12}) { std::memcpy(&b, &F.R[k], 4); mix(b); }
+    return h | 1ull;
+}
+// CG_LAT_ORDER (A/B runs): 0 the default dispatch order, 1 frame-major measured order, 2
+// interleaved measured order (frame groups, tile-major inside a group; the default).  Measured on
+// C2's 20-frame calls (profiles/r05_ab_order.json): interleaved takes the 1/8 bands of the N = 8
+// split from 163-169 to 145-168 us (the floor bands gain most: their launch ended on a heavy
+// tile's tail), frame-major gains nothing there; both cost whole frames 1-2 % (0.920 -> 0.935 ms
+// per 20-frame lattice launch), so only launches of at most kLatOrderRounds rounds of resident
+// workgroups take the order (a band's ~13k workgroups: yes; a whole frame's 105k: no).
+static int lat_order_mode()
+{
+    static const int m = [] {
+        const char *e = std::getenv("CG_LAT_ORDER");
+        return e && *e ? std::atoi(e) : 2;
+    }();
+    return m;
+}
+constexpr long long kLatOrderRounds = 12;
+static long long lat_resident_wgs()
+{
+    static const long long r = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (long long)cus * 6;   // rt_lattice_kernel: 6 workgroups per CU
+    }();
+    return r;
+}
+
 static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_camera *cams, int nf,
                                     void *d_out, size_t stride, hipStream_t st, uint32_t *d_done,
-                                    uint32_t *tiles_per_frame)
+                                    uint32_t *tiles_per_frame, const uint8_t *groups, int ngroups)
 {
     // Workgroups only for the tile columns the scene's box can be seen in by
     // some camera of the batch (O(1) per camera from the box, rt_box_columns);
@@ -858,9 +910,42 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     const bool cold = hipEventQuery(c->ev_lat[0]) == hipSuccess && hipEventQuery(c->ev_lat[1]) == hipSuccess;
     hipStream_t cst = cold ? st : c->aux;
     if (!cold) CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
+    // Measured order (one-light lattice kernel): sort the latest complete
+    // recording of this geometry -- the other slot's (the previous call) when
+    // every lattice launch is done, else this slot's (two calls ago, complete:
+    // cst waited on it) -- in the certificate launch; this launch records into
+    // this slot.
+    const int gx = F.txn ? F.txn : lat_tiles_x_host(F), gy = (F.rows_out + kLatTileH - 1) / kLatTileH;
+    const unsigned long long key = lat_order_key(c, F);
+    LatOrder order{};
+    LatFlatten flat{};
+    const bool ordered = lat_order_mode() > 0 && F.n_lights == 1 &&
+                         (long long)gx * gy * nf <= kLatOrderRounds * lat_resident_wgs();
+    if (ordered) {
+        for (int q = 0; q < 2; ++q) {
+            CG_TRY(c, c->lcost[q].ensure((size_t)gx * gy), "alloc lattice order");
+            CG_TRY(c, c->lflat[q].ensure((size_t)gx * gy * sizeof(uint32_t)), "alloc lattice order");
+        }
+        const int src = (cold && c->lrec_key[k ^ 1] == key) ? (k ^ 1) : c->lrec_key[k] == key ? k : -1;
+        if (src >= 0) flat = LatFlatten{(const uint8_t *)c->lcost[src].p, (uint32_t *)c->lflat[k].p, gx * gy};
+    }
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)btc.p,
-                                (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm),
+                                (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm,
+                                flat.n > 0 ? &flat : nullptr),
            "rt_prepare launch");
+    if (ordered) {
+        if (flat.n < 0) order.flat = (const uint32_t *)c->lflat[k].p;   // sorted by the certificate launch
+        order.cost = (uint8_t *)c->lcost[k].p;
+        c->lrec_key[k] = key;
+        order.ngroups = -1;   // frame-major
+        if (lat_order_mode() == 2) {
+            order.ngroups = 0;
+            if (groups && ngroups > 0 && ngroups <= kLatMaxGroups) {
+                order.ngroups = ngroups;
+                for (int g = 0; g <= ngroups; ++g) order.gs[g] = groups[g];
+            }
+        }
+    }
     // light sets: the per-unit shadow certificates, with the other certificates
     unsigned long long *um = nullptr;
     if (rt_lattice_unit_bytes(F, nf)) {
@@ -875,7 +960,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     }
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
                                        (const RtSphere *)c->sph.p, lat, um, fc, nf, stride, (uint32_t *)d_out, st,
-                                       d_done),
+                                       d_done, ordered ? &order : nullptr),
            "rt_lattice launch");
     CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
     return CG_OK;
@@ -897,7 +982,7 @@ static size_t pix_bytes(int fmt) { return fmt == CG_PIX_RGB24 ? 3 : 4; }
 namespace cg {
 int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
                      const cg_rt_shard *shard, void *d_out, size_t frame_stride, int pix_format, void *stream,
-                     uint32_t *d_done, uint32_t *target);
+                     uint32_t *d_done, uint32_t *target, const int *group_starts, int ngroups);
 }
 
 extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int n_lights,
@@ -905,7 +990,7 @@ extern "C" int cg_rt_render_frames_device(cg_ctx *c, const cg_light *lights, int
                                           void *d_out, size_t frame_stride, int pix_format, void *stream)
 {
     return rt_render_frames(c, lights, n_lights, cams, n_frames, shard, d_out, frame_stride, pix_format, stream,
-                            nullptr, nullptr);
+                            nullptr, nullptr, nullptr, 0);
 }
 
 namespace cg {
@@ -913,9 +998,11 @@ namespace cg {
 // with d_done (signal memory, zeroed by the caller), frame f is complete once
 // d_done[f] >= target[f] (the lattice kernels count the frame's tiles as they
 // are stored; other paths write 1 after the frame's kernels).
+// group_starts (optional, ngroups + 1 entries, the last n_frames): frames
+// dispatched group after group (cg_dist's chunks, sent as each completes).
 int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cams, int n_frames,
                      const cg_rt_shard *shard, void *d_out, size_t frame_stride, int pix_format, void *stream,
-                     uint32_t *d_done, uint32_t *target)
+                     uint32_t *d_done, uint32_t *target, const int *group_starts, int ngroups)
 {
     if (!c || !d_out || n_frames < 0 || (n_frames && !cams)) return CG_E_INVALID;
     if (pix_format != CG_PIX_ARGB8888 && pix_format != CG_PIX_RGB24) return CG_E_INVALID;
@@ -987,8 +1074,18 @@ int rt_render_frames(cg_ctx *c, const cg_light *lights, int n_lights, const cg_r
     for (int f0 = 0; f0 < n_frames;) {
         const int nf = std::min(kMaxFrameBatch, n_frames - f0);
         uint32_t wg = 0;
+        uint8_t gs[kLatMaxGroups + 1];   // the groups within this launch's frames
+        int ng = 0;
+        if (group_starts && ngroups > 0) {
+            gs[0] = 0;
+            for (int g = 1; g <= ngroups && ng < kLatMaxGroups; ++g) {
+                const int e = std::min(group_starts[g], f0 + nf) - f0;
+                if (e > gs[ng]) gs[++ng] = (uint8_t)e;
+            }
+            if (ng == 0 || gs[ng] != nf) ng = 0;   // not covering the launch: one group
+        }
         rc = rt_enqueue_lattice_batch(c, F, cams + f0, nf, out + (size_t)f0 * fbytes, stride, st,
-                                      d_done ? d_done + f0 : nullptr, &wg);
+                                      d_done ? d_done + f0 : nullptr, &wg, ng ? gs : nullptr, ng);
         if (rc) return rc;
         if (d_done)
             for (int f = f0; f < f0 + nf; ++f) target[f] = wg;   // the launch's workgroups per frame
@@ -1118,7 +1215,7 @@ extern "C" int cg_rt_render_frames(cg_ctx *c, const cg_light *lights, int n_ligh
         const int s = j & 1, f0 = j * ch, nf = std::min(ch, n_frames - f0);
         if (j >= 2) CG_TRY(c, hipStreamWaitEvent(c->stream, c->ev_cdone[s], 0), "slot wait");   // chunk j - 2 downloaded
         int rc = rt_render_frames(c, lights, n_lights, cams + f0, nf, nullptr, c->hslot[s].p, px, CG_PIX_ARGB8888,
-                                  c->stream, nullptr, nullptr);
+                                  c->stream, nullptr, nullptr, nullptr, 0);
         if (rc) return rc;
         CG_TRY(c, hipEventRecord(c->ev_rdone[s], c->stream), "render event");
         if (j >= 1 && (rc = download(j - 1))) return rc;
