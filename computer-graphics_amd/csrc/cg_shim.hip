@@ -3,12 +3,17 @@
 // across the ABI; HIP failures become CG_E_HIP with the HIP message kept in
 // the context for cg_last_error().
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cg_internal.h"
@@ -82,6 +87,94 @@ struct DevBuf {
     }
 };
 
+// Host threads that store the certified-black columns of frames delivered
+// into host memory (cg_rt_render / cg_rt_render_frames): a frame's 3.2 MB of
+// black columns (C2) take one thread longer than the PCIe copy of its
+// window, so the rows are shared by the workers and the caller.  run() hands
+// out a job; wait() helps and returns when every row is stored.
+class HostFill {
+  public:
+    struct Frame {
+        uint32_t *dst;   // W x rows pixels, row pitch W
+    };
+    explicit HostFill(int n)
+    {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~HostFill()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void run(std::vector<Frame> frames, int W, int rows, int c0, int c1)
+    {
+        wait();
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fr_ = std::move(frames);
+            W_ = W;
+            rows_ = rows;
+            c0_ = c0;
+            c1_ = c1;
+            total_ = (int)fr_.size() * rows;
+            next_.store(0);
+            busy_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+    }
+    void wait()
+    {
+        work();
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return busy_ == 0; });
+    }
+
+  private:
+    static constexpr int kRowsPerGrab = 32;
+    void work()
+    {
+        for (;;) {
+            const int r0 = next_.fetch_add(kRowsPerGrab);
+            if (r0 >= total_) return;
+            const int r1 = std::min(total_, r0 + kRowsPerGrab);
+            for (int r = r0; r < r1; ++r) {
+                uint32_t *row = fr_[r / rows_].dst + (size_t)(r % rows_) * W_;
+                std::fill(row, row + c0_, 0x80000000u);   // PutPixelSDL(0, 0, 0)
+                std::fill(row + c1_, row + W_, 0x80000000u);
+            }
+        }
+    }
+    void loop()
+    {
+        unsigned seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> g(mu_);
+            if (--busy_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    bool quit_ = false;
+    unsigned gen_ = 0;
+    int busy_ = 0;
+    std::vector<Frame> fr_;
+    int W_ = 0, rows_ = 1, c0_ = 0, c1_ = 0, total_ = 0;
+    std::atomic<int> next_{0};
+};
+
 struct cg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -111,6 +204,7 @@ struct cg_ctx {
     hipStream_t xfer = nullptr;
     hipEvent_t ev_rdone[2] = {nullptr, nullptr}, ev_cdone[2] = {nullptr, nullptr};
     DevBuf hslot[2];
+    std::unique_ptr<HostFill> hfill;    // their black columns (created on first use)
     RtGrid grid{};                      // large scenes only (n_tris > 64)
     int pend_cap = 0;                   // cg_rt_set_pending_cap (0 = default)
     // large-scene pools (cg_rt_big.hip): capacities in entries, sized on the
@@ -1127,6 +1221,73 @@ extern "C" int cg_rt_assemble_device(cg_ctx *c, const void *d_src, int pix_forma
     return CG_OK;
 }
 
+// Host-buffer delivery of frames (cg_rt_render, cg_rt_render_frames): only the
+// columns the camera can see anything in (cg_rt_frame_columns, from the
+// scene's box) cross PCIe; the columns outside are certainly
+// PutPixelSDL(0, 0, 0) = 0x80000000 (no ray there can hit anything,
+// skeleton.cpp:160-166) and the host stores them itself while the GPU renders
+// and copies.  C2: columns 384-1551, 61 % of the bytes.  CG_DRAW_WINDOW=0:
+// whole rows (A/B runs).
+static bool draw_window_on()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("CG_DRAW_WINDOW");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// [c0, c1) of frame f's download; false: whole rows
+static bool draw_window(const cg_ctx *c, const cg_rt_camera *cam, int &c0, int &c1)
+{
+    c0 = 0;
+    c1 = cam->width;
+    if (!draw_window_on()) return false;
+    ctx_rt_columns(c, cam, &c0, &c1);
+    if (c1 <= c0) c0 = c1 = 0;   // nothing visible: a black frame, nothing to copy
+    return c0 > 0 || c1 < cam->width;
+}
+// frames of rows x W pixels (row pitch W): columns outside [c0, c1) black, on
+// the context's fill threads (CG_DRAW_THREADS, default min(8, cores / 2));
+// returns at once, HostFill::wait() before the frames are complete
+static HostFill *host_black_outside(cg_ctx *c, std::vector<HostFill::Frame> frames, int W, int rows, int c0, int c1)
+{
+    if (!c->hfill) {
+        const char *e = std::getenv("CG_DRAW_THREADS");
+        const int hw = (int)std::thread::hardware_concurrency();
+        const int n = e && *e ? std::atoi(e) : std::min(8, std::max(1, hw / 2));
+        c->hfill.reset(new HostFill(std::max(0, std::min(n, 64))));
+    }
+    c->hfill->run(std::move(frames), W, rows, c0, c1);
+    return c->hfill.get();
+}
+// D2H of frames [nf frames of W x H at src (pitch W, frame stride px)] into
+// dst (frame stride `stride`): the window's columns only (one pitched copy
+// when the frames are contiguous on both sides), or everything.
+static hipError_t download_frames(uint32_t *dst, size_t stride, const uint32_t *src, int W, int H, int nf, int c0,
+                                  int c1, bool window, hipStream_t st)
+{
+    const size_t px = (size_t)W * H;
+    if (!window) {
+        if (stride == px) return hipMemcpyAsync(dst, src, (size_t)nf * px * 4, hipMemcpyDeviceToHost, st);
+        for (int f = 0; f < nf; ++f) {
+            const hipError_t e = hipMemcpyAsync(dst + (size_t)f * stride, src + (size_t)f * px, px * 4,
+                                                hipMemcpyDeviceToHost, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    if (c1 <= c0) return hipSuccess;
+    if (stride == px)
+        return hipMemcpy2DAsync(dst + c0, (size_t)W * 4, src + c0, (size_t)W * 4, (size_t)(c1 - c0) * 4,
+                                (size_t)nf * H, hipMemcpyDeviceToHost, st);
+    for (int f = 0; f < nf; ++f) {
+        const hipError_t e = hipMemcpy2DAsync(dst + (size_t)f * stride + c0, (size_t)W * 4, src + (size_t)f * px + c0,
+                                              (size_t)W * 4, (size_t)(c1 - c0) * 4, H, hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
                             uint32_t *argb, cg_stats *stats)
 {
@@ -1141,8 +1302,14 @@ extern "C" int cg_rt_render(cg_ctx *c, const cg_light *lights, int n_lights, con
     rc = rt_enqueue(c, F, (uint32_t *)c->frame.p, c->stream);
     if (rc) return rc;
     CG_TRY(c, hipEventRecord(c->ev1, c->stream), "event");
-    CG_TRY(c, hipMemcpyAsync(argb, c->frame.p, (size_t)F.H * F.W * sizeof(uint32_t),
-                             hipMemcpyDeviceToHost, c->stream), "download frame");
+    int c0, c1;
+    const bool window = draw_window(c, cam, c0, c1);
+    // the black columns beside the render and the copy
+    HostFill *hf = window ? host_black_outside(c, {{argb}}, F.W, F.H, c0, c1) : nullptr;
+    const hipError_t e = download_frames(argb, (size_t)F.W * F.H, (const uint32_t *)c->frame.p, F.W, F.H, 1, c0, c1,
+                                         window, c->stream);
+    if (hf) hf->wait();
+    CG_TRY(c, e, "download frame");
     CG_TRY(c, hipStreamSynchronize(c->stream), "rt frame");
     if (stats) {
         float ms = 0.f;
@@ -1191,6 +1358,7 @@ extern "C" int cg_rt_render_frames(cg_ctx *c, const cg_light *lights, int n_ligh
         cg_ctx *c;
         ~Drain()
         {
+            if (c->hfill) c->hfill->wait();   // the host's black columns
             (void)hipStreamSynchronize(c->xfer);
             (void)hipStreamSynchronize(c->stream);
         }
@@ -1200,13 +1368,25 @@ extern "C" int cg_rt_render_frames(cg_ctx *c, const cg_light *lights, int n_ligh
     auto download = [&](int j) -> int {
         const int s = j & 1, f0 = j * ch, nf = std::min(ch, n_frames - f0);
         CG_TRY(c, hipStreamWaitEvent(c->xfer, c->ev_rdone[s], 0), "copy wait");
-        if (stride == px)
-            CG_TRY(c, hipMemcpyAsync(argb + (size_t)f0 * stride, c->hslot[s].p, (size_t)nf * px * sizeof(uint32_t),
-                                     hipMemcpyDeviceToHost, c->xfer), "download frames");
-        else
-            for (int f = 0; f < nf; ++f)
-                CG_TRY(c, hipMemcpyAsync(argb + (size_t)(f0 + f) * stride, (uint32_t *)c->hslot[s].p + (size_t)f * px,
-                                         px * sizeof(uint32_t), hipMemcpyDeviceToHost, c->xfer), "download frame");
+        // the chunk's union window (cg_rt_render's delivery, above)
+        int a = W, b = 0;
+        bool window = true;
+        for (int f = f0; f < f0 + nf && window; ++f) {
+            int x0, x1;
+            window = draw_window(c, &cams[f], x0, x1);
+            if (x1 > x0) {
+                a = std::min(a, x0);
+                b = std::max(b, x1);
+            }
+        }
+        if (a >= b) a = b = 0;
+        if (window) {   // the fill threads beside the copy (a pageable copy returns only when done)
+            std::vector<HostFill::Frame> fr;
+            for (int f = f0; f < f0 + nf; ++f) fr.push_back({argb + (size_t)f * stride});
+            host_black_outside(c, std::move(fr), W, H, a, b);
+        }
+        CG_TRY(c, download_frames(argb + (size_t)f0 * stride, stride, (const uint32_t *)c->hslot[s].p, W, H, nf, a, b,
+                                  window, c->xfer), "download frames");
         CG_TRY(c, hipEventRecord(c->ev_cdone[s], c->xfer), "copy event");
         return CG_OK;
     };

@@ -70,3 +70,32 @@ def test_render_frames_host_error_returns_cleanly(ctx):
     want = _per_frame(ctx, cams, cgamd.default_lights())
     out, _ = ctx.rt_render_frames(cams, None, chunk=2)
     assert np.array_equal(out.reshape(6, W * H), want)
+
+
+def test_render_host_window_columns_exact(ctx):
+    """Only the columns the camera can see anything in cross PCIe (cg_rt_frame_columns); the
+    host stores the rest as PutPixelSDL(0, 0, 0).  Cameras moving sideways (windows at either
+    edge, none at all), a yawed camera (whole rows) and a light set: cg_rt_render and
+    cg_rt_render_frames (pageable and pinned) == the device-resident frame, every pixel."""
+    W, H = 320, 256
+    tris, nt, sph = cgamd.rt_scene()
+    ctx.rt_set_scene(tris, nt, sph, 1)
+    xs = [-40.0, -1.6, -0.7, 0.0, 0.35, 1.1, 2.4, 40.0]
+    cams = [cgamd.rt_camera(W, H, 256.0, (x, 0.1 * k - 0.3, -3.0, 1.0)) for k, x in enumerate(xs)]
+    cams.append(cgamd.rt_camera(W, H, 256.0, (0.0, 0.0, -3.0, 1.0), cgamd.yaw_matrix(0.3)))
+    cols = [cgamd.frame_columns(tris, nt, sph, 1, c) for c in cams]
+    assert any(0 < c0 < c1 < W for c0, c1 in cols) and cols[0][0] >= cols[0][1]
+    for lights in (cgamd.default_lights(), cgamd.area_lights(cgamd.default_lights()[0], 0.1, 2)):
+        want = []
+        for c in cams:
+            d = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            ctx.rt_render_frames_device([c], d.data_ptr(), lights=lights)
+            torch.cuda.synchronize()
+            want.append(d.cpu().numpy().view(np.uint32).copy())
+        for k, c in enumerate(cams):
+            got, _ = ctx.rt_render(c, lights)
+            assert np.array_equal(got, want[k]), ("cg_rt_render", k)
+        for pinned in (False, True):
+            out, view = _host(len(cams) * W * H, pinned)
+            ctx.rt_render_frames(cams, out, chunk=3, lights=lights)
+            assert np.array_equal(view.reshape(len(cams), -1), np.stack(want)), ("frames", pinned)
