@@ -157,7 +157,7 @@ struct RastTriHdr {
 // ---- live kernel timing (cg_ktime.hip, cg_kernel_timing) ---------------
 enum KtId {
     KT_RT_PREPARE, KT_RT_TILE_CERT, KT_RT_LATTICE_UNITS, KT_RT_LATTICE, KT_RT_LATTICE_LIGHTS, KT_RT_PIXEL,
-    KT_RT_BIG_PRIMARY, KT_RT_SHADOW_HINTS, KT_RT_BIG_FRAME, KT_RAST_FILL, KT_RAST_POST, KT_RAST_FILL_POST, KT_COUNT
+    KT_RT_BIG_PRIMARY, KT_RT_SHADOW_HINTS, KT_RT_BIG_FRAME, KT_RAST_FILL, KT_RAST_POST, KT_COUNT
 };
 // HIP events on `st` around the scope's launches while timing is on (id
 // outside [0, KT_COUNT): nothing).

@@ -20,7 +20,7 @@ namespace cg {
 static const char *const kKtNames[KT_COUNT] = {
     "rt_prepare_kernel",        "rt_tile_cert_kernel",   "rt_lattice_units_kernel", "rt_lattice_kernel",
     "rt_lattice_lights_kernel", "rt_pixel_kernel",       "rt_big_primary_kernel",   "rt_shadow_hints_kernel",
-    "rt_big_frame",             "rast_fill_kernel",      "rast_post_kernel",        "rast_fill_post_kernel",
+    "rt_big_frame",             "rast_fill_kernel",      "rast_post_kernel",
 };
 
 namespace {

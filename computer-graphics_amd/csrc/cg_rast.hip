@@ -34,16 +34,6 @@ void *ctx_buf(cg_ctx *c, int which, size_t bytes, hipError_t *e);
 int ctx_fail(cg_ctx *c, hipError_t e, const char *what);
 int ctx_invalid(cg_ctx *c, const char *what);
 void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b);
-bool rast_fused_on(cg_ctx *c);
-static int rast_fused_diag()   // CG_RAST_FUSED_DIAG (diagnostic A/B only): 1 no waits, 4 fills before posts
-{
-    static const int d = [] {
-        const char *e = std::getenv("CG_RAST_FUSED_DIAG");
-        return e && *e ? std::atoi(e) : 0;
-    }();
-    return d;
-}
-void ctx_rast_fault_flag(cg_ctx *c, int *d_flag);
 
 constexpr int kSetupThreads = 256;
 constexpr int kRastMaxRows = 4096;   // LDS rows per triangle in span setup (H <= 4096)
@@ -349,8 +339,7 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
                                                        const RastSpan *__restrict__ spans,
                                                        const RastHdr *__restrict__ hdr,
                                                        const int *__restrict__ first_tri,
-                                                       RowRec *__restrict__ recs, int *__restrict__ count,
-                                                       int *__restrict__ row_done)
+                                                       RowRec *__restrict__ recs, int *__restrict__ count)
 {
     int m;
     const int g = xcd_group(A.H, kXcdRows / 4, m);
@@ -394,13 +383,7 @@ __global__ __launch_bounds__(256) void rast_rows_kernel(const cg_rtri *__restric
             c += __popcll(mk);
         }
     }
-    if (lane == 0) {
-        count[y] = c;
-        if (row_done) {   // rast_fill_post_kernel's per-row counts (and its fault flag) start at 0
-            row_done[y] = 0;
-            if (y == 0) row_done[A.H] = 0;
-        }
-    }
+    if (lane == 0) count[y] = c;
 }
 
 // Colour mode 0: fill -> post state, 4 bytes per pixel: 1 + the row record of
@@ -420,15 +403,22 @@ constexpr int kFillPx = 64;   // pixels per wave; 128 / 256 measured 3 % / 10 % 
 // TEX: texture modes 1-3 possible (A.textured): a fragment of texture 2/3
 // that passes the depth test but hits a transparent texel sets the depth to 0
 // and shades nothing (:619, :643, :665) -- decided in the ordered walk.
-// One fill unit: row y, pixels x0 .. x0 + 63, one per lane.  COH: the state
-// words are stored coherently at agent scope (rast_fill_post_kernel: post
-// tiles on other XCDs read them in the same launch).
-template <bool TEX, bool COH>
-__device__ __forceinline__ void fill_unit(const RastArgs &A, const RowRec *__restrict__ recs,
-                                          const int *__restrict__ count, uint32_t *__restrict__ state,
-                                          float *__restrict__ depth_out, int32_t *__restrict__ shadow_out, int y,
-                                          int x0, int lane)
+template <bool TEX>
+__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec *__restrict__ recs,
+                                                       const int *__restrict__ count, uint32_t *__restrict__ state,
+                                                       float *__restrict__ depth_out, int32_t *__restrict__ shadow_out)
 {
+    const int segs = (A.W + kFillPx - 1) / kFillPx;
+    // wave-uniform by construction; readfirstlane lets the compiler keep the
+    // record walk on the scalar unit (uniform branches)
+    int m;
+    const int g = xcd_group(A.H, (segs * kXcdRows + 3) / 4, m);
+    if (g < 0) return;
+    const int unit = m * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (row, segment) in the group
+    const int lane = threadIdx.x & 63;
+    const int y = g * kXcdRows + unit / segs;
+    if (unit >= segs * kXcdRows || y >= A.H) return;
+    const int x0 = (unit % segs) * kFillPx;
     const int x = x0 + lane;
     float depth = 0.0f;                                   // :247
     int shadow = 0, win = -1;                             // :259; record of the last shading fragment
@@ -492,42 +482,13 @@ __device__ __forceinline__ void fill_unit(const RastArgs &A, const RowRec *__res
             }
         }
     }
-    if (COH) {
-        // write-through (sc1) 16-B stores: lane 4 q stores the words of lanes
-        // 4 q .. 4 q + 3 (narrow sc1 stores publish several times slower;
-        // W % 4 == 0 on this path, MI355X_MICROARCH.md visibility table)
-        const uint32_t wv = (uint32_t)(win + 1) | (shadow ? kStShadow : 0u);
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const v4u q = {wv, (uint32_t)__shfl_down((int)wv, 1, 64), (uint32_t)__shfl_down((int)wv, 2, 64),
-                       (uint32_t)__shfl_down((int)wv, 3, 64)};
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(state, 0, A.W * A.H * 4, 0x00020000);
-        if ((lane & 3) == 0 && x < A.W) __builtin_amdgcn_raw_buffer_store_b128(q, rsrc, (y * A.W + x) * 4, 0, 16);
-    }
     if (x < A.W) {
         const size_t o = (size_t)y * A.W + x;
-        if (COH) {
-        } else if (A.state16) ((uint16_t *)state)[o] = (uint16_t)((win + 1) | (shadow ? 0x8000 : 0));
+        if (A.state16) ((uint16_t *)state)[o] = (uint16_t)((win + 1) | (shadow ? 0x8000 : 0));
         else state[o] = (uint32_t)(win + 1) | (shadow ? kStShadow : 0u);
         if (depth_out) depth_out[o] = depth;
         if (shadow_out) shadow_out[o] = shadow;
     }
-}
-
-template <bool TEX>
-__global__ __launch_bounds__(256) void rast_fill_kernel(RastArgs A, const RowRec *__restrict__ recs,
-                                                       const int *__restrict__ count, uint32_t *__restrict__ state,
-                                                       float *__restrict__ depth_out, int32_t *__restrict__ shadow_out)
-{
-    const int segs = (A.W + kFillPx - 1) / kFillPx;
-    // wave-uniform by construction; readfirstlane lets the compiler keep the
-    // record walk on the scalar unit (uniform branches)
-    int m;
-    const int g = xcd_group(A.H, (segs * kXcdRows + 3) / 4, m);
-    if (g < 0) return;
-    const int unit = m * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (row, segment) in the group
-    const int y = g * kXcdRows + unit / segs;
-    if (unit >= segs * kXcdRows || y >= A.H) return;
-    fill_unit<TEX, false>(A, recs, count, state, depth_out, shadow_out, y, (unit % segs) * kFillPx, threadIdx.x & 63);
 }
 
 // shade buffers of one pixel as they stand after the fill (:580-585), from its
@@ -601,13 +562,12 @@ constexpr int kPostTW = 64, kPostTH = 8;
 constexpr int kPostHW = kPostTW + 2, kPostHH = kPostTH + 2;      // shade halo 1
 constexpr int kPostSW = kPostTW + 4, kPostSH = kPostTH + 4;      // shadow halo 2
 
-// One post tile: row group g (rows g * kPostTH ..), columns m * kPostTW ..
-// COH: the state words are read coherently at agent scope (written by fill
-// units of the same launch, rast_fill_post_kernel; 4-byte state words).
-template <bool DIRECT, bool TEX, bool COH>
-__device__ __forceinline__ void post_tile(const cg_rtri *__restrict__ tris, const RastArgs &A0,
-                                          const void *__restrict__ state_v, const RowRec *__restrict__ recs,
-                                          const int32_t *__restrict__ sh, uint32_t *__restrict__ argb, int g, int m)
+template <bool DIRECT, bool TEX>
+__global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A0,
+                                                       const void *__restrict__ state_v,
+                                                       const RowRec *__restrict__ recs,
+                                                       const int32_t *__restrict__ sh,
+                                                       uint32_t *__restrict__ argb)
 {
     RastArgs A = A0;
     if (!DIRECT && A.d_light) {                           // light from the device geometry (:223)
@@ -625,11 +585,13 @@ __device__ __forceinline__ void post_tile(const cg_rtri *__restrict__ tris, cons
     int (*s_sh)[kPostSW] = reinterpret_cast<int (*)[kPostSW]>(&s_c[0][0][0]);
     const int W = A.W, H = A.H;
     static_assert(kPostTH == kXcdRows, "a post tile row is one XCD row group");
+    int m;
+    const int g = xcd_group(H, (W + kPostTW - 1) / kPostTW, m);
+    if (g < 0) return;
     const int gx0 = m * kPostTW, gy0 = g * kPostTH;
     const uint32_t *st4 = static_cast<const uint32_t *>(state_v);
     const uint16_t *st2 = static_cast<const uint16_t *>(state_v);
     auto state_at = [&](size_t o) -> uint32_t {   // the 4-byte form
-        if (COH) return __hip_atomic_load(const_cast<uint32_t *>(&st4[o]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!A.state16) return st4[o];
         const uint32_t v = st2[o];
         return (v & 0x7fffu) | ((v >> 15) << 31);
@@ -779,127 +741,6 @@ __device__ __forceinline__ void post_tile(const cg_rtri *__restrict__ tris, cons
     }
 }
 
-template <bool DIRECT, bool TEX>
-__global__ __launch_bounds__(256) void rast_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A0,
-                                                       const void *__restrict__ state_v,
-                                                       const RowRec *__restrict__ recs,
-                                                       const int32_t *__restrict__ sh,
-                                                       uint32_t *__restrict__ argb)
-{
-    int m;
-    const int g = xcd_group(A0.H, (A0.W + kPostTW - 1) / kPostTW, m);
-    if (g < 0) return;
-    post_tile<DIRECT, TEX, false>(tris, A0, state_v, recs, sh, argb, g, m);
-}
-
-// Fill and post-pass in one launch (colour mode 0), a post tile starting as
-// soon as the rows it reads are filled instead of after the whole fill: the
-// fill's tail and the post's head overlap.  Roles by dispatch order: XCD k
-// (workgroup ids = k mod 8, dispatched in order on that XCD) runs its row
-// groups g = k, k + 8, .. as in the split kernels, in steps j = 0 .. J: the
-// fill units of group k + 8 j, then the post tiles of group k + 8 (j - 1).
-// Post tile g reads the state of rows 8 g - 2 .. 8 g + 9: groups g - 1, g,
-// g + 1 -- the neighbours' fills come earlier in their XCDs' orders (group
-// g + 1 on XCD k + 1 at step j - 1, before that XCD's post of step j - 1), so
-// every wait is on work that cannot itself be waiting on this one.  Each fill
-// wave stores its state coherently, waits for the stores and counts its row
-// in row_done; a post tile's first threads poll its rows' counts.  The polls
-// are bounded (~2 ms): a post that times out sets *err (the host then takes
-// the split kernels) -- never a hang.
-template <bool TEX>
-__global__ __launch_bounds__(256) void rast_fill_post_kernel(const cg_rtri *__restrict__ tris, RastArgs A,
-                                                            const RowRec *__restrict__ recs,
-                                                            const int *__restrict__ count, uint32_t *__restrict__ state,
-                                                            float *__restrict__ depth_out,
-                                                            int32_t *__restrict__ shadow_out, uint32_t *__restrict__ argb,
-                                                            int *__restrict__ row_done, int *__restrict__ err, int diag)
-{
-    const int segs = (A.W + kFillPx - 1) / kFillPx;
-    const int fper = (segs * kXcdRows + 3) / 4, pper = (A.W + kPostTW - 1) / kPostTW;
-    const int G = (A.H + kXcdRows - 1) / kXcdRows, J = (G + kXcds - 1) / kXcds;
-    const int k = (int)(blockIdx.x % kXcds);
-    int l = (int)(blockIdx.x / kXcds), j;
-    bool fill;
-    if (diag & 4) {   // diagnostic: every fill before every post (split order in one launch)
-        const int nf = kXcds * J * fper;
-        const int b = (int)blockIdx.x < nf ? (int)blockIdx.x : (int)blockIdx.x - nf;
-        fill = (int)blockIdx.x < nf;
-        const int kk = b % kXcds, ll = b / kXcds;
-        j = fill ? ll / fper : ll / pper + 1;
-        l = fill ? ll % fper : ll % pper;
-        if (fill) {
-            const int g = kk + kXcds * j;
-            const int unit = l * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            const int y = g * kXcdRows + unit / segs;
-            if (g >= G || unit >= segs * kXcdRows || y >= A.H) return;
-            fill_unit<TEX, true>(A, recs, count, state, depth_out, shadow_out, y, (unit % segs) * kFillPx, threadIdx.x & 63);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(&row_done[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        const int g = kk + kXcds * (j - 1);
-        if (g >= G || l >= pper) return;
-        const int y0 = max(0, g * kXcdRows - 2), y1 = min(A.H, g * kXcdRows + kXcdRows + 2);
-        if ((int)threadIdx.x < y1 - y0 && !(diag & 1)) {
-            const unsigned long long t_end = wall_clock64() + 200000ull;
-            while (__hip_atomic_load(&row_done[y0 + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < segs) {
-                if (wall_clock64() > t_end) {
-                    atomicOr(err, 1);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __syncthreads();
-        post_tile<false, TEX, true>(tris, A, state, recs, nullptr, argb, g, l);
-        return;
-    }
-    if (l < fper) {
-        j = 0;
-        fill = true;
-    } else {
-        l -= fper;
-        j = 1 + l / (fper + pper);
-        l -= (j - 1) * (fper + pper);
-        fill = j < J && l < fper;
-        if (!fill) l -= j < J ? fper : 0;
-    }
-    if (fill) {
-        const int g = k + kXcds * j;
-        const int unit = l * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int y = g * kXcdRows + unit / segs;
-        if (g >= G || unit >= segs * kXcdRows || y >= A.H) return;
-        const int lane = threadIdx.x & 63;
-        fill_unit<TEX, true>(A, recs, count, state, depth_out, shadow_out, y, (unit % segs) * kFillPx, lane);
-        // the wave's state stores complete (visible at agent scope), then its row counts it
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_s_waitcnt(0);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0) __hip_atomic_fetch_add(&row_done[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const int g = k + kXcds * (j - 1);
-    if (g >= G || l >= pper) return;
-    // wait for rows 8 g - 2 .. 8 g + 9 (those in the frame)
-    const int y0 = max(0, g * kXcdRows - 2), y1 = min(A.H, g * kXcdRows + kXcdRows + 2);
-    const int t = threadIdx.x;
-    if (t < y1 - y0 && !(diag & 1)) {
-        const unsigned long long t_end = wall_clock64() + 200000ull;   // 100 MHz: 2 ms
-        while (__hip_atomic_load(&row_done[y0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < segs) {
-            if (wall_clock64() > t_end) {
-                atomicOr(err, 1);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __syncthreads();
-    post_tile<false, TEX, true>(tris, A, state, recs, nullptr, argb, g, l);
-}
-
 int rast_colour_fill(cg_ctx *c, const RastArgs &A, const cg_rast_params *p, const RowRec *recs, const int *count,
                      const RastHdr *hdr, const int *n_dev, int max_recs, float4 *state, float *d_depth,
                      int32_t *shadow, hipStream_t st, long long *n_shaded);
@@ -1013,11 +854,9 @@ static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg
     // fill -> post state: 4 B/pixel in colour mode 0, the colour fill's 16 B in modes 1-2
     void *state = ctx_buf(c, 3, npx * (p->colour_mode == 0 ? sizeof(uint32_t) : sizeof(float4)), &e);
     if (!state) return ctx_fail(c, e, "alloc state");
-    // count[H] | first_tri | row_done[H] + the fused kernel's fault flag
-    int *misc = (int *)ctx_buf(c, 7, (2 * (size_t)H + 32) * sizeof(int), &e);
+    int *misc = (int *)ctx_buf(c, 7, ((size_t)H + 16) * sizeof(int), &e);   // count[H] | first_tri
     if (!misc) return ctx_fail(c, e, "alloc counts");
-    int *count = misc, *first_tri = misc + H, *row_done = misc + H + 16;
-    const bool fused = p->colour_mode == 0 && W % 4 == 0 && rast_fused_on(c);   // 16-B state stores
+    int *count = misc, *first_tri = misc + H;
     RowRec *recs = (RowRec *)ctx_buf(c, 8, (size_t)H * nn * sizeof(RowRec), &e);
     if (!recs) return ctx_fail(c, e, "alloc row records");
     int32_t *shadow = d_shadow;   // mode 0 carries the marks in the state; modes 1-2 need the plane
@@ -1044,7 +883,7 @@ static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg
         return ctx_invalid(c, "marble: normalMap_marble[y * 2000 + x] would index past the map");
     A.textured = (tex_mask & 0xe) != 0;
     A.use_inv = p->yaw != 0.0f;
-    A.state16 = p->colour_mode == 0 && nn < 32768 && !fused;   // the fused kernel's coherent stores: 4-byte words
+    A.state16 = p->colour_mode == 0 && nn < 32768;
     A.tris = d_tris;
     A.cam[0] = p->camera.x; A.cam[1] = p->camera.y; A.cam[2] = p->camera.z; A.cam[3] = p->camera.w;
     mat4_inverse_glm(p->R, A.Rinv);
@@ -1062,7 +901,7 @@ static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg
         if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_setup launch");
     }
     hipLaunchKernelGGL(rast_rows_kernel, dim3(xcd_grid(H, kXcdRows / 4)), dim3(256), 0, st, d_tris, A, n_dev, spans, hdr,
-                       first_tri, recs, count, fused ? row_done : nullptr);
+                       first_tri, recs, count);
     if ((e = hipGetLastError()) != hipSuccess) return ctx_fail(c, e, "rast_rows launch");
     const int post_grid = xcd_grid(H, (W + kPostTW - 1) / kPostTW);
     if (p->colour_mode != 0) {
@@ -1072,20 +911,6 @@ static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg
         if (stats) stats->n_shaded = ns;
         hipLaunchKernelGGL((rast_post_kernel<true, false>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
                            (const void *)state, (const RowRec *)recs, shadow, d_argb);
-    } else if (fused) {
-        const int fper = ((W + kFillPx - 1) / kFillPx * kXcdRows + 3) / 4, pper = (W + kPostTW - 1) / kPostTW;
-        const int G = (H + kXcdRows - 1) / kXcdRows, J = (G + kXcds - 1) / kXcds;
-        KtScope kt(KT_RAST_FILL_POST, st);
-        if (A.textured)
-            hipLaunchKernelGGL(rast_fill_post_kernel<true>, dim3(kXcds * J * (fper + pper)), dim3(256), 0, st, d_tris,
-                               A, recs, count, (uint32_t *)state, d_depth, d_shadow, d_argb, row_done, row_done + H,
-                               rast_fused_diag());
-        else
-            hipLaunchKernelGGL(rast_fill_post_kernel<false>, dim3(kXcds * J * (fper + pper)), dim3(256), 0, st, d_tris,
-                               A, recs, count, (uint32_t *)state, d_depth, d_shadow, d_argb, row_done, row_done + H,
-                               rast_fused_diag());
-        if (stats) stats->n_shaded = -1;
-        ctx_rast_fault_flag(c, row_done + H);
     } else {
         const int fgrid = xcd_grid(H, ((W + kFillPx - 1) / kFillPx * kXcdRows + 3) / 4);
         {

@@ -255,8 +255,6 @@ struct cg_ctx {
     hipEvent_t lane_ev[kRastLanes] = {};
     hipEvent_t start_ev = nullptr;
     unsigned scene_gen = 0, lane_gen[kRastLanes] = {};
-    bool rast_fused_fault = false;       // a fused fill -> post frame timed out: split kernels from now on
-    int *rast_fault_flag = nullptr;      // the last fused frame's fault flag (device)
 };
 
 namespace cg {
@@ -316,17 +314,6 @@ void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b)
     *a = c->ev0;
     *b = c->ev1;
 }
-// The fused fill -> post kernel (cg_rast.hip rast_fill_post_kernel), unless
-// CG_RAST_FUSED=0 or a fused frame of this context reported a timed-out wait.
-bool rast_fused_on(cg_ctx *c)
-{
-    static const bool env = [] {
-        const char *e = std::getenv("CG_RAST_FUSED");
-        return !(e && e[0] == '0');
-    }();
-    return env && !c->rast_fused_fault;
-}
-void ctx_rast_fault_flag(cg_ctx *c, int *d_flag) { c->rast_fault_flag = d_flag; }
 void rast_release(cg_ctx *c)
 {
     c->rtris.release(); c->rhdr.release(); c->rspan.release(); c->rpix.release();
@@ -1744,20 +1731,9 @@ extern "C" int cg_rast_draw(cg_ctx *c, const cg_rast_params *p, uint32_t *argb, 
     int32_t *d_shadow = (int32_t *)ctx_buf(c, 6, npx * 4, &e);
     if (!d_shadow) return ctx_fail(c, e, "alloc shadow");
     int *d_n = nullptr;
-    c->rast_fault_flag = nullptr;
     int rc = rast_draw_device(c, (const cg_rtri *)c->rroom.p, c->n_room, (const cg_rtri *)c->rboxes.p, c->n_boxes, p,
                               d_argb, d_depth, d_shadow, c->stream, stats, &d_n, c->scene_tex);
     if (rc) return rc;
-    if (c->rast_fault_flag) {   // a fused frame whose post waited past its bound is redrawn split
-        int fault = 0;
-        CG_TRY(c, hipMemcpyAsync(&fault, c->rast_fault_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream),
-               "d2h fault");
-        CG_TRY(c, hipStreamSynchronize(c->stream), "rast frame");
-        if (fault) {
-            c->rast_fused_fault = true;
-            return cg_rast_draw(c, p, argb, depth, shadow, stats);
-        }
-    }
     int n = 0;
     CG_TRY(c, hipMemcpyAsync(&n, d_n, sizeof(int), hipMemcpyDeviceToHost, c->stream), "d2h count");
     CG_TRY(c, hipMemcpyAsync(argb, d_argb, npx * 4, hipMemcpyDeviceToHost, c->stream), "d2h argb");
