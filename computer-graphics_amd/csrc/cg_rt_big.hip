@@ -1176,15 +1176,36 @@ __global__ __launch_bounds__(1024) void rt_walk_order_kernel(BigBufs B, int gx, 
     for (int w = t; w < n; w += 1024) B.walk_order[atomicAdd(&s_cnt[cls(w)], 1)] = w;
 }
 
+// An opaque copy of v: values derived from it are recomputed where they are
+// used instead of being hoisted (and kept live) across a loop.
+__device__ __forceinline__ int launder(int v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+#ifndef CG_WALK_PARK
+#define CG_WALK_PARK 1   // the walk parks its ray slots in LDS around each certificate batch (A/B: 0)
+#endif
+// Waves per SIMD of the walk: the lattice mode (C5) fits 4 in 123 VGPRs with
+// no scratch once its slots are parked and its wave index is uniform; the
+// yawed (7 slots) and per-pixel (9 slots) modes need 3 for no scratch.
+// CG_WALK_WAVES overrides every mode (A/B builds).
+#ifdef CG_WALK_WAVES
+template <int LM> constexpr int walk_waves() { return CG_WALK_WAVES; }
+#else
+template <int LM> constexpr int walk_waves() { return LM == 1 ? 4 : 3; }
+#endif
+
 template <int LM>   // 0: per-pixel mode, 1: lattice, 2: lattice with per-pixel columns
-__global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, walk_waves<LM>()) void rt_big_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                     const RtShade *__restrict__ shade,
                                                                     const RtSphere *__restrict__ sph, BigBufs B)
 {
     WGTB_T0;
     constexpr bool kLat = LM > 0;
     constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     int bx = blockIdx.x, by = blockIdx.y;
     if (B.walk_order) {   // heavy-first (rt_walk_order_kernel): the long lists start early, not in the tail
         const int w = __builtin_amdgcn_readfirstlane(B.walk_order[blockIdx.y * gridDim.x + blockIdx.x]);
@@ -1200,38 +1221,53 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
     vec4 dir = v4(0.0f, 0.0f, 0.0f, 0.0f);
     int u = 0, L = 0, nsu = NS;
     float x0, x1, y0, y1;
+    // The slots' geometry from the lane index (formed again after each parked
+    // certificate batch, from a laundered lane, so it is not live across the
+    // certificate's FP64 code)
+    auto geom = [&](int ln) {
+        if constexpr (kLat) {
+            const LatOwn o = lat_own(F, B, tx, ty);
+            const int n = o.nx * o.ny;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int k = s * 64 + ln;
+                on[s] = k < n;
+                const int kk = on[s] ? k : 0;
+                rx[s] = lat_x(F, B, o.xi0 + kk % max(o.nx, 1));
+                ry[s] = lat_y(F, o.yi0 + kk / max(o.nx, 1));
+            }
+        } else {
+            u = tx * 8 + (ln & 7);
+            L = ty * 8 + (ln >> 3);
+            const bool inside = u < F.W && L < F.rows_out;
+            const int v = inside ? shard_row(F, L) : 0;
+            const bool active = inside && v < F.H;
+            dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
+            dir = mat4_mul(F.R, dir);                                                    // :128
+#pragma unroll
+            for (int s = 0; s < NS; ++s) on[s] = active;
+        }
+    };
+    geom(lane);
     if constexpr (kLat) {
         const LatOwn o = lat_own(F, B, tx, ty);
-        const int n = o.nx * o.ny;
-        nsu = __builtin_amdgcn_readfirstlane((n + 63) >> 6);
+        nsu = __builtin_amdgcn_readfirstlane((o.nx * o.ny + 63) >> 6);
         float a0 = FLT_MAX, a1 = -FLT_MAX, b0 = FLT_MAX, b1 = -FLT_MAX;
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const int k = s * 64 + lane;
-            on[s] = k < n;
-            const int kk = on[s] ? k : 0;
-            rx[s] = lat_x(F, B, o.xi0 + kk % max(o.nx, 1));
-            ry[s] = lat_y(F, o.yi0 + kk / max(o.nx, 1));
+        for (int s = 0; s < NS; ++s)
             if (on[s]) {
                 a0 = fminf(a0, rx[s]); a1 = fmaxf(a1, rx[s]);
                 b0 = fminf(b0, ry[s]); b1 = fmaxf(b1, ry[s]);
             }
-        }
         x0 = wave_min(a0); x1 = wave_max(a1); y0 = wave_min(b0); y1 = wave_max(b1);
     } else {
-        u = tx * 8 + (lane & 7);
-        L = ty * 8 + (lane >> 3);
-        const bool inside = u < F.W && L < F.rows_out;
-        const int v = inside ? shard_row(F, L) : 0;
-        const bool active = inside && v < F.H;
-        dir = v4((float)(u - F.W / 2), (float)(v - F.H / 2), F.focal, 1.0f);        // :126
-        dir = mat4_mul(F.R, dir);                                                    // :128
-#pragma unroll
-        for (int s = 0; s < NS; ++s) on[s] = active;
+        const bool active = on[0];
         x0 = wave_min(active ? dir.x : FLT_MAX); x1 = wave_max(active ? dir.x : -FLT_MAX);
         y0 = wave_min(active ? dir.y : FLT_MAX); y1 = wave_max(active ? dir.y : -FLT_MAX);
         x0 = x0 - 0.5f; x1 = x1 + 0.5f; y0 = y0 - 0.5f; y1 = y1 + 0.5f;
     }
+    // the wave's bundle is uniform: SGPRs, not four VGPRs live through the walk
+    x0 = uniform_f32(x0); x1 = uniform_f32(x1); y0 = uniform_f32(y0); y1 = uniform_f32(y1);
     auto slot_nd = [&](int s) -> vec3 {                                              // :137
         if constexpr (kLat) return v3(rx[s], ry[s], F.focal);
         else return v3(dir.x + (m * (float)(s / 3 - 1)), dir.y + (m * (float)(s % 3 - 1)), F.focal);
@@ -1266,10 +1302,33 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
 #ifdef CG_WALK_STATS
     int st_chunks = 0, st_pass = 0, st_batches = 0, st_walked = 0, st_buckets = 0, st_all = 0, st_wide = 0;
 #endif
+#if CG_WALK_PARK
+    // the slots' running minima parked in LDS while the certificate's FP64
+    // code runs (its registers would otherwise spill them to scratch)
+    __shared__ float s_park[kRtThreads / 64][3 * NS][64];
+#endif
     auto certify_walk = [&](int cnt) {                             // the first cnt (<= 64) queued entries
         const int cand = lane < cnt ? q_w[lane] : -1;
+#if CG_WALK_PARK
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            s_park[wave][s][lane] = best[s];
+            s_park[wave][NS + s][lane] = bt[s];
+            s_park[wave][2 * NS + s][lane] = __int_as_float(bi[s]);
+        }
+#endif
         const bool keep = cand >= 0 && !cull_primary(tc[cand], x0, x1, y0, y1, F.focal);
         unsigned long long mask = __ballot(keep);
+#if CG_WALK_PARK
+        geom(launder(lane));
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            best[s] = s_park[wave][s][lane];
+            bt[s] = s_park[wave][NS + s][lane];
+            bi[s] = __float_as_int(s_park[wave][2 * NS + s][lane]);
+            len[s] = length(slot_nd(s));                                             // :307
+        }
+#endif
 #ifdef CG_WALK_STATS
         ++st_batches;
         st_walked += __popcll(mask);
@@ -1289,7 +1348,7 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
 #pragma unroll
         for (int s = 0; s < NS; ++s)
             if (on[s]) lm = fmaxf(lm, best[s]);
-        tb = wave_max(lm);
+        tb = uniform_f32(wave_max(lm));
     };
     if (B.bin_over[bin]) {   // overflowed bin list: every triangle through the wave's certificate
         for (int c0 = 0; any && c0 < F.n_tris; c0 += 64) {
@@ -1305,13 +1364,15 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
 #ifdef CG_WALK_STATS
         ++st_buckets;
 #endif
-        // the next chunk's entries are loaded while this one is scanned
-        unsigned long long ent_n = b0 + lane < b1 ? list[b0 + lane] : 0ull;
-        unsigned long long pb_n = b0 + lane < b1 ? pboxes[b0 + lane] : 0ull;
+        // the next chunk's entries are loaded while this one is scanned (the
+        // lane's addresses formed per bucket, not hoisted and spilled)
+        const int ln = launder(lane);
+        unsigned long long ent_n = b0 + ln < b1 ? list[b0 + ln] : 0ull;
+        unsigned long long pb_n = b0 + ln < b1 ? pboxes[b0 + ln] : 0ull;
         for (int c0 = b0; c0 < b1; c0 += 64) {
-            const bool in = c0 + lane < b1;
+            const bool in = c0 + ln < b1;
             const unsigned long long ent = ent_n, pb = pb_n;
-            const int cn = c0 + 64 + lane;
+            const int cn = c0 + 64 + ln;
             ent_n = cn < b1 ? list[cn] : 0ull;
             pb_n = cn < b1 ? pboxes[cn] : 0ull;
             // projected box first (no gather), then the key
@@ -1372,7 +1433,7 @@ __global__ __launch_bounds__(kRtThreads, 3) void rt_big_primary_kernel(RtFrame F
         const int hit = best[s] < FLT_MAX ? bi[s] : INT_MIN;                         // :357
         size_t id;
         if constexpr (kLat) {
-            const int k = s * 64 + lane;
+            const int k = s * 64 + launder(lane);   // not the start's k / nx, kept live (spilled) till here
             id = (size_t)(o.yi0 + k / o.nx) * B.lat_w + o.xi0 + k % o.nx;
         } else {
             id = s * npix + pix;
@@ -1534,19 +1595,37 @@ __device__ int grid_blocker(const RtGrid &G, const RtTri *__restrict__ tc, const
             tdel[a] = G.h / fabsf(d[a]);
         }
     }
+    // the walk with one named variable per axis: indexing the arrays by the
+    // runtime axis kept them in scratch memory (88 B per lane)
+    int cx = c[0], cy = c[1], cz = c[2];
+    float mx = tmax[0], my = tmax[1], mz = tmax[2];
+    const float dx = tdel[0], dy = tdel[1], dz = tdel[2];
+    const int sx = step[0], sy = step[1], sz = step[2];
     const int max_steps = G.res[0] + G.res[1] + G.res[2] + 3;
     for (int it = 0; it < max_steps; ++it) {
-        const int cell = (c[2] * G.res[1] + c[1]) * G.res[0] + c[0];
+        const int cell = (cz * G.res[1] + cy) * G.res[0] + cx;
         for (int i = G.start[cell], e = G.start[cell + 1]; i < e; ++i) {
             const int k = G.tris[i];
             if (ntest) ++*ntest;
             if (tri_shadows(tc[k], q.origin, q.nd, q.len, q.rmag)) return k;
         }
-        const int a = tmax[0] < tmax[1] ? (tmax[0] < tmax[2] ? 0 : 2) : (tmax[1] < tmax[2] ? 1 : 2);
-        if (tmax[a] > t1) break;
-        c[a] += step[a];
-        if (c[a] < 0 || c[a] >= G.res[a]) break;
-        tmax[a] += tdel[a];
+        // axis a = tmax[0] < tmax[1] ? (tmax[0] < tmax[2] ? 0 : 2) : (tmax[1] < tmax[2] ? 1 : 2)
+        const int a = mx < my ? (mx < mz ? 0 : 2) : (my < mz ? 1 : 2);
+        const float ma = a == 0 ? mx : a == 1 ? my : mz;
+        if (ma > t1) break;
+        if (a == 0) {
+            cx += sx;
+            if (cx < 0 || cx >= G.res[0]) break;
+            mx += dx;
+        } else if (a == 1) {
+            cy += sy;
+            if (cy < 0 || cy >= G.res[1]) break;
+            my += dy;
+        } else {
+            cz += sz;
+            if (cz < 0 || cz >= G.res[2]) break;
+            mz += dz;
+        }
     }
     return -1;
 }
@@ -1582,15 +1661,18 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // n_lights + l, lattice mode point bits l.  Every lane walks the same (slot,
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
+#ifndef CG_HINT_WAVES
+#define CG_HINT_WAVES 6
+#endif
 template <int LM>
-__global__ __launch_bounds__(kRtThreads, 6) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
+__global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
                                                                      const RtSphere *__restrict__ sph, BigBufs B)
 {
     WGTB_T0;
     constexpr bool kLat = LM > 0;
     constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
     const float m = 0.5f;
@@ -1621,7 +1703,9 @@ __global__ __launch_bounds__(kRtThreads, 6) void rt_shadow_hints_kernel(RtFrame 
         vec3 nd;
         size_t id;
         if constexpr (kLat) {
-            const int k = s * 64 + lane;
+            // per slot from a laundered lane: hoisted, these per-lane values
+            // lived through the slot loop and spilled to scratch at 6 waves/SIMD
+            const int k = s * 64 + launder(lane);
             on = k < n;
             const int kk = on ? k : 0, Xi = o.xi0 + kk % max(o.nx, 1), Yi = o.yi0 + kk / max(o.nx, 1);
             nd = v3(lat_x(F, B, Xi), lat_y(F, Yi), F.focal);
@@ -1950,7 +2034,7 @@ __global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, con
                                                                   uint32_t *__restrict__ out)
 {
     constexpr bool kLat = LM > 0;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
     if (tx >= B.tiles_x) return;
     const int u = tx * 8 + (lane & 7), L = ty * 8 + (lane >> 3);

@@ -491,6 +491,11 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v)
     return ((unsigned long long)hi << 32) | lo;
 }
 
+__device__ __forceinline__ float uniform_f32(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 __device__ __forceinline__ float wave_min(float v)
 {
 #pragma unroll
