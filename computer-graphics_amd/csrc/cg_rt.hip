@@ -997,7 +997,7 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     tc += (size_t)frame * F.n_tris;
     lat_masks += (size_t)frame * lat_tiles_x(F) * gridDim.y * 2;
     const LatOut o = lat_out(F, frame, out_stride, out);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int by = S.by, bx = F.tx0 + S.bx;
     LatTile G = lat_tile(F, bx, by);
     G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here

@@ -1096,9 +1096,12 @@ __device__ __forceinline__ LatOwn lat_own(const RtFrame &F, const BigBufs &B, in
 // x of lattice column Xi: the half-pixel lattice, or (yawed camera, see
 // cg_rt.hip lat_yaw) pixel Xi / 3's sub-ray i = Xi % 3 - 1, fl(dir.x + 0.5 i)
 // -- dir.x formed with y = 0, which only changes the sign of a zero dir.x.
+// LM (the kernels' mode): 1 is the unrotated lattice, so the yaw form is not
+// even compiled there (its uniform pieces otherwise held registers).
+template <int LM = 0>
 __device__ __forceinline__ float lat_x(const RtFrame &F, const BigBufs &B, int Xi)
 {
-    if (!B.lat_yaw) return 0.5f * (float)(Xi - 1 - 2 * (F.W / 2));
+    if (LM == 1 || !B.lat_yaw) return 0.5f * (float)(Xi - 1 - 2 * (F.W / 2));
     const int u = Xi / 3, i = Xi - 3 * u - 1;
     return mat4_mul(F.R, v4((float)(u - F.W / 2), 0.0f, F.focal, 1.0f)).x + (0.5f * (float)i);   // :126-137
 }
@@ -1233,7 +1236,7 @@ __global__ __launch_bounds__(kRtThreads, walk_waves<LM>()) void rt_big_primary_k
                 const int k = s * 64 + ln;
                 on[s] = k < n;
                 const int kk = on[s] ? k : 0;
-                rx[s] = lat_x(F, B, o.xi0 + kk % max(o.nx, 1));
+                rx[s] = lat_x<LM>(F, B, o.xi0 + kk % max(o.nx, 1));
                 ry[s] = lat_y(F, o.yi0 + kk / max(o.nx, 1));
             }
         } else {
@@ -1662,7 +1665,7 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
 #ifndef CG_HINT_WAVES
-#define CG_HINT_WAVES 6
+#define CG_HINT_WAVES 5   // 12-16 B of scratch (one value per slot); 6: 68-76 B, same speed (r05)
 #endif
 template <int LM>
 __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
@@ -1708,7 +1711,7 @@ __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_ker
             const int k = s * 64 + launder(lane);
             on = k < n;
             const int kk = on ? k : 0, Xi = o.xi0 + kk % max(o.nx, 1), Yi = o.yi0 + kk / max(o.nx, 1);
-            nd = v3(lat_x(F, B, Xi), lat_y(F, Yi), F.focal);
+            nd = v3(lat_x<LM>(F, B, Xi), lat_y(F, Yi), F.focal);
             id = (size_t)Yi * B.lat_w + Xi;
             shadowed = pending = 0ull;
         } else {

@@ -197,6 +197,7 @@ struct cg_ctx {
     // measured lattice order (LatOrder, cg_internal.h): per slot, the recording
     // of its last lattice launch (class per tile) and the order sorted for it
     DevBuf lcost[2], lflat[2];
+    int umask_frames = 0;                            // light sets: frames the unit-mask slots are sized for
     unsigned long long lrec_key[2] = {0ull, 0ull};   // geometry key of the slot's recording (0: none)
     unsigned rt_scene_gen = 0;                       // cg_rt_set_scene count (part of the key)
     // cg_rt_render_frames (host output): chunks render into two device slots
@@ -975,19 +976,24 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k], &bum = c->pumask[k];
     const size_t tiles = rt_lattice_tiles(F);
     // Both slots' certificate buffers are sized together, for a full batch
-    // (kMaxFrameBatch frames; the unit masks of light sets too: 40 MB per 4K
-    // frame, 2 x 1.3 GB of the 288 GB): a call never allocates -- hipMalloc /
-    // hipFree, the latter a device-wide wait -- in front of its kernels merely
-    // because it batches more frames than the previous one or is the first on
-    // its slot.
+    // (kMaxFrameBatch frames): a call never allocates -- hipMalloc / hipFree,
+    // the latter a device-wide wait -- in front of its kernels merely because
+    // it batches more frames than the previous one or is the first on its
+    // slot.  The light sets' unit masks (40 MB per 4K frame) are the
+    // exception: they are sized for the largest batch this context has asked
+    // for so far (a one-frame or band call keeps ~40 MB per slot, not 1.3 GB),
+    // growing both slots together when a call batches more.
     const size_t nfa = std::max(nf, kMaxFrameBatch);
     for (int q = 0; q < 2; ++q) {
         CG_TRY(c, c->plat[q].ensure(nfa * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
         CG_TRY(c, c->ptc[q].ensure(nfa * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
         CG_TRY(c, c->pshade[q].ensure((size_t)std::max(F.n_tris, 1) * sizeof(RtShade)), "alloc tri shading");
         CG_TRY(c, c->psup[q].ensure(nfa * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
-        if (rt_lattice_unit_bytes(F, nf))
-            CG_TRY(c, c->pumask[q].ensure(rt_lattice_unit_bytes(F, (int)nfa)), "alloc lattice unit masks");
+    }
+    if (rt_lattice_unit_bytes(F, nf)) {
+        c->umask_frames = std::max(c->umask_frames, nf);
+        for (int q = 0; q < 2; ++q)
+            CG_TRY(c, c->pumask[q].ensure(rt_lattice_unit_bytes(F, c->umask_frames)), "alloc lattice unit masks");
     }
     RtFrameCams fc{};
     for (int f = 0; f < nf; ++f) {

@@ -82,6 +82,10 @@ uint32_t cgo_rt_pixel(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris
 void cgo_rt_draw_pixels(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
                         const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
                         int n_threads);
+/* as cgo_rt_draw_pixels; *worker_cpu_s (optional) = the workers' summed own CPU time */
+void cgo_rt_draw_pixels_timed(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                              const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
+                              int n_threads, double *worker_cpu_s);
 /* Build-defined workloads, restated from their definition in
  * include/cg_render.h: C4 area light (n x n lights, colour/(n*n)) and the C5
  * PCG32 random scene. */

@@ -15,6 +15,7 @@
 #include <float.h>
 #include <math.h>
 #include <pthread.h>
+#include <time.h>
 #include <string.h>
 
 /* ---- GLM subset (glm/detail/func_geometric.inl, func_matrix.inl) ---- */
@@ -373,30 +374,54 @@ void cgo_rt_draw(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
 typedef struct {
     const cgo_rt_params *p; const cgo_rt_tri *tris; int n_tris;
     const cgo_sphere *sph; int n_sph; const int *xy; int n; uint32_t *out; int stride, k;
+    double cpu_s;   /* this worker's own CPU time (CLOCK_THREAD_CPUTIME_ID) */
 } px_job;
+
+static double thread_cpu_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static void *px_worker(void *arg)
 {
     px_job *j = (px_job *)arg;
+    const double c0 = thread_cpu_s();
     for (int i = j->k; i < j->n; i += j->stride)
         j->out[i] = cgo_rt_pixel(j->p, j->tris, j->n_tris, j->sph, j->n_sph, j->xy[2 * i], j->xy[2 * i + 1], 0);
+    j->cpu_s = thread_cpu_s() - c0;
     return 0;
 }
 
-void cgo_rt_draw_pixels(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
-                        const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
-                        int n_threads)
+/* Pixels xy of the frame on n_threads threads; *worker_cpu_s (optional) = the
+ * sum of the workers' own CPU times (no other thread of the process counted). */
+void cgo_rt_draw_pixels_timed(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                              const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
+                              int n_threads, double *worker_cpu_s)
 {
     if (n_threads < 1) n_threads = 1;
     if (n_threads > 256) n_threads = 256;
     pthread_t th[256];
     px_job jobs[256];
     for (int k = 0; k < n_threads; ++k) {
-        jobs[k] = (px_job){p, tris, n_tris, sph, n_sph, xy, n, out, n_threads, k};
+        jobs[k] = (px_job){p, tris, n_tris, sph, n_sph, xy, n, out, n_threads, k, 0.0};
         if (k) pthread_create(&th[k], 0, px_worker, &jobs[k]);
     }
     px_worker(&jobs[0]);
     for (int k = 1; k < n_threads; ++k) pthread_join(th[k], 0);
+    if (worker_cpu_s) {
+        double t = 0.0;
+        for (int k = 0; k < n_threads; ++k) t += jobs[k].cpu_s;
+        *worker_cpu_s = t;
+    }
+}
+
+void cgo_rt_draw_pixels(const cgo_rt_params *p, const cgo_rt_tri *tris, int n_tris,
+                        const cgo_sphere *sph, int n_sph, const int *xy, int n, uint32_t *out,
+                        int n_threads)
+{
+    cgo_rt_draw_pixels_timed(p, tris, n_tris, sph, n_sph, xy, n, out, n_threads, 0);
 }
 
 /* ---- build-defined workloads ---- */

@@ -116,6 +116,8 @@ def load():
         "cgo_put_pixel": (C.c_uint32, [V3]),
         "cgo_rt_draw_pixels": (None, [C.POINTER(RtParams), C.POINTER(RtTri), C.c_int, C.POINTER(Sphere),
                                       C.c_int, P, C.c_int, P, C.c_int]),
+        "cgo_rt_draw_pixels_timed": (None, [C.POINTER(RtParams), C.POINTER(RtTri), C.c_int, C.POINTER(Sphere),
+                                            C.c_int, P, C.c_int, P, C.c_int, C.POINTER(C.c_double)]),
         "cgo_rt_area_lights": (C.c_int, [Light, C.c_float, C.c_int, C.POINTER(Light)]),
         "cgo_rt_random_scene": (C.c_int, [C.c_uint64, C.c_int, C.POINTER(RtTri)]),
         "cgo_rast_load_scene": (C.c_int, [C.POINTER(RastTri), C.POINTER(C.c_int),
@@ -211,8 +213,9 @@ def rt_random_scene(seed, n):
     return tris
 
 
-def rt_draw_pixels(p, xy, scene=None, threads=1):
-    """Pixels xy (int array (k, 2) of (u, v)) of the RT frame; scene as in rt_draw."""
+def rt_draw_pixels(p, xy, scene=None, threads=1, worker_cpu=False):
+    """Pixels xy (int array (k, 2) of (u, v)) of the RT frame; scene as in rt_draw.  With
+    worker_cpu: (pixels, the workers' summed own CPU seconds -- no other thread counted)."""
     lib = load()
     if scene is None:
         tris1, n1, sph1 = rt_scene()
@@ -220,9 +223,10 @@ def rt_draw_pixels(p, xy, scene=None, threads=1):
     tris, n_tris, sph, n_sph = scene
     xy = np.ascontiguousarray(np.asarray(xy, np.int32).reshape(-1, 2))
     out = np.zeros(len(xy), np.uint32)
-    lib.cgo_rt_draw_pixels(C.byref(p), tris, n_tris, sph, n_sph, xy.ctypes.data_as(C.c_void_p),
-                           len(xy), out.ctypes.data_as(C.c_void_p), threads)
-    return out
+    cpu = C.c_double(0.0)
+    lib.cgo_rt_draw_pixels_timed(C.byref(p), tris, n_tris, sph, n_sph, xy.ctypes.data_as(C.c_void_p),
+                                 len(xy), out.ctypes.data_as(C.c_void_p), threads, C.byref(cpu))
+    return (out, cpu.value) if worker_cpu else out
 
 
 def glibc_rand(offset, n):
