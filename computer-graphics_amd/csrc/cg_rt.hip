@@ -997,7 +997,9 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     tc += (size_t)frame * F.n_tris;
     lat_masks += (size_t)frame * lat_tiles_x(F) * gridDim.y * 2;
     const LatOut o = lat_out(F, frame, out_stride, out);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
+    // (wave as a uniform SGPR value -- readfirstlane -- measured 5 % slower here: 0.913 -> 0.960 ms
+    // per 20-frame launch, more VGPRs and SGPRs; the yawed form 0.7 % faster; profiles/r05_ab_walk.json)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int by = S.by, bx = F.tx0 + S.bx;
     LatTile G = lat_tile(F, bx, by);
     G.yaw = PITCH != kLatW;   // the launch's choice (lat_yaw), a constant here
@@ -1766,8 +1768,12 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             // frames: bands of 90-188 rows have 760-1,520 super-tiles (four waves 176-185 us per
             // band call, two 169-190), the whole frame 6,840 (one wave 77-78 us, two 88, four
             // 128; in the raster order one wave took 105-111, two 100-105).
+            // Round 5: two waves while they fit one round (2 x resident4 128-thread workgroups) -- the
+            // 1/8 bands of 9-13 tile rows (1,140-1,520 super-tile-frames) took one wave per chain
+            // before, 24-44 us of certificates for their band call.
             const size_t cnt = (size_t)units_w * nframes;
-            const int tthreads = force_threads ? force_threads : cnt <= (size_t)resident4 ? 256 : 64;
+            const int tthreads = force_threads ? force_threads
+                                 : cnt <= (size_t)resident4 ? 256 : cnt <= 2 * (size_t)resident4 ? 128 : 64;
             const int tprep = (n + tthreads - 1) / tthreads;
             KtScope kt(KT_RT_TILE_CERT, st);
             const int ff = tprep + units_w <= 65535;
