@@ -23,8 +23,10 @@ python3 -c "import json, sys; sys.path.insert(0, '$ROOT/computer-graphics_amd');
 json.dump({k: codeobj.kernel_sha256(k) for k in codeobj.kernel_names()}, open('$OUT/code_sha256.json', 'w'), indent=1)"
 WLS=${WLS:-rt rast c4 c5 c5yaw yaw f256}
 has() { case " $WLS " in *" $1 "*) return 0;; esac; return 1; }
+# every launch of a profiled kernel carries the same frames (the --stats mean is per launch)
 for w in $WLS; do
-  run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-sub
+  case $w in c4|yaw|f256) P="--steps 32 --warmup 32";; *) P="";; esac
+  run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- $B --workload $w --no-sub $P
 done
 for wl in rt rast c4 c5 c5yaw yaw f256; do
   has $wl || continue
