@@ -84,9 +84,11 @@ def test_default_line_roofline_is_the_kernels_own():
         live = r["kernel_ms_live"][kern]
         assert live["busy_ms"] / live["launches"] == pytest.approx(ro["kernel_ms"])
         assert live["busy_ms"] <= live["total_ms"] * (1 + 1e-9)
-    if rnd >= "r05":   # C5's fraction also on the committed rocprofv3 mean
-        fp = d["c5"]["roofline"]["frac_profile_mean"]
-        assert fp is not None and 0 < fp <= 1 and "kernel_stats.csv" in d["c5"]["roofline"]["frac_profile_mean_note"]
+    if rnd >= "r05":   # every fraction also on the committed rocprofv3 mean
+        for r in (d, d["c4"], d["c5"]):
+            fp = r["roofline"]["frac_profile_mean"]
+            assert fp is not None and 0 < fp <= 1 and "kernel_stats.csv" in r["roofline"]["frac_profile_mean_note"]
+        assert d["c5"]["roofline"]["frac_profile_mean"] >= 0.30   # the C5 walk
     assert d["c5"]["cpu_baseline"]["sampled_pixels"] >= 1024
     assert d["c5"]["cpu_baseline"]["threads"] >= 1 and d["c5"]["cpu_baseline"]["cores"] == 1
 
