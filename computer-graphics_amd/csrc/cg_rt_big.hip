@@ -582,28 +582,143 @@ __device__ unsigned long long bundle_mask(const RtTri &c, const float (*bb)[4], 
 // the box travels with the entry so that the bins test it before gathering
 // the triangle (every direction a super-bin ray can accept lies in it, and a
 // bin's rays are super-bin rays).
-__global__ __launch_bounds__(256) void rt_sup_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+//
+// One workgroup per (1,024-triangle chunk, group of super-bins: blockIdx.y of
+// sup_groups(), at most 64 super-bins each): each triangle's constants are
+// read once per group and its linear forms formed once for all the group's
+// bundles (bundle_mask: a cleared bit is a super-bin the
+// certificate culls over the group's enclosing bundle, hence over its own),
+// and only the surviving (super-bin, triangle) pairs -- ~2.5 per triangle at
+// C5 -- run cull_primary and the projected box.  Round 4 ran one workgroup per
+// (chunk, super-bin), re-reading the 64 MB of triangle constants and
+// re-forming them for each of C5's 36 super-bins (2.8 GB of the frame's HBM
+// traffic).  The lists are the same: a pair is kept iff cull_primary keeps
+// it and its box meets the bundle, appended in ascending triangle order, one
+// chunk per (super-bin, workgroup) as before.
+constexpr int kSupGroup = 64;
+// Super-bin groups per chunk: at least 4 (C5's 36 super-bins: 4 groups of 9), so the
+// pass has ~4 workgroups per chunk in flight rather than one long one.
+__host__ __device__ __forceinline__ int sup_groups(int nsup) { return max(4, (nsup + kSupGroup - 1) / kSupGroup); }
+#ifndef CG_SUP_WAVES
+#define CG_SUP_WAVES 3   // 168 VGPRs; 2 waves (182) 562 us, 4 waves (136 B scratch) 468, 3: 452 (C5, one frame; r05)
+#endif
+__global__ __launch_bounds__(256, CG_SUP_WAVES) void rt_sup_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                              const cg_tri *__restrict__ tris, BigBufs B)
 {
-    const int sup = blockIdx.y;
-    float x0, x1, y0, y1;
-    const bool ok = sup_bundle(F, sup % B.sups_x, sup / B.sups_x, x0, x1, y0, y1);
-    const int base = blockIdx.x * kBinTris;
-    bool kept[4];
-    unsigned long long pb[4];
+    __shared__ float s_sb[kSupGroup][4];         // the group's super-bin bundles (x0 > x1: no pixel)
+    __shared__ int s_cnt[kSupGroup][4][4];       // kept per (super-bin, triangle slot r, wave)
+    __shared__ int s_base[kSupGroup];            // the chunk's pool offset per super-bin (-1: overflow)
+    const int nsup = B.sups_x * B.sups_y, base = blockIdx.x * kBinTris;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int gsz = (nsup + (int)gridDim.y - 1) / (int)gridDim.y;   // <= kSupGroup
+    {
+        const int g0 = (int)blockIdx.y * gsz;
+        const int ng = min(gsz, nsup - g0);
+        if (ng <= 0) return;
+        if ((int)threadIdx.x < ng) {
+            const int sup = g0 + (int)threadIdx.x;
+            float *q = s_sb[threadIdx.x];
+            if (!sup_bundle(F, sup % B.sups_x, sup / B.sups_x, q[0], q[1], q[2], q[3])) {
+                q[0] = 1.0f;
+                q[1] = 0.0f;
+                q[2] = q[3] = 0.0f;
+            }
+        }
+        __syncthreads();
+        float ex0 = FLT_MAX, ex1 = -FLT_MAX, ey0 = FLT_MAX, ey1 = -FLT_MAX;   // the enclosing bundle
+        unsigned long long valid = 0ull;   // the group's super-bins with pixels
+        for (int k = 0; k < ng; ++k)
+            if (!(s_sb[k][0] > s_sb[k][1])) {
+                valid |= 1ull << k;
+                ex0 = fminf(ex0, s_sb[k][0]);
+                ex1 = fmaxf(ex1, s_sb[k][1]);
+                ey0 = fminf(ey0, s_sb[k][2]);
+                ey1 = fmaxf(ey1, s_sb[k][3]);
+            }
+        // kept[r] bit k: triangle base + r * 256 + tid for super-bin g0 + k; the boxes of
+        // each triangle's first two kept super-bins are kept for the write pass
+        unsigned long long km[4], pbc[4][2];
+        int kc[4][2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = base + r * 256 + (int)threadIdx.x;
-        PrimDet pd;
-        kept[r] = ok && i < F.n_tris && !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
-        pb[r] = kProjAll;
-        if (kept[r]) {
-            pb[r] = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
-            kept[r] = proj_meets(pb[r], x0, x1, y0, y1);
+        for (int r = 0; r < 4; ++r) {
+            kc[r][0] = kc[r][1] = -1;
+            pbc[r][0] = pbc[r][1] = kProjAll;
+            const int i = base + r * 256 + (int)threadIdx.x;
+            // (bundle_mask answers ~0 when its error terms are not finite: every valid bundle is tested)
+            unsigned long long m = (i < F.n_tris && valid)
+                                       ? bundle_mask(tc[i], s_sb, ng, ex0, ex1, ey0, ey1, F.focal) & valid : 0ull;
+            unsigned long long kept = 0ull;
+            while (m) {
+                const int k = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const float x0 = s_sb[k][0], x1 = s_sb[k][1], y0 = s_sb[k][2], y1 = s_sb[k][3];
+                PrimDet pd;
+                if (!cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd)) {
+                    const unsigned long long pb = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                    if (proj_meets(pb, x0, x1, y0, y1)) {
+                        if (kc[r][0] < 0) {
+                            kc[r][0] = k;
+                            pbc[r][0] = pb;
+                        } else if (kc[r][1] < 0) {
+                            kc[r][1] = k;
+                            pbc[r][1] = pb;
+                        }
+                        kept |= 1ull << k;
+                    }
+                }
+            }
+            km[r] = kept;
+        }
+        // counts per (super-bin, r, wave), then one pool reservation per super-bin
+        for (int k = 0; k < ng; ++k)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const unsigned long long b = __ballot((km[r] >> k) & 1ull);
+                if (lane == 0) s_cnt[k][r][w] = __popcll(b);
+            }
+        __syncthreads();
+        if ((int)threadIdx.x < ng) {
+            const int k = (int)threadIdx.x, sup = g0 + k;
+            int tot = 0;
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q) tot += s_cnt[k][r][q];
+            const int g = pool_reserve(B.pool_n + kPoolSup, B.cap_sup, tot, B.sup_over + sup);
+            B.sup_chunk[(size_t)sup * B.nch + blockIdx.x] = Chunk{g < 0 ? 0 : g, g < 0 ? 0 : tot};
+            s_base[k] = g;
+        }
+        __syncthreads();
+        // the entries, in ascending triangle order within each chunk (pooled_append's)
+        for (int k = 0; k < ng; ++k) {
+            if (s_base[k] < 0) continue;   // overflowed: the list is redone at a larger capacity
+            int off = s_base[k];
+            const float x0 = s_sb[k][0], x1 = s_sb[k][1], y0 = s_sb[k][2], y1 = s_sb[k][3];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool kr = (km[r] >> k) & 1ull;
+                const unsigned long long b = __ballot(kr);
+                int before = 0;
+                for (int q = 0; q < 4; ++q) before += q < w ? s_cnt[k][r][q] : 0;
+                if (kr) {
+                    const int i = base + r * 256 + (int)threadIdx.x;
+                    unsigned long long pb;
+                    if (kc[r][0] == k) {
+                        pb = pbc[r][0];
+                    } else if (kc[r][1] == k) {
+                        pb = pbc[r][1];
+                    } else {   // a third or later kept super-bin: the same box again
+                        PrimDet pd;
+                        (void)cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
+                        pb = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                    }
+                    const int at = off + before + __popcll(b & lt);
+                    B.sup_pool[at] = i;
+                    B.sup_pbox_pool[at] = pb;
+                }
+                for (int q = 0; q < 4; ++q) off += s_cnt[k][r][q];
+            }
         }
     }
-    pooled_append(kept, base, B.sup_pool, B.pool_n + kPoolSup, B.cap_sup, B.sup_chunk + (size_t)sup * B.nch + blockIdx.x,
-                  B.sup_over + sup, pb, B.sup_pbox_pool);
 }
 
 // The super lists' chunks copied into one contiguous array per super-bin.
@@ -2263,8 +2378,8 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const bool flags_fit = lat || 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
-    hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, B.sups_x * B.sups_y), dim3(256), 0, st, F, d_tc, d_tris,
-                       B);
+    hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, sup_groups(B.sups_x * B.sups_y)), dim3(256), 0, st, F,
+                       d_tc, d_tris, B);
     const int sups = B.sups_x * B.sups_y;
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(sups), dim3(1024), 0, st, B.sup_chunk, nullptr, B.nch, B.sup_pre,
                        B.sup_tot);
