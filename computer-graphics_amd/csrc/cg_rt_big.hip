@@ -1780,7 +1780,7 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
 #ifndef CG_HINT_WAVES
-#define CG_HINT_WAVES 5   // 12-16 B of scratch (one value per slot); 6: 68-76 B, same speed (r05)
+#define CG_HINT_WAVES 4   // 99-101 VGPRs, no scratch; 5: 12-16 B, 6: 68-76 B -- all the same speed (r05_ab_walk.json)
 #endif
 template <int LM>
 __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
