@@ -723,14 +723,15 @@ __global__ __launch_bounds__(256, CG_SUP_WAVES) void rt_sup_primary_kernel(RtFra
 
 // The super lists' chunks copied into one contiguous array per super-bin.
 // (An entry without a box gets its bin mask here, in a dense pass.)
+constexpr int kCompactPre = 4096;   // chunk prefixes staged in LDS (lists of up to 4M triangles)
 __global__ __launch_bounds__(256, 6) void rt_sup_compact_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
-    const int sup = blockIdx.y, c = blockIdx.x;
+    const int sup = blockIdx.y;
     if (B.sup_over[sup]) return;
-    const Chunk ch = B.sup_chunk[(size_t)sup * B.nch + c];
-    if (ch.n == 0) return;
-    const size_t at = (size_t)B.sup_base[sup] + B.sup_pre[(size_t)sup * B.nch + c];
+    const int tot = B.sup_tot[sup];
+    if ((int)blockIdx.x * 256 >= tot) return;
     __shared__ float s_bb[kSupBins * kSupBins][4];   // the super-bin's bins' bundles
+    __shared__ int s_pre[kCompactPre];
     const int sx = sup % B.sups_x, sy = sup / B.sups_x;
     float ex0, ex1, ey0, ey1;
     const bool sv = sup_bundle(F, sx, sy, ex0, ex1, ey0, ey1);
@@ -742,16 +743,33 @@ __global__ __launch_bounds__(256, 6) void rt_sup_compact_kernel(RtFrame F, const
             q[1] = 0.0f;
         }
     }
+    const int nch = B.nch;
+    const int *pre = B.sup_pre + (size_t)sup * nch;
+    const bool lds = nch <= kCompactPre;
+    if (lds)
+        for (int c = (int)threadIdx.x; c < nch; c += 256) s_pre[c] = pre[c];
     __syncthreads();
-    for (int e = (int)threadIdx.x; e < ch.n; e += 256) {
+    const Chunk *tab = B.sup_chunk + (size_t)sup * nch;
+    const size_t at = (size_t)B.sup_base[sup];
+    // the list's entries in flat order, strided over the super-bin's workgroups: entry j lies in
+    // the last chunk c with pre[c] <= j (an empty chunk shares its successor's prefix)
+    for (int j = (int)(blockIdx.x * 256 + threadIdx.x); j < tot; j += (int)gridDim.x * 256) {
+        int lo = 0, hi = nch - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((lds ? s_pre[mid] : pre[mid]) <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const Chunk ch = tab[lo];
+        const int e = j - (lds ? s_pre[lo] : pre[lo]);
         const int i = B.sup_pool[ch.off + e];
         unsigned long long pb = B.sup_pbox_pool[ch.off + e];
         if (pb == kProjAll && sv) {
             const unsigned long long m = bundle_mask(tc[i], s_bb, kSupBins * kSupBins, ex0, ex1, ey0, ey1, F.focal);
             pb = m ? (m << 32) | kMaskTag : kProjNone;
         }
-        B.sup_flat[at + e] = i;
-        B.sup_flat_pbox[at + e] = pb;
+        B.sup_flat[at + j] = i;
+        B.sup_flat_pbox[at + j] = pb;
     }
 }
 
@@ -2384,13 +2402,38 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(sups), dim3(1024), 0, st, B.sup_chunk, nullptr, B.nch, B.sup_pre,
                        B.sup_tot);
     hipLaunchKernelGGL(rt_list_base_kernel, dim3(1), dim3(1024), 0, st, B.sup_tot, sups, B.sup_base);
-    hipLaunchKernelGGL(rt_sup_compact_kernel, dim3(B.nch, sups), dim3(256), 0, st, F, d_tc, B);
-    hipLaunchKernelGGL(rt_bin_primary_kernel, dim3(std::min(64, (int)bgrid.x), bins), dim3(256), 0, st, F, d_tc,
+    // the compaction strides over each super list's flat entries with 128 workgroups per
+    // super-bin (one per chunk left most lanes idle: ~70 entries per chunk at C5): C5 one frame
+    // 320 -> 173 us (32: 386, 512: 203); CG_CMP_WGS: A/B runs
+    static const int cmp_wgs = [] {
+        const char *e = std::getenv("CG_CMP_WGS");
+        const int v = e ? std::atoi(e) : 128;
+        return v > 0 ? v : 128;
+    }();
+    hipLaunchKernelGGL(rt_sup_compact_kernel, dim3(std::min(cmp_wgs, (F.n_tris + 255) / 256), sups), dim3(256), 0, st,
+                       F, d_tc, B);
+    // workgroups per bin striding over its super list: fewer, longer workgroups fill the
+    // certificate batches (1,024 entries per batch; C5's ~70k-entry super lists give each of 64
+    // workgroups one ~110-entry batch) -- C5 bin pass 379 -> 272 us at 16, 266 at 8, 314 at 4;
+    // C5 178 -> 181-182 fps (profiles/r05_ab_bins.json).  CG_BIN_WGS: A/B runs.
+    static const int bin_wgs = [] {
+        const char *e = std::getenv("CG_BIN_WGS");
+        const int v = e ? std::atoi(e) : 16;
+        return v > 0 ? v : 16;
+    }();
+    hipLaunchKernelGGL(rt_bin_primary_kernel, dim3(std::min(bin_wgs, (int)bgrid.x), bins), dim3(256), 0, st, F, d_tc,
                        d_tris, B);
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(bins), dim3(1024), 0, st, B.bin_chunk, B.bin_nch, B.nch, B.bin_pre,
                        B.bin_tot);
     hipLaunchKernelGGL(rt_list_base_kernel, dim3(1), dim3(1024), 0, st, B.bin_tot, bins, B.bin_base);
-    const dim3 egrid(std::min(64, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
+    // workgroups per bin for the bucket count and scatter passes over a bin's list: C5 count
+    // 241 -> 165 us at 16, 166 at 8; scatter 106 -> 63 / 49 us; CG_CNT_WGS: A/B runs
+    static const int cnt_wgs = [] {
+        const char *e = std::getenv("CG_CNT_WGS");
+        const int v = e ? std::atoi(e) : 8;
+        return v > 0 ? v : 8;
+    }();
+    const dim3 egrid(std::min(cnt_wgs, (F.n_tris + 1023) / 1024), bins);   // workgroups stride over a bin's list
     hipLaunchKernelGGL(rt_bin_count_kernel, egrid, dim3(256), 0, st, F, d_tc, d_tris, B);
     hipLaunchKernelGGL(rt_bin_scan_kernel, dim3(1), dim3(1024), 0, st, B, 2 * bins);
     // sizing passes (cg_shim.hip) stop early and report the demand: dry 1
