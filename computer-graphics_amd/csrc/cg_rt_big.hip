@@ -1176,23 +1176,53 @@ __global__ __launch_bounds__(64) void rt_half_tiles_kernel(RtFrame F, BigBufs B)
     *(float4 *)q = make_float4(x0, x1, y0, y1);
 }
 
+// The entries needing a mask are a minority scattered through the sorted pool: each
+// workgroup queues them in LDS (ballot compaction) and certifies them 256 at a time, one per
+// lane, instead of leaving most lanes of each grid-stride step idle beside bundle_mask.
+__device__ __forceinline__ void half_mask_one(const RtFrame &F, const RtTri *__restrict__ tc, const BigBufs &B,
+                                              long long p)
+{
+    const unsigned long long pb = B.bin_spbox[p];
+    // (entries of an overflowed bin may be another frame's: never walked, skipped here)
+    const int sub = (int)(pb >> 32), bin = sub >> 1;
+    if (sub < 0 || sub >= 2 * B.bins_x * B.bins_y || B.bin_over[bin]) return;
+    float hx0, hx1, hy0, hy1;
+    if (!bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, sub & 1, hx0, hx1, hy0, hy1)) return;
+    const int i = (int)(unsigned)(B.bin_sorted[p] & 0xffffffffull);
+    if (i < 0 || i >= F.n_tris) return;
+    const unsigned long long mk = bundle_mask(tc[i], (const float(*)[4])(B.tile_bb + (size_t)sub * 128), 32, hx0,
+                                              hx1, hy0, hy1, F.focal);
+    B.bin_spbox[p] = mk ? (mk << 32) | kMaskTag : kProjNone;
+}
 __global__ __launch_bounds__(256) void rt_half_mask_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
     const long long total = (long long)min((unsigned long long)B.pool_n[kPoolSorted], (unsigned long long)B.cap_sorted);
-    for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < total; p += (long long)gridDim.x * 256) {
-        const unsigned long long pb = B.bin_spbox[p];
-        if ((unsigned)pb != kNeedTag) continue;
-        // (entries of an overflowed bin may be another frame's: never walked, skipped here)
-        const int sub = (int)(pb >> 32), bin = sub >> 1;
-        if (sub < 0 || sub >= 2 * B.bins_x * B.bins_y || B.bin_over[bin]) continue;
-        float hx0, hx1, hy0, hy1;
-        if (!bin_half_bundle(F, bin % B.bins_x, bin / B.bins_x, sub & 1, hx0, hx1, hy0, hy1)) continue;
-        const int i = (int)(unsigned)(B.bin_sorted[p] & 0xffffffffull);
-        if (i < 0 || i >= F.n_tris) continue;
-        const unsigned long long mk = bundle_mask(tc[i], (const float(*)[4])(B.tile_bb + (size_t)sub * 128), 32, hx0,
-                                                  hx1, hy0, hy1, F.focal);
-        B.bin_spbox[p] = mk ? (mk << 32) | kMaskTag : kProjNone;
+    __shared__ long long s_q[512];
+    __shared__ int s_w[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int qn = 0;   // queued (workgroup-uniform)
+    for (long long b0 = (long long)blockIdx.x * 256; b0 < total; b0 += (long long)gridDim.x * 256) {
+        const long long p = b0 + threadIdx.x;
+        const bool need = p < total && (unsigned)B.bin_spbox[p] == kNeedTag;
+        const unsigned long long m = __ballot(need);
+        if (lane == 0) s_w[w] = __popcll(m);
+        __syncthreads();
+        int before = qn;
+        for (int q = 0; q < w; ++q) before += s_w[q];
+        if (need) s_q[before + __popcll(m & lt)] = p;
+        qn += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+        if (qn >= 256) {
+            half_mask_one(F, tc, B, s_q[threadIdx.x]);
+            const long long mv = (int)threadIdx.x + 256 < qn ? s_q[threadIdx.x + 256] : 0;
+            __syncthreads();
+            if ((int)threadIdx.x + 256 < qn) s_q[threadIdx.x] = mv;
+            qn -= 256;
+            __syncthreads();
+        }
     }
+    if ((int)threadIdx.x < qn) half_mask_one(F, tc, B, s_q[threadIdx.x]);
 }
 
 // Ray slots of one wave tile (K1, K4 and the shading kernel read them):
@@ -2447,7 +2477,12 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     if (dry == 1) return demand();
     hipLaunchKernelGGL(rt_half_tiles_kernel, dim3(2 * bins), dim3(64), 0, st, F, B);
     hipLaunchKernelGGL(rt_bin_scatter_kernel, egrid, dim3(256), 0, st, F, B);
-    hipLaunchKernelGGL(rt_half_mask_kernel, dim3(2048), dim3(256), 0, st, F, d_tc, B);
+    static const int hm_wgs = [] {   // A/B: CG_HM_WGS
+        const char *e = std::getenv("CG_HM_WGS");
+        const int v = e ? std::atoi(e) : 2048;
+        return v > 0 ? v : 2048;
+    }();
+    hipLaunchKernelGGL(rt_half_mask_kernel, dim3(hm_wgs), dim3(256), 0, st, F, d_tc, B);
     {
         const char *wo = std::getenv("CG_WALK_ORDER");
         if (wo && wo[0] == '0') B.walk_order = nullptr;
@@ -2477,7 +2512,12 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
             else
                 hipLaunchKernelGGL(rt_shadow_hints_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         }
-        hipLaunchKernelGGL(rt_pending_lit_kernel, dim3(1024), dim3(256), 0, st, F, d_tc, B);
+        static const int pl_wgs = [] {   // A/B: CG_PL_WGS
+            const char *e = std::getenv("CG_PL_WGS");
+            const int v = e ? std::atoi(e) : 1024;
+            return v > 0 ? v : 1024;
+        }();
+        hipLaunchKernelGGL(rt_pending_lit_kernel, dim3(pl_wgs), dim3(256), 0, st, F, d_tc, B);
     }
     if (lat && B.lat_yaw)
         hipLaunchKernelGGL(rt_big_shade_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B, d_out);
