@@ -753,24 +753,61 @@ __global__ __launch_bounds__(256, 6) void rt_sup_compact_kernel(RtFrame F, const
     const size_t at = (size_t)B.sup_base[sup];
     // the list's entries in flat order, strided over the super-bin's workgroups: entry j lies in
     // the last chunk c with pre[c] <= j (an empty chunk shares its successor's prefix)
-    for (int j = (int)(blockIdx.x * 256 + threadIdx.x); j < tot; j += (int)gridDim.x * 256) {
-        int lo = 0, hi = nch - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((lds ? s_pre[mid] : pre[mid]) <= j) lo = mid;
-            else hi = mid - 1;
+    // (entries without a box -- a minority -- are queued in LDS and given their bin masks 256 at
+    // a time, so bundle_mask runs on full waves)
+    __shared__ int s_qi[512], s_qj[512];
+    __shared__ int s_w[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int qn = 0;   // queued (workgroup-uniform)
+    auto masked = [&](int i, int j) {
+        const unsigned long long m = bundle_mask(tc[i], s_bb, kSupBins * kSupBins, ex0, ex1, ey0, ey1, F.focal);
+        B.sup_flat_pbox[at + j] = m ? (m << 32) | kMaskTag : kProjNone;
+    };
+    for (int j0 = (int)blockIdx.x * 256; j0 < tot; j0 += (int)gridDim.x * 256) {   // workgroup-uniform bounds
+        const int j = j0 + (int)threadIdx.x;
+        bool need = false;
+        int i = 0;
+        if (j < tot) {
+            int lo = 0, hi = nch - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if ((lds ? s_pre[mid] : pre[mid]) <= j) lo = mid;
+                else hi = mid - 1;
+            }
+            const Chunk ch = tab[lo];
+            const int e = j - (lds ? s_pre[lo] : pre[lo]);
+            i = B.sup_pool[ch.off + e];
+            const unsigned long long pb = B.sup_pbox_pool[ch.off + e];
+            B.sup_flat[at + j] = i;
+            need = pb == kProjAll && sv;
+            if (!need) B.sup_flat_pbox[at + j] = pb;
         }
-        const Chunk ch = tab[lo];
-        const int e = j - (lds ? s_pre[lo] : pre[lo]);
-        const int i = B.sup_pool[ch.off + e];
-        unsigned long long pb = B.sup_pbox_pool[ch.off + e];
-        if (pb == kProjAll && sv) {
-            const unsigned long long m = bundle_mask(tc[i], s_bb, kSupBins * kSupBins, ex0, ex1, ey0, ey1, F.focal);
-            pb = m ? (m << 32) | kMaskTag : kProjNone;
+        const unsigned long long m = __ballot(need);
+        if (lane == 0) s_w[w] = __popcll(m);
+        __syncthreads();
+        int before = qn;
+        for (int q = 0; q < w; ++q) before += s_w[q];
+        if (need) {
+            s_qi[before + __popcll(m & lt)] = i;
+            s_qj[before + __popcll(m & lt)] = j;
         }
-        B.sup_flat[at + j] = i;
-        B.sup_flat_pbox[at + j] = pb;
+        qn += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+        if (qn >= 256) {
+            masked(s_qi[threadIdx.x], s_qj[threadIdx.x]);
+            const bool mv = (int)threadIdx.x + 256 < qn;
+            const int mi = mv ? s_qi[threadIdx.x + 256] : 0, mj = mv ? s_qj[threadIdx.x + 256] : 0;
+            __syncthreads();
+            if (mv) {
+                s_qi[threadIdx.x] = mi;
+                s_qj[threadIdx.x] = mj;
+            }
+            qn -= 256;
+            __syncthreads();
+        }
     }
+    if ((int)threadIdx.x < qn) masked(s_qi[threadIdx.x], s_qj[threadIdx.x]);
 }
 
 // K0: camera-ray certificate per (bin, triangle of its super list), with the
@@ -999,37 +1036,73 @@ __global__ __launch_bounds__(256, 4) void rt_bin_count_kernel(RtFrame F, const R
         (&s_min[0][0])[threadIdx.x] = 0u;
     }
     __syncthreads();
-    // chunk by chunk, each entry also copied to its place in the compacted list
+    // chunk by chunk, each entry also copied to its place in the compacted list; the box-less
+    // entries (a minority, each two certificates) are queued in LDS and certified 256 at a time
+    __shared__ unsigned long long s_qa[512], s_qd[512];   // (source, destination) of queued entries
+    __shared__ int s_w[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int qn = 0;   // queued (workgroup-uniform)
+    auto finish = [&](size_t at, size_t d, bool boxless) {
+        const unsigned long long ent = B.bin_ent[at];
+        unsigned long long pb[2];
+        pb[0] = B.bin_pbox[at];
+        pb[1] = B.bin_pbox2[at];
+        if (boxless) {
+            const int i = (int)(unsigned)(ent & 0xffffffffull);
+            for (int h = 0; h < 2; ++h) {
+                PrimDet ph;
+                pb[h] = kProjNone;
+                if (hv[h] && !cull_primary(tc[i], hx0[h], hx1[h], hy0[h], hy1[h], F.focal, &ph))
+                    pb[h] = proj_box16(tc[i], ph, tris[i], F.cam, F.focal);
+            }
+        }
+        B.flat_ent[d] = ent;
+        B.flat_pbox[d] = pb[0];
+        B.flat_pbox2[d] = pb[1];
+        const unsigned kb = (unsigned)(ent >> 32);
+        const int b = depth_bucket(kb, B, bin);
+        for (int h = 0; h < 2; ++h)
+            if (hv[h] && proj_meets(pb[h], hx0[h], hx1[h], hy0[h], hy1[h])) {
+                atomicAdd(&s_cnt[h][b], 1);
+                atomicMax(&s_min[h][b], ~kb);
+            }
+    };
     for (int c = blockIdx.x; c < nc; c += gridDim.x) {
         const Chunk ch = tab[c];
         const size_t dst = base + pre[c];
-        for (int e = (int)threadIdx.x; e < ch.n; e += 256) {
+        for (int e0 = 0; e0 < ch.n; e0 += 256) {   // workgroup-uniform bounds
+            const int e = e0 + (int)threadIdx.x;
             const size_t at = (size_t)ch.off + e;
-            const unsigned long long ent = B.bin_ent[at];
-            unsigned long long pb[2];
-            pb[0] = B.bin_pbox[at];
-            pb[1] = B.bin_pbox2[at];
-            if (pb[0] == kProjAll) {
-                const int i = (int)(unsigned)(ent & 0xffffffffull);
-                for (int h = 0; h < 2; ++h) {
-                    PrimDet ph;
-                    pb[h] = kProjNone;
-                    if (hv[h] && !cull_primary(tc[i], hx0[h], hx1[h], hy0[h], hy1[h], F.focal, &ph))
-                        pb[h] = proj_box16(tc[i], ph, tris[i], F.cam, F.focal);
-                }
+            const bool in = e < ch.n;
+            const bool boxless = in && B.bin_pbox[at] == kProjAll;
+            if (in && !boxless) finish(at, dst + e, false);
+            const unsigned long long m = __ballot(boxless);
+            if (lane == 0) s_w[w] = __popcll(m);
+            __syncthreads();
+            int before = qn;
+            for (int q = 0; q < w; ++q) before += s_w[q];
+            if (boxless) {
+                s_qa[before + __popcll(m & lt)] = at;
+                s_qd[before + __popcll(m & lt)] = dst + e;
             }
-            B.flat_ent[dst + e] = ent;
-            B.flat_pbox[dst + e] = pb[0];
-            B.flat_pbox2[dst + e] = pb[1];
-            const unsigned kb = (unsigned)(ent >> 32);
-            const int b = depth_bucket(kb, B, bin);
-            for (int h = 0; h < 2; ++h)
-                if (hv[h] && proj_meets(pb[h], hx0[h], hx1[h], hy0[h], hy1[h])) {
-                    atomicAdd(&s_cnt[h][b], 1);
-                    atomicMax(&s_min[h][b], ~kb);
+            qn += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+            __syncthreads();
+            if (qn >= 256) {
+                finish(s_qa[threadIdx.x], s_qd[threadIdx.x], true);
+                const bool mv = (int)threadIdx.x + 256 < qn;
+                const unsigned long long ma = mv ? s_qa[threadIdx.x + 256] : 0ull, md = mv ? s_qd[threadIdx.x + 256] : 0ull;
+                __syncthreads();
+                if (mv) {
+                    s_qa[threadIdx.x] = ma;
+                    s_qd[threadIdx.x] = md;
                 }
+                qn -= 256;
+                __syncthreads();
+            }
         }
     }
+    if ((int)threadIdx.x < qn) finish(s_qa[threadIdx.x], s_qd[threadIdx.x], true);
     __syncthreads();
     if (threadIdx.x < 2 * kDepthBuckets && (&s_cnt[0][0])[threadIdx.x]) {   // [h][b] -> sub 2 bin + h
         atomicAdd(&B.bkt_cnt[2 * bin * kDepthBuckets + threadIdx.x], (&s_cnt[0][0])[threadIdx.x]);
