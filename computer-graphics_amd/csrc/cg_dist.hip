@@ -156,7 +156,17 @@ int default_timeout_ms()
     return v > 0 && v < (1L << 30) ? (int)v : 60000;
 }
 
-void poll_pause() { std::this_thread::sleep_for(std::chrono::microseconds(20)); }
+// Pause between two polls of a bounded wait that began at `since`: the first 5 ms only yield
+// (a wait at the end of a call is timed by its caller -- bench.py's N > 1 loop ends on
+// cg_dist_wait -- and a 20 us sleep rounds up to the kernel's timer slack, ~50-60 us), then
+// sleep 20 us per poll.
+void poll_pause(Clock::time_point since = Clock::time_point::min())
+{
+    if (since != Clock::time_point::min() && Clock::now() - since < std::chrono::milliseconds(5))
+        std::this_thread::yield();
+    else
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
 
 // ncclCommAbort on a helper thread, joined for at most 10 s: an abort that
 // itself stalls (a peer's socket never answering) must not turn the error
@@ -184,7 +194,7 @@ void abort_comm(cg_dist *d)
 int nccl_settle(cg_dist *d, ncclResult_t r, const char *what)
 {
     if (r == ncclInProgress && d->comm) {
-        const auto end = Clock::now() + std::chrono::milliseconds(d->timeout_ms);
+        const auto t0 = Clock::now(), end = t0 + std::chrono::milliseconds(d->timeout_ms);
         for (;;) {
             ncclResult_t st = ncclSuccess;
             const ncclResult_t q = ncclCommGetAsyncError(d->comm, &st);
@@ -195,7 +205,7 @@ int nccl_settle(cg_dist *d, ncclResult_t r, const char *what)
                 return fail(d, CG_E_TIMEOUT, std::string(what) + ": no progress within " + std::to_string(d->timeout_ms) +
                                                  " ms (a peer missing?); communicator aborted");
             }
-            poll_pause();
+            poll_pause(t0);
         }
     }
     if (r == ncclSuccess) return CG_OK;
@@ -213,7 +223,7 @@ int nccl_settle(cg_dist *d, ncclResult_t r, const char *what)
 // the communicator's asynchronous error meanwhile.
 int wait_events(cg_dist *d, const hipEvent_t *ev, int n, const char *what)
 {
-    const auto end = Clock::now() + std::chrono::milliseconds(d->timeout_ms);
+    const auto t0 = Clock::now(), end = t0 + std::chrono::milliseconds(d->timeout_ms);
     for (int i = 0; i < n;) {
         if (!ev[i]) {
             ++i;
@@ -239,7 +249,7 @@ int wait_events(cg_dist *d, const hipEvent_t *ev, int n, const char *what)
             return fail(d, CG_E_TIMEOUT, std::string(what) + ": not done within " + std::to_string(d->timeout_ms) +
                                              " ms; communicator aborted");
         }
-        poll_pause();
+        poll_pause(t0);
     }
     return CG_OK;
 }
