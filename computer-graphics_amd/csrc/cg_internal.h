@@ -1,6 +1,7 @@
 // cg_internal.h -- device-side data layouts shared by the shim and kernels.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -173,5 +174,26 @@ class KtScope {
     hipStream_t st_;
     hipEvent_t a_ = nullptr;
 };
+
+// One timed launch while timing is on: the start / stop events ride on the
+// kernel's own dispatch (hipExtLaunchKernel), so no marker packets sit between
+// the launches; a and b are null (a plain launch) while timing is off.
+class KtLaunch {
+  public:
+    KtLaunch(int id, hipStream_t st);
+    ~KtLaunch();
+    KtLaunch(const KtLaunch &) = delete;
+    KtLaunch &operator=(const KtLaunch &) = delete;
+    hipEvent_t a = nullptr, b = nullptr;
+
+  private:
+    int id_;
+};
+template <class K, class... A>
+inline void kt_launch(int id, K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, A... args)
+{
+    KtLaunch t(id, st);
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, st, t.a, t.b, 0u, args...);
+}
 
 }  // namespace cg

@@ -142,6 +142,39 @@ KtScope::~KtScope()
     if (s.pending.size() >= 2048) s.settle_completed();
 }
 
+KtLaunch::KtLaunch(int id, hipStream_t st) : id_(id)
+{
+    KtState &s = kt();
+    if (!s.on_fast.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> g(s.mu);
+    if (!s.on || id < 0 || id >= KT_COUNT) return;
+    if (!s.ref_set) {   // one recorded event anchors the busy-time spans
+        if (!s.ref && hipEventCreate(&s.ref) != hipSuccess) s.ref = nullptr;
+        s.ref_set = s.ref && hipEventRecord(s.ref, st) == hipSuccess;
+    }
+    a = s.get();
+    b = s.get();
+    if (!a || !b) {
+        if (a) s.pool.push_back(a);
+        if (b) s.pool.push_back(b);
+        a = b = nullptr;
+    }
+}
+
+KtLaunch::~KtLaunch()
+{
+    if (!a) return;
+    KtState &s = kt();
+    std::lock_guard<std::mutex> g(s.mu);
+    if (!s.on) {
+        s.pool.push_back(a);
+        s.pool.push_back(b);
+        return;
+    }
+    s.pending.push_back({id_, a, b});
+    if (s.pending.size() >= 2048) s.settle_completed();
+}
+
 }  // namespace cg
 
 using namespace cg;

@@ -914,20 +914,20 @@ static int rast_pipeline(cg_ctx *c, cg_rtri *d_tris, int n, int *n_dev, const cg
     } else {
         const int fgrid = xcd_grid(H, ((W + kFillPx - 1) / kFillPx * kXcdRows + 3) / 4);
         {
-            KtScope kt(KT_RAST_FILL, st);
+            const int kt_id = KT_RAST_FILL;
             if (A.textured)
-                hipLaunchKernelGGL(rast_fill_kernel<true>, dim3(fgrid), dim3(256), 0, st, A, recs, count,
+                kt_launch(kt_id, rast_fill_kernel<true>, dim3(fgrid), dim3(256), 0, st, A, recs, count,
                                    (uint32_t *)state, d_depth, d_shadow);
             else
-                hipLaunchKernelGGL(rast_fill_kernel<false>, dim3(fgrid), dim3(256), 0, st, A, recs, count,
+                kt_launch(kt_id, rast_fill_kernel<false>, dim3(fgrid), dim3(256), 0, st, A, recs, count,
                                    (uint32_t *)state, d_depth, d_shadow);
         }
-        KtScope kt(KT_RAST_POST, st);
+        const int kt_id = KT_RAST_POST;
         if (A.textured)
-            hipLaunchKernelGGL((rast_post_kernel<false, true>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
+            kt_launch(kt_id, (rast_post_kernel<false, true>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
                                (const void *)state, (const RowRec *)recs, (const int32_t *)nullptr, d_argb);
         else
-            hipLaunchKernelGGL((rast_post_kernel<false, false>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
+            kt_launch(kt_id, (rast_post_kernel<false, false>), dim3(post_grid), dim3(256), 0, st, d_tris, A,
                                (const void *)state, (const RowRec *)recs, (const int32_t *)nullptr, d_argb);
         if (stats) stats->n_shaded = -1;
     }

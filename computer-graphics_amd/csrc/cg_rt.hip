@@ -1775,10 +1775,10 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             const int tthreads = force_threads ? force_threads
                                  : cnt <= (size_t)resident4 ? 256 : cnt <= 2 * (size_t)resident4 ? 128 : 64;
             const int tprep = (n + tthreads - 1) / tthreads;
-            KtScope kt(KT_RT_TILE_CERT, st);
+            const int kt_id = KT_RT_TILE_CERT;
             const int ff = tprep + units_w <= 65535;
             const dim3 cg = ff ? dim3(nframes, tprep + units_w) : dim3(tprep + units_w, nframes);
-            hipLaunchKernelGGL(rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, n, cams, Fl, d_sph,
+            kt_launch(kt_id, rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, n, cams, Fl, d_sph,
                                (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep, ff,
                                Z ? *Z : LatFlatten{});
             if (Z) Z->n = -Z->n;   // done (the caller's flag: the lattice launch may use the order)
@@ -1789,15 +1789,15 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         const int tpw = n <= 31 ? 2 : 1;   // units per wave (rt_prepare_kernel)
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
         {
-            KtScope kt(KT_RT_PREPARE, st);
-            hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
+            const int kt_id = KT_RT_PREPARE;
+            kt_launch(kt_id, rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
                                d_tc, d_shade, prep, Fl, d_sph, d_sup_masks, 1);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        KtScope kt(KT_RT_TILE_CERT, st);
+        const int kt_id = KT_RT_TILE_CERT;
         const int ff = units <= 65535;
-        hipLaunchKernelGGL(rt_tile_cert_kernel, ff ? dim3(nframes, units) : dim3(units, nframes), dim3(tthreads), 0, st,
+        kt_launch(kt_id, rt_tile_cert_kernel, ff ? dim3(nframes, units) : dim3(units, nframes), dim3(tthreads), 0, st,
                            d_tris, n, cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks,
                            (RtTri *)nullptr, (RtShade *)nullptr, 0, ff, LatFlatten{});
         return hipGetLastError();
@@ -1808,8 +1808,8 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         const int tpw = n <= 31 ? 2 : 1;
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
     }
-    KtScope kt(KT_RT_PREPARE, st);
-    hipLaunchKernelGGL(rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
+    const int kt_id = KT_RT_PREPARE;
+    kt_launch(kt_id, rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
                        d_tc, d_shade, prep, Fl, d_sph, d_lat_masks, 0);
     return hipGetLastError();
 }
@@ -1868,12 +1868,12 @@ hipError_t launch_rt_lattice_units(const RtFrame &F, const RtTri *d_tc, const Rt
 {
     if (F.n_lights <= 1) return hipSuccess;
     const dim3 grid(F.txn ? F.txn : lat_tiles_x(F), (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
-    KtScope kt(KT_RT_LATTICE_UNITS, st);
+    const int kt_id = KT_RT_LATTICE_UNITS;
     if (lat_yaw(F))
-        hipLaunchKernelGGL(rt_lattice_units_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+        kt_launch(kt_id, rt_lattice_units_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, d_umask);
     else
-        hipLaunchKernelGGL(rt_lattice_units_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+        kt_launch(kt_id, rt_lattice_units_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, d_umask);
     return hipGetLastError();
 }
@@ -1888,18 +1888,18 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
     const dim3 grid(F.txn ? F.txn : lat_tiles_x(F), (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     if (F.n_lights > 1 && !d_umask) return hipErrorInvalidValue;
     if (F.txn && (F.tx0 < 0 || F.tx0 + F.txn > lat_tiles_x(F))) return hipErrorInvalidValue;
-    KtScope kt(F.n_lights == 1 ? KT_RT_LATTICE : KT_RT_LATTICE_LIGHTS, st);
+    const int kt_id = F.n_lights == 1 ? KT_RT_LATTICE : KT_RT_LATTICE_LIGHTS;
     if (F.n_lights == 1 && lat_yaw(F))
-        hipLaunchKernelGGL(rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+        kt_launch(kt_id, rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, cams, out_stride, d_out, d_done, O);
     else if (F.n_lights == 1)
-        hipLaunchKernelGGL(rt_lattice_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
+        kt_launch(kt_id, rt_lattice_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
                            cams, out_stride, d_out, d_done, O);
     else if (lat_yaw(F))
-        hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+        kt_launch(kt_id, rt_lattice_lights_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, d_umask, cams, out_stride, d_out, d_done);
     else
-        hipLaunchKernelGGL(rt_lattice_lights_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
+        kt_launch(kt_id, rt_lattice_lights_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, d_umask, cams, out_stride, d_out, d_done);
     return hipGetLastError();
 }
@@ -1917,12 +1917,12 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, d_umask, cams, 1, 0, d_out, st,
                                         nullptr, nullptr);
     }
-    KtScope kt(KT_RT_PIXEL, st);
+    const int kt_id = KT_RT_PIXEL;
     if (F.n_tris <= 64 && F.cull_primary)
-        hipLaunchKernelGGL(rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
+        kt_launch(kt_id, rt_pixel_kernel<true>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     else
-        hipLaunchKernelGGL(rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
+        kt_launch(kt_id, rt_pixel_kernel<false>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade,
                            d_sph, d_out);
     return hipGetLastError();
 }

@@ -2562,13 +2562,13 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
         else hipLaunchKernelGGL(rt_walk_order_kernel, dim3(1), dim3(1024), 0, st, B, (int)pgrid.x, (int)pgrid.y);
     }
     {
-        KtScope kt(KT_RT_BIG_PRIMARY, st);
+        const int kt_id = KT_RT_BIG_PRIMARY;
         if (lat && B.lat_yaw)
-            hipLaunchKernelGGL(rt_big_primary_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+            kt_launch(kt_id, rt_big_primary_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         else if (lat)
-            hipLaunchKernelGGL(rt_big_primary_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+            kt_launch(kt_id, rt_big_primary_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         else
-            hipLaunchKernelGGL(rt_big_primary_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+            kt_launch(kt_id, rt_big_primary_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
     }
     if (!flags_fit) {
         hipLaunchKernelGGL(rt_bin_boxes_kernel, dim3(bins), dim3(64), 0, st, B);
@@ -2577,13 +2577,13 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     } else if (F.n_lights > 0) {
         hipLaunchKernelGGL(rt_lit_class_kernel, dim3(bgrid.x), dim3(256), 0, st, F, d_tc, B);
         {
-            KtScope kt(KT_RT_SHADOW_HINTS, st);
+            const int kt_id = KT_RT_SHADOW_HINTS;
             if (lat && B.lat_yaw)
-                hipLaunchKernelGGL(rt_shadow_hints_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+                kt_launch(kt_id, rt_shadow_hints_kernel<2>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
             else if (lat)
-                hipLaunchKernelGGL(rt_shadow_hints_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+                kt_launch(kt_id, rt_shadow_hints_kernel<1>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
             else
-                hipLaunchKernelGGL(rt_shadow_hints_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
+                kt_launch(kt_id, rt_shadow_hints_kernel<0>, pgrid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, B);
         }
         static const int pl_wgs = [] {   // A/B: CG_PL_WGS
             const char *e = std::getenv("CG_PL_WGS");
