@@ -1226,6 +1226,47 @@ __device__ __forceinline__ bool lat_lights_tile(const RtFrame &F0, const RtTri *
 template <int PITCH>
 __host__ __device__ constexpr int lat_unit_slots() { return kLatParts * PITCH; }
 
+// The unit masks in HBM.  Each is a subset of its tile's shadow mask (plus
+// bit 63, a sphere may block), so a tile with at most kUnitNarrow candidates
+// stores a unit as one byte -- bit i: the tile's i-th candidate is kept, bit
+// 7: the sphere flag -- in a byte array [frame][tile][slot]; a wider tile
+// stores the units' 64-bit masks in the array that follows (8-byte aligned).
+// C4's tiles have 0-5 candidates: 1 byte per unit written and read instead of 8.
+// A tile with no candidate triangle and no sphere that may block (every unit
+// mask 0) stores and reads nothing.
+constexpr int kUnitNarrow = 7;
+__device__ __forceinline__ bool lat_units_empty(unsigned long long smask, const RtFrame &Fs)
+{
+    return smask == 0ull && Fs.n_sph == 0;
+}
+template <int PITCH>
+__device__ __forceinline__ size_t lat_unit_index(const RtFrame &F, size_t tix)
+{
+    return ((size_t)blockIdx.z * lat_tiles_x(F) * gridDim.y + tix) * lat_unit_slots<PITCH>() + threadIdx.x;
+}
+template <int PITCH>
+__device__ __forceinline__ size_t lat_unit_wide_bytes(const RtFrame &F)   // byte offset of the 64-bit array
+{
+    const size_t n = (size_t)gridDim.z * lat_tiles_x(F) * gridDim.y * lat_unit_slots<PITCH>();
+    return (n + 7) & ~(size_t)7;
+}
+__device__ __forceinline__ uint32_t lat_unit_code(unsigned long long um, unsigned long long smask)
+{
+    uint32_t c = (uint32_t)(um >> 63) << 7;
+    int i = 0;
+    for (unsigned long long m = smask; m; m &= m - 1ull, ++i)
+        if (um & (m & (0ull - m))) c |= 1u << i;
+    return c;
+}
+__device__ __forceinline__ unsigned long long lat_unit_mask(uint32_t code, unsigned long long smask)
+{
+    unsigned long long um = (unsigned long long)(code >> 7) << 63;
+    int i = 0;
+    for (unsigned long long m = smask; m; m &= m - 1ull, ++i)
+        if ((code >> i) & 1u) um |= m & (0ull - m);
+    return um;
+}
+
 // The unit certificates of a light-set tile: the tile's shadow mask
 // re-certified over each (part, column) unit's exact hit positions (pos as
 // DirectLight forms it), plus the own-triangle certificate when every hit of
@@ -1314,9 +1355,13 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
     __syncthreads();
     if (threadIdx.x < kLatParts * PITCH) {
         const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
-        if (h < nhalf && cx < cols)
-            umask[((size_t)blockIdx.z * lat_tiles_x(F) * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x] =
-                s_umask[h][cx];
+        if (h < nhalf && cx < cols && !lat_units_empty(smask, T.Fs)) {
+            const size_t ui = lat_unit_index<PITCH>(F, T.tix);
+            if (nc <= kUnitNarrow)
+                ((uint8_t *)umask)[ui] = (uint8_t)lat_unit_code(s_umask[h][cx], smask);
+            else
+                ((unsigned long long *)((uint8_t *)umask + lat_unit_wide_bytes<PITCH>(F)))[ui] = s_umask[h][cx];
+        }
     }
 }
 
@@ -1358,9 +1403,14 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
         // the units' shadow candidates (rt_lattice_units_kernel)
         if (threadIdx.x < kLatParts * PITCH) {
             const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
-            if (h < T.nhalf && cx < cols)
-                s_umask[h][cx] =
-                    umask[((size_t)blockIdx.z * lat_tiles_x(F) * gridDim.y + T.tix) * lat_unit_slots<PITCH>() + threadIdx.x];
+            if (h < T.nhalf && cx < cols) {
+                const size_t ui = lat_unit_index<PITCH>(F, T.tix);
+                s_umask[h][cx] = lat_units_empty(T.smask, Fs) ? 0ull
+                                 : __popcll(T.smask) <= kUnitNarrow
+                                     ? lat_unit_mask(((const uint8_t *)umask)[ui], T.smask)
+                                     : ((const unsigned long long *)((const uint8_t *)umask +
+                                                                     lat_unit_wide_bytes<PITCH>(F)))[ui];
+            }
         }
     }
     __syncthreads();
@@ -1859,7 +1909,8 @@ size_t rt_lattice_unit_bytes(const RtFrame &F, int nframes)
 {
     if (!rt_use_lattice(F) || F.n_lights <= 1) return 0;
     const int slots = lat_yaw(F) ? lat_unit_slots<kLatWY>() : lat_unit_slots<kLatW>();
-    return (size_t)nframes * rt_lattice_tiles(F) * slots * sizeof(unsigned long long);
+    const size_t n = (size_t)nframes * rt_lattice_tiles(F) * slots;   // byte codes, then the 64-bit masks
+    return ((n + 7) & ~(size_t)7) + n * sizeof(unsigned long long);
 }
 
 hipError_t launch_rt_lattice_units(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade,
