@@ -1227,14 +1227,15 @@ template <int PITCH>
 __host__ __device__ constexpr int lat_unit_slots() { return kLatParts * PITCH; }
 
 // The unit masks in HBM.  Each is a subset of its tile's shadow mask (plus
-// bit 63, a sphere may block), so a tile with at most kUnitNarrow candidates
-// stores a unit as one byte -- bit i: the tile's i-th candidate is kept, bit
-// 7: the sphere flag -- in a byte array [frame][tile][slot]; a wider tile
-// stores the units' 64-bit masks in the array that follows (8-byte aligned).
-// C4's tiles have 0-5 candidates: 1 byte per unit written and read instead of 8.
-// A tile with no candidate triangle and no sphere that may block (every unit
-// mask 0) stores and reads nothing.
-constexpr int kUnitNarrow = 7;
+// bit 63, a sphere may block), so a tile with few candidates stores its units
+// as codes in a byte array [frame][tile][slot]: with at most kUnitNibble
+// candidates a unit is a nibble (bit i: the tile's i-th candidate is kept, bit
+// 3: the sphere flag; units 2j and 2j + 1 share byte j), with at most
+// kUnitNarrow a byte (sphere flag bit 7); a wider tile stores the units'
+// 64-bit masks in the array that follows (8-byte aligned).  A tile with no
+// candidate triangle and no sphere that may block (every unit mask 0) stores
+// and reads nothing.  C4's tiles have 0-5 candidates.
+constexpr int kUnitNibble = 3, kUnitNarrow = 7;
 __device__ __forceinline__ bool lat_units_empty(unsigned long long smask, const RtFrame &Fs)
 {
     return smask == 0ull && Fs.n_sph == 0;
@@ -1250,17 +1251,17 @@ __device__ __forceinline__ size_t lat_unit_wide_bytes(const RtFrame &F)   // byt
     const size_t n = (size_t)gridDim.z * lat_tiles_x(F) * gridDim.y * lat_unit_slots<PITCH>();
     return (n + 7) & ~(size_t)7;
 }
-__device__ __forceinline__ uint32_t lat_unit_code(unsigned long long um, unsigned long long smask)
+__device__ __forceinline__ uint32_t lat_unit_code(unsigned long long um, unsigned long long smask, int sb)
 {
-    uint32_t c = (uint32_t)(um >> 63) << 7;
+    uint32_t c = (uint32_t)(um >> 63) << sb;
     int i = 0;
     for (unsigned long long m = smask; m; m &= m - 1ull, ++i)
         if (um & (m & (0ull - m))) c |= 1u << i;
     return c;
 }
-__device__ __forceinline__ unsigned long long lat_unit_mask(uint32_t code, unsigned long long smask)
+__device__ __forceinline__ unsigned long long lat_unit_mask(uint32_t code, unsigned long long smask, int sb)
 {
-    unsigned long long um = (unsigned long long)(code >> 7) << 63;
+    unsigned long long um = (unsigned long long)((code >> sb) & 1u) << 63;
     int i = 0;
     for (unsigned long long m = smask; m; m &= m - 1ull, ++i)
         if ((code >> i) & 1u) um |= m & (0ull - m);
@@ -1353,12 +1354,24 @@ __device__ __forceinline__ void lattice_units_body(const RtFrame &F0, const RtTr
         if (may) atomicOr(&s_umask[h][cx], 1ull << 63);
     }
     __syncthreads();
-    if (threadIdx.x < kLatParts * PITCH) {
+    constexpr int kSlots = kLatParts * PITCH;
+    if (lat_units_empty(smask, T.Fs)) return;
+    const size_t ui = lat_unit_index<PITCH>(F, T.tix);
+    if (nc <= kUnitNibble) {   // units 2j, 2j + 1 -> byte j (units outside the tile: 0)
+        const int j = threadIdx.x;
+        if (2 * j < kSlots) {
+            uint32_t b = 0u;
+            for (int e = 0; e < 2; ++e) {
+                const int u = 2 * j + e, h = u / PITCH, cx = u - h * PITCH;
+                if (u < kSlots && h < nhalf && cx < cols) b |= lat_unit_code(s_umask[h][cx], smask, 3) << (4 * e);
+            }
+            ((uint8_t *)umask)[ui - threadIdx.x + j] = (uint8_t)b;
+        }
+    } else if (threadIdx.x < kSlots) {
         const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
-        if (h < nhalf && cx < cols && !lat_units_empty(smask, T.Fs)) {
-            const size_t ui = lat_unit_index<PITCH>(F, T.tix);
+        if (h < nhalf && cx < cols) {
             if (nc <= kUnitNarrow)
-                ((uint8_t *)umask)[ui] = (uint8_t)lat_unit_code(s_umask[h][cx], smask);
+                ((uint8_t *)umask)[ui] = (uint8_t)lat_unit_code(s_umask[h][cx], smask, 7);
             else
                 ((unsigned long long *)((uint8_t *)umask + lat_unit_wide_bytes<PITCH>(F)))[ui] = s_umask[h][cx];
         }
@@ -1405,11 +1418,15 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
             const int h = threadIdx.x / PITCH, cx = threadIdx.x - h * PITCH;
             if (h < T.nhalf && cx < cols) {
                 const size_t ui = lat_unit_index<PITCH>(F, T.tix);
-                s_umask[h][cx] = lat_units_empty(T.smask, Fs) ? 0ull
-                                 : __popcll(T.smask) <= kUnitNarrow
-                                     ? lat_unit_mask(((const uint8_t *)umask)[ui], T.smask)
-                                     : ((const unsigned long long *)((const uint8_t *)umask +
-                                                                     lat_unit_wide_bytes<PITCH>(F)))[ui];
+                const int nc = __popcll(T.smask);
+                const uint8_t *code = (const uint8_t *)umask;
+                s_umask[h][cx] =
+                    lat_units_empty(T.smask, Fs) ? 0ull
+                    : nc <= kUnitNibble
+                        ? lat_unit_mask(code[ui - threadIdx.x + threadIdx.x / 2] >> (4 * (threadIdx.x & 1)), T.smask, 3)
+                    : nc <= kUnitNarrow
+                        ? lat_unit_mask(code[ui], T.smask, 7)
+                        : ((const unsigned long long *)(code + lat_unit_wide_bytes<PITCH>(F)))[ui];
             }
         }
     }
