@@ -424,12 +424,13 @@ int cg_image_decode_jpeg_device(cg_ctx *ctx, const uint8_t *data, size_t n, uint
                                 void *stream);
 
 /* ---- measurement ----------------------------------------------------- */
-/* Live device time of the hot kernels: while on, HIP events are recorded
- * around each launch of rt_prepare_kernel, rt_tile_cert_kernel,
+/* Live device time of the hot kernels: while on, a start / stop HIP event
+ * pair rides on each launch's own dispatch (hipExtLaunchKernel) of
+ * rt_prepare_kernel, rt_tile_cert_kernel,
  * rt_lattice_units_kernel, rt_lattice_kernel, rt_lattice_lights_kernel,
  * rt_pixel_kernel, rt_big_primary_kernel, rt_shadow_hints_kernel,
  * rast_fill_kernel and rast_post_kernel, on the stream it runs on, plus
- * "rt_big_frame" (a large scene's whole frame).  cg_kernel_timing(on)
+ * "rt_big_frame" (a large scene's whole frame: events recorded around it).  cg_kernel_timing(on)
  * resets the totals (process-wide); cg_kernel_time waits for the recorded
  * launches and returns one kernel's summed launch milliseconds, its busy
  * milliseconds (the union of its launches' spans: launches that overlap on
