@@ -9,11 +9,21 @@ one light, 3x3 supersampling) on N MI355X.
 8x8 area light = 64 lights) and c5 (1080p over 1M random triangles) are the
 build-defined SURVEY.md 8d workloads, measured the same way.
 
-A step is one whole frame: every rank renders its framebuffer stripes
-(cg_rt_render_device, inputs already resident in HBM), rank 0 gathers the
-stripes over RCCL and reassembles the frame on the device
-(cg_rt_unstripe_device).  N > 1 is launched by the driver with torchrun.
-Prints ONE JSON line on rank 0.
+A step is one whole frame, inputs resident in HBM.  N = 1: frames rendered 32
+per cg_rt_render_frames_device call.  N > 1 (default layout `bands`): every
+rank renders one balanced contiguous band of rows through the library's
+cg_rt_render_frames_dist (csrc/cg_dist.hip); ranks > 0 send their bands in the
+RGB24 wire format to rank 0 over RCCL point-to-point (xGMI), and rank 0
+assembles the frames in place.  `--layout stripes` (the gloo rehearsal's
+default) is the older round-robin stripes + gather + unstripe path.
+
+N > 1 either comes from a launcher (torchrun: WORLD_SIZE/RANK/LOCAL_RANK/
+MASTER_* in the environment; WORLD_SIZE must equal --gpus) or, when WORLD_SIZE
+is unset, from bench.py itself: the parent starts N fresh rank processes
+before anything touches the GPU (launch_ranks), each with RANK = LOCAL_RANK =
+r, WORLD_SIZE = N and MASTER_ADDR/PORT = 127.0.0.1:<free port>, relays rank 0's
+single JSON line and exits non-zero if any rank fails or outlives
+--rank-timeout.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -27,6 +37,129 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+# ---- N > 1 without an external launcher -----------------------------------
+# Everything here runs before torch / the library are imported: the parent never touches the GPU,
+# and its children are fresh processes (never an exec of an initialised one).
+
+def argv_gpus(argv):
+    """--gpus N / --gpus=N from a command line (1 when absent)."""
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def free_port(host="127.0.0.1"):
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind((host, 0))
+        return sk.getsockname()[1]
+
+
+def launch_plan(n, argv, base_env, port, addr="127.0.0.1", python=None):
+    """(argv, env) of each of the n rank processes: the same bench.py command line, with the
+    torch.distributed rendezvous of one node in the environment."""
+    python = python or sys.executable
+    plan = []
+    for r in range(n):
+        env = dict(base_env)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=addr, MASTER_PORT=str(port))
+        plan.append(([python, "-u"] + list(argv), env))
+    return plan
+
+
+def _die_with_parent():
+    """Child side of Popen: SIGKILL this rank if the launching parent dies (Linux prctl)."""
+    try:
+        import ctypes as _c
+        import signal as _s
+        _c.CDLL("libc.so.6", use_errno=True).prctl(1, int(_s.SIGKILL))   # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):
+        pass
+
+
+def run_ranks(plan, timeout_s=None, poll_s=0.05, out=None, err=None):
+    """Start every rank of `plan` as a child process, rank 0's stdout to `out` (the parent's
+    stdout: its one JSON line), the other ranks' stdout to `err`; return 0 when every rank exits
+    0, else the first failing rank's exit code (a signal -s as 128 + s), after terminating the
+    others.  A rank still running after timeout_s seconds fails the job with 124."""
+    import signal
+    import subprocess
+    out = out if out is not None else sys.stdout
+    err = err if err is not None else sys.stderr
+    out.flush()
+    err.flush()
+    procs = []
+    try:
+        for r, (cmd, env) in enumerate(plan):
+            procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=out if r == 0 else err, stderr=err,
+                                          preexec_fn=_die_with_parent))
+        t0 = time.monotonic()
+        failed = None
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                failed = 128 - c if c < 0 else c
+                print(f"bench.py launcher: rank {r} exited with {c}; stopping the other ranks",
+                      file=err, flush=True)
+                break
+            if all(c == 0 for c in codes):
+                return 0
+            if timeout_s and time.monotonic() - t0 > timeout_s:
+                print(f"bench.py launcher: ranks still running after {timeout_s} s; stopping them",
+                      file=err, flush=True)
+                failed = 124
+                break
+            time.sleep(poll_s)
+        return failed
+    finally:
+        for p in procs:                     # exactly the PIDs started here
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        end = time.monotonic() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+
+def launch_if_needed(argv):
+    """None when this process is a rank (a launcher set WORLD_SIZE, or N = 1); otherwise the
+    exit code of the N-rank job started here.  WORLD_SIZE set and != --gpus fails loudly."""
+    n = argv_gpus(argv)
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        given = any(a == "--gpus" or a.startswith("--gpus=") for a in argv)
+        if given and int(ws) != n:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {n}")
+        return None
+    if n <= 1:
+        return None
+    timeout = 0.0
+    for i, a in enumerate(argv):
+        if a == "--rank-timeout" and i + 1 < len(argv):
+            timeout = float(argv[i + 1])
+        elif a.startswith("--rank-timeout="):
+            timeout = float(a.split("=", 1)[1])
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this host driver
+    plan = launch_plan(n, [os.path.abspath(__file__)] + list(argv), env, free_port())
+    return run_ranks(plan, timeout_s=timeout or None)
+
+
+if __name__ == "__main__":
+    _rc = launch_if_needed(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
 sys.path[:0] = [os.path.join(ROOT, "computer-graphics_amd"), os.path.join(ROOT, "oracle"),
                 os.path.join(ROOT, "tests", "golden")]
 
@@ -452,9 +585,10 @@ def main():
                     help="RT frames per render call (launches of <= 32 frames, their certificates pipelined) "
                          "and, for N > 1, per transfer to rank 0 (halves the per-frame host cost of the "
                          "exchange vs 16); every frame is rendered and gathered")
-    ap.add_argument("--layout", choices=["bands", "stripes"], default="bands",
-                    help="N > 1 RT sharding: balanced contiguous bands received in place (default), or "
-                         "round-robin stripes + RCCL gather + unstripe")
+    ap.add_argument("--layout", choices=["bands", "stripes"], default=None,
+                    help="N > 1 RT sharding: balanced contiguous bands received in place (default with nccl), or "
+                         "round-robin stripes + gather + unstripe (default with gloo: the rehearsal of N ranks on "
+                         "fewer GPUs, through host memory)")
     ap.add_argument("--chunk", type=int, default=4,
                     help="N > 1 bands: frames per chunk of the library's render/transfer pipeline")
     ap.add_argument("--balance-rounds", type=int, default=3,
@@ -464,7 +598,11 @@ def main():
                          "past it the communicator is aborted and the run fails instead of hanging")
     ap.add_argument("--backend", default=os.environ.get("CG_DIST_BACKEND", "nccl"),
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 ranks on one GPU")
+    ap.add_argument("--rank-timeout", type=float, default=0.0,
+                    help="N > 1 started by bench.py itself: fail the job (exit 124) if a rank runs longer (s; 0 = none)")
     args = ap.parse_args()
+    if args.layout is None:
+        args.layout = "bands" if args.backend == "nccl" else "stripes"
     if args.steps is None:
         args.steps = {"rt": 800, "rast": 800, "c4": 64, "c5": 20, "c5yaw": 20, "yaw": 320, "f256": 800}[args.workload]
     if args.warmup is None:

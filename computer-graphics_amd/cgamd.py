@@ -575,8 +575,16 @@ class Context:
         arr = (RtCamera * len(cams))(*cams)
         npx = cams[0].width * cams[0].height
         stride = frame_stride or npx
+        if stride < npx:
+            raise ValueError(f"frame_stride {stride} < W*H = {npx}")
         if out is None:
             out = np.zeros(len(cams) * stride, np.uint32)
+        # the C entry has no capacity argument: the last frame ends at (n - 1) * stride + W * H
+        # pixels, and a caller's buffer shorter than that would be written past its end
+        need = (len(cams) - 1) * stride + npx
+        have = (out.nbytes if isinstance(out, np.ndarray) else out.numel() * out.element_size()) // 4
+        if have < need:
+            raise ValueError(f"out holds {have} pixels, {len(cams)} frames at stride {stride} need {need}")
         ptr = out.ctypes.data if isinstance(out, np.ndarray) else out.data_ptr()
         st = Stats()
         self._check(self.lib.cg_rt_render_frames(self.h, lights, len(lights), arr, len(cams), P(ptr), stride, chunk,

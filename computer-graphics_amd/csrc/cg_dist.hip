@@ -126,6 +126,7 @@ struct cg_dist {
     // bounded waits
     int timeout_ms = 60000;           // deadline of every host wait
     bool aborted = false;             // communicator aborted after an error / timeout
+    bool leaked = false;              // the abort did not finish in time: device memory kept (see abort_comm)
     hipStream_t last_st = nullptr;    // render stream of the last call
     hipEvent_t ev_wait[2] = {};       // cg_dist_wait: render stream, transfer stream
 };
@@ -184,8 +185,15 @@ void abort_comm(cg_dist *d)
     });
     const auto end = Clock::now() + std::chrono::seconds(10);
     while (!done->load() && Clock::now() < end) poll_pause();
-    if (done->load()) t.join();
-    else t.detach();
+    if (done->load()) {
+        t.join();
+    } else {
+        // the abort is still running, and RCCL kernels it has not yet ended may
+        // still read or write this handle's buffers: cg_dist_destroy leaks them
+        // (and the streams) rather than free memory a running kernel may touch
+        t.detach();
+        d->leaked = true;
+    }
 }
 
 // The communicator's state after an RCCL call: ncclInProgress (non-blocking
@@ -219,11 +227,38 @@ int nccl_settle(cg_dist *d, ncclResult_t r, const char *what)
         if (rc_) return rc_;                                   \
     } while (0)
 
+// Rank 0's receives of one chunk from ranks 1 .. n-1 (bytes[p] each, packed
+// from buf in rank order) as one RCCL group.  The group is always closed --
+// ncclGroupEnd runs even when a receive inside it failed -- before the error
+// is settled (and the communicator aborted), so the calling thread's RCCL group
+// depth never stays open after an error return.
+int recv_group(cg_dist *d, uint8_t *buf, const size_t *bytes, int n)
+{
+    if (d->aborted) return fail(d, CG_E_HIP, "communicator was aborted by an earlier error");
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return nccl_settle(d, r, "ncclGroupStart");
+    ncclResult_t first = ncclSuccess;
+    size_t off = 0;
+    for (int p = 1; p < n; ++p) {
+        if (bytes[p] && first == ncclSuccess) {
+            r = ncclRecv(buf + off, bytes[p], ncclUint8, p, d->comm, d->xs);
+            if (r != ncclSuccess && r != ncclInProgress) first = r;
+        }
+        off += bytes[p];
+    }
+    const ncclResult_t e = ncclGroupEnd();
+    return first != ncclSuccess ? nccl_settle(d, first, "ncclRecv") : nccl_settle(d, e, "ncclGroupEnd");
+}
+
 // Host wait for events (nullptr entries skipped) against the deadline, polling
-// the communicator's asynchronous error meanwhile.
+// the communicator's asynchronous error meanwhile.  The deadline runs from the
+// last progress -- the start of the wait, or the latest event seen complete --
+// so a healthy rank that queued more than timeout_ms of work in several steps
+// is not aborted; a wait on ONE event still covers everything queued before it.
 int wait_events(cg_dist *d, const hipEvent_t *ev, int n, const char *what)
 {
-    const auto t0 = Clock::now(), end = t0 + std::chrono::milliseconds(d->timeout_ms);
+    const auto t0 = Clock::now();
+    auto end = t0 + std::chrono::milliseconds(d->timeout_ms);
     for (int i = 0; i < n;) {
         if (!ev[i]) {
             ++i;
@@ -232,6 +267,7 @@ int wait_events(cg_dist *d, const hipEvent_t *ev, int n, const char *what)
         const hipError_t q = hipEventQuery(ev[i]);
         if (q == hipSuccess) {
             ++i;
+            end = Clock::now() + std::chrono::milliseconds(d->timeout_ms);
             continue;
         }
         if (q != hipErrorNotReady) return fail(d, CG_E_HIP, std::string(what) + ": " + hipGetErrorString(q));
@@ -513,7 +549,7 @@ extern "C" void cg_dist_destroy(cg_dist *d)
     for (int k = 0; k < 2; ++k) {
         if (d->ev_call[k]) (void)hipEventDestroy(d->ev_call[k]);
         if (d->ev_zero[k]) (void)hipEventDestroy(d->ev_zero[k]);
-        if (d->done[k]) (void)hipFree(d->done[k]);
+        if (d->done[k] && !d->leaked) (void)hipFree(d->done[k]);
     }
     for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
     for (auto *pool : {&d->t_rend, &d->t_asm})
@@ -521,6 +557,12 @@ extern "C" void cg_dist_destroy(cg_dist *d)
             (void)hipEventDestroy(t.a);
             (void)hipEventDestroy(t.b);
         }
+    if (d->leaked) {
+        // an abort that did not finish (abort_comm): keep every device buffer and
+        // the transfer stream alive for the process's lifetime
+        for (Mem *m : {&d->sbuf[0], &d->sbuf[1], &d->rbuf[0], &d->rbuf[1], &d->sall, &d->stats}) m->p = nullptr;
+        d->xs = nullptr;
+    }
     if (d->xs) (void)hipStreamDestroy(d->xs);
     if (d->group) {   // the last member frees the group
         auto &m = d->group->members;
@@ -801,13 +843,13 @@ static int render_signalled(cg_dist *d, const cg_light *lights, int n_lights, co
                     off += bytes;
                 }
             } else {
-                DN(d, ncclGroupStart(), "ncclGroupStart");
+                std::vector<size_t> bytes(n, 0);
                 for (int p = 1; p < n; ++p) {
-                    const size_t bytes = (size_t)nf * d->rows[p] * row_bytes;
-                    if (bytes) DN(d, ncclRecv(cb + off, bytes, ncclUint8, p, d->comm, d->xs), "ncclRecv");
-                    off += bytes;
+                    bytes[p] = (size_t)nf * d->rows[p] * row_bytes;
+                    off += bytes[p];
                 }
-                DN(d, ncclGroupEnd(), "ncclGroupEnd");
+                rc = recv_group(d, cb, bytes.data(), n);
+                if (rc) return rc;
             }
             // assembly of the chunk on the transfer stream (rows disjoint from
             // the render's own band)
@@ -920,14 +962,10 @@ extern "C" int cg_rt_render_frames_dist(cg_dist *d, const cg_light *lights, int 
                     off += bytes;
                 }
             } else {
-                DN(d, ncclGroupStart(), "ncclGroupStart");
-                size_t off = 0;
-                for (int p = 1; p < n; ++p) {
-                    const size_t bytes = (size_t)nf * d->rows[p] * row_bytes;
-                    if (bytes) DN(d, ncclRecv(rb + off, bytes, ncclUint8, p, d->comm, d->xs), "ncclRecv");
-                    off += bytes;
-                }
-                DN(d, ncclGroupEnd(), "ncclGroupEnd");
+                std::vector<size_t> bytes(n, 0);
+                for (int p = 1; p < n; ++p) bytes[p] = (size_t)nf * d->rows[p] * row_bytes;
+                rc = recv_group(d, rb, bytes.data(), n);
+                if (rc) return rc;
             }
             DT(d, hipEventRecord(d->ev_recv[s], d->xs), "event");
             // assembly of the received bands on the render stream

@@ -1023,6 +1023,9 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
                          (long long)gx * gy * nf <= kLatOrderRounds * lat_resident_wgs();
     if (ordered) {
         for (int q = 0; q < 2; ++q) {
+            // a reallocated cost map holds no recording: forget both slots' keys, or a later
+            // call of the earlier geometry would sort uninitialised memory
+            if ((size_t)gx * gy > c->lcost[q].bytes) c->lrec_key[0] = c->lrec_key[1] = 0ull;
             CG_TRY(c, c->lcost[q].ensure((size_t)gx * gy), "alloc lattice order");
             CG_TRY(c, c->lflat[q].ensure((size_t)gx * gy * sizeof(uint32_t)), "alloc lattice order");
         }

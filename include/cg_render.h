@@ -271,7 +271,13 @@ int cg_dist_unique_id(cg_dist_id *id);
  * else 60000 ms).  An RCCL error returns CG_E_HIP and a passed deadline
  * CG_E_TIMEOUT; either aborts the communicator (ncclCommAbort: kernels still
  * waiting on a peer exit) and every later call on the handle fails CG_E_HIP.
- * A missing peer therefore ends the job with an error instead of a hang. */
+ * A missing peer therefore ends the job with an error instead of a hang.
+ * The deadline runs from the last progress of a wait (its start, or the
+ * latest of its events seen complete), but one event covers everything queued
+ * before it: cg_dist_wait's deadline must exceed the rank's queued backlog.
+ * If the abort itself does not return within 10 s it is left running and
+ * cg_dist_destroy deliberately leaks the handle's device buffers and transfer
+ * stream (RCCL kernels may still be using them). */
 int cg_dist_create(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, cg_dist **out);
 /* cg_dist_create with an explicit deadline in ms (0: the default above). */
 int cg_dist_create_timed(cg_ctx *ctx, int nranks, int rank, const cg_dist_id *id, int timeout_ms, cg_dist **out);
