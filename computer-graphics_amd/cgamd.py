@@ -107,6 +107,7 @@ _SIGS = {
     "cg_rt_pool_demand": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "cg_rt_route": (C.c_int, [C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "cg_rt_set_pool_caps": (C.c_int, [P, C.c_longlong, C.c_longlong, C.c_longlong, C.c_longlong]),
+    "cg_rt_render_brute_device": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int, C.c_int, P, P]),
     "cg_rt_render": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), P, C.POINTER(Stats)]),
     "cg_rt_render_frames": (C.c_int, [P, C.POINTER(Light), C.c_int, C.POINTER(RtCamera), C.c_int, P,
                                       C.c_size_t, C.c_int, C.POINTER(Stats)]),
@@ -545,6 +546,13 @@ class Context:
     def rt_set_pool_caps(self, sup=0, bin=0, sbin=0, sorted=0):
         """Test hook: pin the large-scene pool capacities (all 0 = automatic)."""
         self._check(self.lib.cg_rt_set_pool_caps(self.h, sup, bin, sbin, sorted), "cg_rt_set_pool_caps")
+
+    def rt_render_brute_device(self, cam, row0, rows, d_out, lights=None, stream=None):
+        """Test hook cg_rt_render_brute_device: rows row0 .. row0 + rows - 1 of cam's frame into the
+        device buffer d_out by the reference's unaccelerated loop (synchronous)."""
+        lights = default_lights() if lights is None else lights
+        self._check(self.lib.cg_rt_render_brute_device(self.h, lights, len(lights), C.byref(cam), row0, rows, P(d_out),
+                                                       P(stream) if stream else None), "cg_rt_render_brute_device")
 
     def rt_scratch_info(self):
         """Large-scene scratch after the latest frame: dict(bytes, listed, capacity, overflows)."""

@@ -74,7 +74,19 @@ struct alignas(16) RtTri {
 };
 static_assert(sizeof(RtTri) == 64, "RtTri must be 64 B");
 
-// Shading attributes, read only on a hit.
+// The camera-independent part of RtTri, formed once per scene (rt_scene_kernel
+// at cg_rt_set_scene): e1, e2, v0 and K1, the same float ops as RtTri's.  48 B,
+// three 16-byte loads, so the per-frame prepare pass streams 48 B in and 64 B
+// out per triangle instead of gathering the 76-byte Triangle records.
+struct alignas(16) RtGeo {
+    float e1x, e1y, e1z, e2x;
+    float e2y, e2z, v0x, v0y;
+    float v0z, K1, pad0, pad1;
+};
+static_assert(sizeof(RtGeo) == 48, "RtGeo must be 48 B");
+
+// Shading attributes, read only on a hit.  Camera-independent: written once
+// per scene (rt_scene_kernel), shared by every slot and frame.
 struct alignas(16) RtShade {
     float nx, ny, nz, nw;   // Triangle::normal (w = 1)
     float cr, cg, cb, pad;  // Triangle::color

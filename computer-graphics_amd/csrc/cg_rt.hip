@@ -286,30 +286,107 @@ __device__ __forceinline__ void unit_cert(const cg_tri *__restrict__ tris, int n
     sm_out = act ? sm : 0ull;
 }
 
-// Per-frame RtTri / RtShade of triangle i (threads of the first n_prep_blocks blocks).
-__device__ __forceinline__ void prep_tri(const cg_tri *__restrict__ tris, int n, int i, int frame, const float camf[4],
-                                         RtTri *__restrict__ out, RtShade *__restrict__ shade)
+// Per-scene constants of triangle i (rt_scene_kernel): the camera-independent
+// part of rt_tri_const (e1, e2, v0, K1: the same float ops) and the shading
+// attributes.
+__global__ void rt_scene_kernel(const cg_tri *__restrict__ tris, int n, RtGeo *__restrict__ geo,
+                                RtShade *__restrict__ shade)
 {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const cg_tri T = tris[i];
-    out[(size_t)frame * n + i] = rt_tri_const(T, camf[0], camf[1], camf[2], camf[3]);
-    if (frame == 0) {   // camera-independent
-        RtShade sh;
-        sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
-        sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
-        shade[i] = sh;
+    const RtTri c = rt_tri_const(T, 0.f, 0.f, 0.f, 0.f);
+    RtGeo g;
+    g.e1x = c.e1x; g.e1y = c.e1y; g.e1z = c.e1z; g.e2x = c.e2x;
+    g.e2y = c.e2y; g.e2z = c.e2z; g.v0x = c.v0x; g.v0y = c.v0y;
+    g.v0z = c.v0z; g.K1 = c.K1; g.pad0 = 0.f; g.pad1 = 0.f;
+    geo[i] = g;
+    RtShade sh;
+    sh.nx = T.normal.x; sh.ny = T.normal.y; sh.nz = T.normal.z; sh.nw = T.normal.w;
+    sh.cr = T.color.x; sh.cg = T.color.y; sh.cb = T.color.z; sh.pad = 0.f;
+    shade[i] = sh;
+}
+
+// RtTri of a triangle for rays from camf, from its per-scene RtGeo: s =
+// cameraPos - v0 (skeleton.cpp:296-297, the xyz of rt_tri_const's vec4
+// difference), detT, K2, K3 -- bit for bit rt_tri_const's.
+__device__ __forceinline__ RtTri rt_tri_frame(const RtGeo &g, const float camf[4])
+{
+    const vec3 e1 = v3(g.e1x, g.e1y, g.e1z), e2 = v3(g.e2x, g.e2y, g.e2z);
+    const vec3 s = v3(camf[0] - g.v0x, camf[1] - g.v0y, camf[2] - g.v0z);
+    RtTri r;
+    r.e1x = e1.x; r.e1y = e1.y; r.e1z = e1.z;
+    r.e2x = e2.x; r.e2y = e2.y; r.e2z = e2.z;
+    r.sx = s.x; r.sy = s.y; r.sz = s.z;
+    r.detT = det3(s, e1, e2);                                          // :305-306
+    r.K1 = g.K1;
+    r.K2 = s.y * e2.z - e2.y * s.z;
+    r.K3 = e1.y * s.z - s.y * e1.z;
+    r.v0x = g.v0x; r.v0y = g.v0y; r.v0z = g.v0z;
+    return r;
+}
+
+// Per-frame RtTri of triangle i (one thread; the small scenes' certificate launch).
+__device__ __forceinline__ void prep_tri(const RtGeo *__restrict__ geo, int n, int i, int frame, const float camf[4],
+                                         RtTri *__restrict__ out)
+{
+    if (i >= n) return;
+    out[(size_t)frame * n + i] = rt_tri_frame(geo[i], camf);
+}
+
+// Per-frame RtTri of the 256 triangles of block blk, staged through LDS so
+// that both streams are coalesced 16-byte accesses: the block's 256 x 48 B of
+// RtGeo are read as 768 consecutive float4s (3 per thread), each thread forms
+// its triangle's RtTri into LDS, and the block's 256 x 64 B go out as 1024
+// consecutive float4s (4 per thread).  A pure streaming pass (C5: 1M
+// triangles, 48 MB in, 64 MB out per frame).
+__device__ __forceinline__ void prep_block(const RtGeo *__restrict__ geo, int n, int blk, int frame,
+                                           const float camf[4], RtTri *__restrict__ out)
+{
+    __shared__ float4 s_buf[kRtThreads * 4];     // 16 KB: RtGeo in (12 KB), then RtTri out
+    const int t = threadIdx.x, i0 = blk * kRtThreads, cnt = min(kRtThreads, n - i0);
+    const float4 *src = reinterpret_cast<const float4 *>(geo + i0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int q = t + k * kRtThreads;
+        if (q < 3 * cnt) s_buf[q] = src[q];
+    }
+    __syncthreads();
+    RtTri r{};
+    if (t < cnt) {
+        const float4 a = s_buf[3 * t], b = s_buf[3 * t + 1], c = s_buf[3 * t + 2];
+        RtGeo g;
+        g.e1x = a.x; g.e1y = a.y; g.e1z = a.z; g.e2x = a.w;
+        g.e2y = b.x; g.e2z = b.y; g.v0x = b.z; g.v0y = b.w;
+        g.v0z = c.x; g.K1 = c.y; g.pad0 = c.z; g.pad1 = c.w;
+        r = rt_tri_frame(g, camf);
+    }
+    __syncthreads();
+    if (t < cnt) {
+        s_buf[4 * t] = make_float4(r.e1x, r.e1y, r.e1z, r.e2x);
+        s_buf[4 * t + 1] = make_float4(r.e2y, r.e2z, r.sx, r.sy);
+        s_buf[4 * t + 2] = make_float4(r.sz, r.detT, r.K1, r.K2);
+        s_buf[4 * t + 3] = make_float4(r.K3, r.v0x, r.v0y, r.v0z);
+    }
+    __syncthreads();
+    float4 *dst = reinterpret_cast<float4 *>(out + (size_t)frame * n + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = t + k * kRtThreads;
+        if (q < 4 * cnt) dst[q] = s_buf[q];
     }
 }
 
-__global__ void rt_prepare_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
-                                  RtTri *__restrict__ out, RtShade *__restrict__ shade, int n_prep_blocks,
-                                  RtFrame F, const RtSphere *__restrict__ sph,
-                                  unsigned long long *__restrict__ lat_masks, int sup)
+__global__ __launch_bounds__(kRtThreads) void rt_prepare_kernel(const cg_tri *__restrict__ tris,
+                                                                const RtGeo *__restrict__ geo, int n, RtFrameCams cams,
+                                                                RtTri *__restrict__ out, int n_prep_blocks,
+                                                                RtFrame F, const RtSphere *__restrict__ sph,
+                                                                unsigned long long *__restrict__ lat_masks, int sup)
 {
     const int frame = blockIdx.y;
     const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
     if ((int)blockIdx.x < n_prep_blocks) {
-        prep_tri(tris, n, blockIdx.x * blockDim.x + threadIdx.x, frame, camf, out, shade);
+        prep_block(geo, n, blockIdx.x, frame, camf, out);
         return;
     }
     // Unit certificates: lpt lanes per unit (lane k = triangle k; the last lane
@@ -377,11 +454,12 @@ __device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int c
 // masks round-trip through memory and no second dependent launch.
 __device__ __forceinline__ void lat_flatten(const LatFlatten &Z);   // below, with the lattice kernel
 
-__global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris, int n, RtFrameCams cams,
+__global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris,
+                                                           const RtGeo *__restrict__ geo, int n, RtFrameCams cams,
                                                            RtFrame F, const RtSphere *__restrict__ sph,
                                                            const unsigned long long *__restrict__ sup_masks,
                                                            unsigned long long *__restrict__ lat_masks,
-                                                           RtTri *__restrict__ tc_out, RtShade *__restrict__ shade_out,
+                                                           RtTri *__restrict__ tc_out,
                                                            int n_prep_blocks, int frame_fast, LatFlatten Z)
 {
     constexpr int kT = kSup * kSup;
@@ -392,7 +470,7 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
     const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     const float camf[4] = {cams.c[frame][0], cams.c[frame][1], cams.c[frame][2], cams.c[frame][3]};
     if (blk < n_prep_blocks) {
-        prep_tri(tris, n, blk * blockDim.x + threadIdx.x, frame, camf, tc_out, shade_out);
+        prep_tri(geo, n, blk * blockDim.x + threadIdx.x, frame, camf, tc_out);
         // the first block (dispatched first) also sorts the lattice launch's order
         if (Z.n > 0 && blk == 0 && frame == 0) lat_flatten(Z);
         return;
@@ -1792,10 +1870,19 @@ static int env_int(const char *name, int dflt)
     return e && *e ? std::atoi(e) : dflt;
 }
 
+// Once per scene (cg_rt_set_scene): RtGeo + RtShade of every triangle.
+hipError_t launch_rt_scene(const cg_tri *d_tris, int n, RtGeo *d_geo, RtShade *d_shade, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rt_scene_kernel, dim3((n + kRtThreads - 1) / kRtThreads), dim3(kRtThreads), 0, st, d_tris, n,
+                       d_geo, d_shade);
+    return hipGetLastError();
+}
+
 // Z (optional): a measured lattice order to sort in the fused certificate
 // launch; on return Z->n < 0 iff it was (the other certificate paths skip it).
-hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cams, int nframes, RtTri *d_tc,
-                             RtShade *d_shade, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
+hipError_t launch_rt_prepare(const cg_tri *d_tris, const RtGeo *d_geo, int n, const RtFrameCams &cams, int nframes,
+                             RtTri *d_tc, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
                              unsigned long long *d_lat_masks, unsigned long long *d_sup_masks, LatFlatten *Z)
 {
     if (n <= 0) return hipSuccess;
@@ -1845,8 +1932,8 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
             const int kt_id = KT_RT_TILE_CERT;
             const int ff = tprep + units_w <= 65535;
             const dim3 cg = ff ? dim3(nframes, tprep + units_w) : dim3(tprep + units_w, nframes);
-            kt_launch(kt_id, rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, n, cams, Fl, d_sph,
-                               (const unsigned long long *)nullptr, d_lat_masks, d_tc, d_shade, tprep, ff,
+            kt_launch(kt_id, rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, d_geo, n, cams, Fl, d_sph,
+                               (const unsigned long long *)nullptr, d_lat_masks, d_tc, tprep, ff,
                                Z ? *Z : LatFlatten{});
             if (Z) Z->n = -Z->n;   // done (the caller's flag: the lattice launch may use the order)
             return hipGetLastError();
@@ -1857,16 +1944,16 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
         {
             const int kt_id = KT_RT_PREPARE;
-            kt_launch(kt_id, rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
-                               d_tc, d_shade, prep, Fl, d_sph, d_sup_masks, 1);
+            kt_launch(kt_id, rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, d_geo, n,
+                               cams, d_tc, prep, Fl, d_sph, d_sup_masks, 1);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         const int kt_id = KT_RT_TILE_CERT;
         const int ff = units <= 65535;
         kt_launch(kt_id, rt_tile_cert_kernel, ff ? dim3(nframes, units) : dim3(units, nframes), dim3(tthreads), 0, st,
-                           d_tris, n, cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks,
-                           (RtTri *)nullptr, (RtShade *)nullptr, 0, ff, LatFlatten{});
+                           d_tris, d_geo, n, cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks,
+                           (RtTri *)nullptr, 0, ff, LatFlatten{});
         return hipGetLastError();
     }
     if (F && d_lat_masks) {   // single-level: every tile (of the window) certified by rt_prepare_kernel
@@ -1876,8 +1963,8 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, int n, const RtFrameCams &cam
         cert = (units + tpw * (threads / 64) - 1) / (tpw * (threads / 64));
     }
     const int kt_id = KT_RT_PREPARE;
-    kt_launch(kt_id, rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, n, cams,
-                       d_tc, d_shade, prep, Fl, d_sph, d_lat_masks, 0);
+    kt_launch(kt_id, rt_prepare_kernel, dim3(prep + cert, nframes), dim3(threads), 0, st, d_tris, d_geo, n, cams,
+                       d_tc, prep, Fl, d_sph, d_lat_masks, 0);
     return hipGetLastError();
 }
 

@@ -20,9 +20,11 @@
 #include "cg_rast_dev.h"
 
 namespace cg {
-hipError_t launch_rt_prepare(const cg_tri *, int, const RtFrameCams &, int, RtTri *, RtShade *, hipStream_t,
+hipError_t launch_rt_prepare(const cg_tri *, const RtGeo *, int, const RtFrameCams &, int, RtTri *, hipStream_t,
                              const RtFrame *, const RtSphere *, unsigned long long *, unsigned long long *,
                              LatFlatten * = nullptr);
+hipError_t launch_rt_scene(const cg_tri *, int, RtGeo *, RtShade *, hipStream_t);
+hipError_t rt_render_brute(const RtFrame &, const cg_tri *, int, const RtSphere *, int, int, uint32_t *, hipStream_t);
 size_t rt_sup_units(const RtFrame &);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                     const unsigned long long *, const unsigned long long *, const RtFrameCams &,
@@ -183,7 +185,7 @@ struct cg_ctx {
     // RT scene
     int n_tris = -1, n_sph = 0;
     float nbound = 0.f;   // largest |normal component| of the scene (shadow certificate)
-    DevBuf tris, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
+    DevBuf tris, geo, tc, shade, sph, frame, probe_a, probe_b, probe_c, probe_d, lights, big, gstart, gtris;
     DevBuf latmask;                     // lattice tiles' certificates (two masks per tile)
     DevBuf supmask;                     // their super-tiles' certificates (two-level path)
     DevBuf umask;                       // light sets: the tiles' per-unit shadow masks
@@ -193,7 +195,7 @@ struct cg_ctx {
     hipStream_t aux = nullptr;
     hipEvent_t ev_cert[2] = {nullptr, nullptr}, ev_lat[2] = {nullptr, nullptr};
     int slot = 0;
-    DevBuf ptc[2], pshade[2], plat[2], psup[2], pumask[2];
+    DevBuf ptc[2], plat[2], psup[2], pumask[2];
     // measured lattice order (LatOrder, cg_internal.h): per slot, the recording
     // of its last lattice launch (class per tile) and the order sorted for it
     DevBuf lcost[2], lflat[2];
@@ -226,7 +228,7 @@ struct cg_ctx {
     // each other's gaps.
     static constexpr int kBigSlots = 4;
     struct ExtraSlot {
-        DevBuf tc, shade, big, frame;
+        DevBuf tc, big, frame;
         unsigned long long *demand = nullptr;
         hipEvent_t ev = nullptr, done = nullptr;
         bool ev_live = false;
@@ -381,7 +383,7 @@ extern "C" void cg_destroy(cg_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf *bufs[] = {&c->tris, &c->tc, &c->shade, &c->sph, &c->frame,
+    DevBuf *bufs[] = {&c->tris, &c->geo, &c->tc, &c->shade, &c->sph, &c->frame,
                       &c->probe_a, &c->probe_b, &c->probe_c, &c->probe_d, &c->lights, &c->big,
                       &c->gstart, &c->gtris};
     if (c->big_ev) {
@@ -398,7 +400,7 @@ extern "C" void cg_destroy(cg_ctx *c)
         }
         if (x.done) (void)hipEventDestroy(x.done);
         if (x.demand) (void)hipHostFree(x.demand);
-        x.tc.release(); x.shade.release(); x.big.release(); x.frame.release();
+        x.tc.release(); x.big.release(); x.frame.release();
         if (x.st) (void)hipStreamDestroy(x.st);
     }
     if (c->bev_start) (void)hipEventDestroy(c->bev_start);
@@ -409,7 +411,7 @@ extern "C" void cg_destroy(cg_ctx *c)
     }
     if (c->start_ev) (void)hipEventDestroy(c->start_ev);
     for (int k = 0; k < 2; ++k) {
-        c->ptc[k].release(); c->pshade[k].release(); c->plat[k].release(); c->psup[k].release();
+        c->ptc[k].release(); c->plat[k].release(); c->psup[k].release();
         c->pumask[k].release();
         if (c->ev_cert[k]) (void)hipEventDestroy(c->ev_cert[k]);
         if (c->ev_lat[k]) (void)hipEventDestroy(c->ev_lat[k]);
@@ -440,15 +442,24 @@ extern "C" int cg_rt_set_scene(cg_ctx *c, const cg_tri *tris, int n_tris, const 
     if (!c || n_tris < 0 || n_spheres < 0 || (n_tris && !tris) || (n_spheres && !spheres))
         return CG_E_INVALID;
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    // frames still in flight on the caller's, auxiliary or slot streams read the
+    // scene buffers rewritten below (triangles, RtGeo, RtShade): let them finish
+    CG_TRY(c, hipDeviceSynchronize(), "scene change");
     ++c->rt_scene_gen;
     size_t nt = n_tris > 0 ? (size_t)n_tris : 1;
     CG_TRY(c, c->tris.ensure(nt * sizeof(cg_tri)), "alloc tris");
     CG_TRY(c, c->tc.ensure(nt * sizeof(RtTri)), "alloc tri constants");
     CG_TRY(c, c->shade.ensure(nt * sizeof(RtShade)), "alloc tri shading");
+    CG_TRY(c, c->geo.ensure(nt * sizeof(RtGeo)), "alloc tri geometry");
     CG_TRY(c, c->sph.ensure((size_t)(n_spheres > 0 ? n_spheres : 1) * sizeof(RtSphere)), "alloc spheres");
-    if (n_tris)
+    if (n_tris) {
         CG_TRY(c, hipMemcpyAsync(c->tris.p, tris, (size_t)n_tris * sizeof(cg_tri),
                                  hipMemcpyHostToDevice, c->stream), "upload tris");
+        // the camera-independent constants (RtGeo) and shading attributes
+        // (RtShade), once per scene: every frame, slot and path reads them
+        CG_TRY(c, launch_rt_scene((const cg_tri *)c->tris.p, n_tris, (RtGeo *)c->geo.p, (RtShade *)c->shade.p,
+                                  c->stream), "rt_scene launch");
+    }
     std::vector<RtSphere> S((size_t)n_spheres);
     for (int i = 0; i < n_spheres; ++i) {
         S[i] = RtSphere{spheres[i].centre.x, spheres[i].centre.y, spheres[i].centre.z,
@@ -613,6 +624,23 @@ static int fill_frame(cg_ctx *c, const cg_light *lights, int n_lights, const cg_
     return set_lights(c, lights, n_lights, st, F);
 }
 
+// Test hook: rows row0 .. row0 + rows - 1 of the frame by
+// the reference's loop with no acceleration (cg_rt_brute.hip), synchronous.
+extern "C" int cg_rt_render_brute_device(cg_ctx *c, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                                         int row0, int rows, uint32_t *d_out, void *stream)
+{
+    if (!c || !d_out || !cam || row0 < 0 || rows <= 0 || row0 + rows > cam->height || n_lights > 64)
+        return CG_E_INVALID;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    RtFrame F;
+    int rc = fill_frame(c, lights, n_lights, cam, nullptr, st, F);
+    if (rc) return rc;
+    CG_TRY(c, rt_render_brute(F, (const cg_tri *)c->tris.p, c->n_tris, (const RtSphere *)c->sph.p, row0, rows, d_out,
+                              st),
+           "brute-force render");
+    return CG_OK;
+}
+
 extern "C" int cg_rt_route(const cg_rt_camera *cam, int n_tris, int n_spheres, int n_lights, const cg_rt_shard *shard)
 {
     if (!cam || cam->width <= 0 || cam->height <= 0 || n_tris < 0 || n_spheres < 0 || n_lights < 0 ||
@@ -637,7 +665,7 @@ extern "C" int cg_rt_route(const cg_rt_camera *cam, int n_tris, int n_spheres, i
 // A large-scene frame slot's buffers (slot 0: the context's own; slot 1: the
 // second frame in flight of rt_render_frames).
 struct BigSlot {
-    DevBuf *tc, *shade, *big, *frame;
+    DevBuf *tc, *big, *frame;
     unsigned long long **demand;
     hipEvent_t *ev;
     bool *ev_live;
@@ -646,9 +674,9 @@ static BigSlot big_slot(cg_ctx *c, int q)
 {
     if (q) {
         cg_ctx::ExtraSlot &x = c->xs[q - 1];
-        return BigSlot{&x.tc, &x.shade, &x.big, &x.frame, &x.demand, &x.ev, &x.ev_live};
+        return BigSlot{&x.tc, &x.big, &x.frame, &x.demand, &x.ev, &x.ev_live};
     }
-    return BigSlot{&c->tc, &c->shade, &c->big, &c->frame, &c->big_demand, &c->big_ev, &c->big_ev_live};
+    return BigSlot{&c->tc, &c->big, &c->frame, &c->big_demand, &c->big_ev, &c->big_ev_live};
 }
 
 static bool big_observe(cg_ctx *c, bool sizing, int q);
@@ -807,7 +835,7 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
             big.release();
         }
         CG_TRY(c, big.ensure(need), "alloc large-scene scratch");
-        CG_TRY(c, launch_rt_big(F, (const RtTri *)S.tc->p, (const RtShade *)S.shade->p, (const RtSphere *)c->sph.p,
+        CG_TRY(c, launch_rt_big(F, (const RtTri *)S.tc->p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
                                 c->grid, big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap, c->big_caps,
                                 *S.demand, dry),
                "rt_big launch");
@@ -850,10 +878,9 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
     if (slot) {
         const size_t nt = (size_t)std::max(c->n_tris, 1);
         CG_TRY(c, S.tc->ensure(nt * sizeof(RtTri)), "alloc tri constants");
-        CG_TRY(c, S.shade->ensure(nt * sizeof(RtShade)), "alloc tri shading");
     }
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, cams, 1, (RtTri *)S.tc->p,
-                                (RtShade *)S.shade->p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, (const RtGeo *)c->geo.p, c->n_tris, cams, 1,
+                                (RtTri *)S.tc->p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
     if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st, slot);
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                (const RtSphere *)c->sph.p, lat, um, d_out, st), "rt_pixel launch");
@@ -973,7 +1000,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     // calls ago, ev_lat[k])
     const int k = c->slot;
     c->slot ^= 1;
-    DevBuf &btc = c->ptc[k], &bsh = c->pshade[k], &blat = c->plat[k], &bsup = c->psup[k], &bum = c->pumask[k];
+    DevBuf &btc = c->ptc[k], &blat = c->plat[k], &bsup = c->psup[k], &bum = c->pumask[k];
     const size_t tiles = rt_lattice_tiles(F);
     // Both slots' certificate buffers are sized together, for a full batch
     // (kMaxFrameBatch frames): a call never allocates -- hipMalloc / hipFree,
@@ -987,7 +1014,6 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     for (int q = 0; q < 2; ++q) {
         CG_TRY(c, c->plat[q].ensure(nfa * tiles * 2 * sizeof(unsigned long long)), "alloc lattice masks");
         CG_TRY(c, c->ptc[q].ensure(nfa * std::max(F.n_tris, 1) * sizeof(RtTri)), "alloc tri constants");
-        CG_TRY(c, c->pshade[q].ensure((size_t)std::max(F.n_tris, 1) * sizeof(RtShade)), "alloc tri shading");
         CG_TRY(c, c->psup[q].ensure(nfa * rt_sup_units(F) * 2 * sizeof(unsigned long long)), "alloc super-tile masks");
     }
     if (rt_lattice_unit_bytes(F, nf)) {
@@ -1032,8 +1058,8 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
         const int src = (cold && c->lrec_key[k ^ 1] == key) ? (k ^ 1) : c->lrec_key[k] == key ? k : -1;
         if (src >= 0) flat = LatFlatten{(const uint8_t *)c->lcost[src].p, (uint32_t *)c->lflat[k].p, gx * gy};
     }
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, fc, nf, (RtTri *)btc.p,
-                                (RtShade *)bsh.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm,
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, (const RtGeo *)c->geo.p, c->n_tris, fc, nf,
+                                (RtTri *)btc.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm,
                                 flat.n > 0 ? &flat : nullptr),
            "rt_prepare launch");
     if (ordered) {
@@ -1053,7 +1079,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     unsigned long long *um = nullptr;
     if (rt_lattice_unit_bytes(F, nf)) {
         um = (unsigned long long *)bum.p;
-        CG_TRY(c, launch_rt_lattice_units(F, (const RtTri *)btc.p, (const RtShade *)bsh.p, (const RtSphere *)c->sph.p,
+        CG_TRY(c, launch_rt_lattice_units(F, (const RtTri *)btc.p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
                                           lat, fc, nf, um, cst),
                "rt_lattice_units launch");
     }
@@ -1061,7 +1087,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
         CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
         CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
     }
-    CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)bsh.p,
+    CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)c->shade.p,
                                        (const RtSphere *)c->sph.p, lat, um, fc, nf, stride, (uint32_t *)d_out, st,
                                        d_done, ordered ? &order : nullptr),
            "rt_lattice launch");
@@ -1494,8 +1520,8 @@ extern "C" int cg_rt_probe_direct_light(cg_ctx *c, const cg_isect *isects, const
     // except s/detT/K2/K3, which the shadow path does not read.
     RtFrameCams zero{};
     zero.c[0][3] = 1.0f;
-    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, c->n_tris, zero, 1, (RtTri *)c->tc.p,
-                                (RtShade *)c->shade.p, c->stream, nullptr, nullptr, nullptr, nullptr), "prepare");
+    CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, (const RtGeo *)c->geo.p, c->n_tris, zero, 1,
+                                (RtTri *)c->tc.p, c->stream, nullptr, nullptr, nullptr, nullptr), "prepare");
     CG_TRY(c, c->probe_c.ensure((size_t)n * sizeof(cg_isect)), "alloc");
     CG_TRY(c, c->probe_a.ensure((size_t)n * sizeof(cg_vec3) + 16), "alloc");
     CG_TRY(c, hipMemcpyAsync(c->probe_c.p, isects, (size_t)n * sizeof(cg_isect), hipMemcpyHostToDevice, c->stream), "h2d");

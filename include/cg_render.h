@@ -247,6 +247,15 @@ int cg_rt_pool_demand(cg_ctx *ctx, uint64_t *out);
  * many-light shadow and bucketed lists; all 0 = automatic sizing).  Lists past a capacity take the fallback over every triangle; the
  * image is the same. */
 int cg_rt_set_pool_caps(cg_ctx *ctx, long long sup, long long bin, long long sbin, long long sorted);
+/* Test hook, a defect detector for the certificate machinery (never a product
+ * path): rows row0 .. row0 + rows - 1 of the camera's frame (rows x width
+ * pixels into d_out, device memory) by the reference's own loop with no
+ * acceleration at all -- every sub-ray against every triangle and sphere, every
+ * shadow ray against every triangle and sphere until its first blocker
+ * (raytracer/Source/skeleton.cpp:120-166, 263-415).  Synchronous; at most 64
+ * lights.  C5 at 1080p: tens of seconds on one MI355X. */
+int cg_rt_render_brute_device(cg_ctx *ctx, const cg_light *lights, int n_lights, const cg_rt_camera *cam,
+                              int row0, int rows, uint32_t *d_out, void *stream);
 
 /* ---- multi-GPU raytracer ------------------------------- */
 /* One process per GPU.  The reference renders every pixel of Draw
