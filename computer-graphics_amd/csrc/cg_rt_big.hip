@@ -429,7 +429,7 @@ __device__ __forceinline__ void bin_append(const bool kept[4], int base, int *li
 // slower super-bin pass.)
 constexpr unsigned long long kProjAll = 0x7fff8000ull | (0x7fff8000ull << 32);
 constexpr unsigned long long kProjNone = 0x80007fffull | (0x80007fffull << 32);   // x0 > x1: meets nothing
-__device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, const cg_tri &T, const float cam[4],
+__device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, const float cam[4],
                                          float f)
 {
     double dmin;
@@ -440,7 +440,7 @@ __device__ unsigned long long proj_box16(const RtTri &c, const PrimDet &pd, cons
     // times the rounding of the dets (1e-3 .. 1e-2 for C5's small triangles)
     const double sig = 2.0 * (pd.Ed + pd.Eu + pd.Ev) / dmin + 0x1p-21;
     if (!(isfinite(sig) && sig < 4.0)) return kProjAll;   // exact bound for any slack; a wide box still prunes
-    const double v0[3] = {(double)T.v0.x, (double)T.v0.y, (double)T.v0.z};
+    const double v0[3] = {(double)c.v0x, (double)c.v0y, (double)c.v0z};   // the Triangle's v0, as RtTri keeps it
     const double a1[3] = {(double)c.e1x, (double)c.e1y, (double)c.e1z}, a2[3] = {(double)c.e2x, (double)c.e2y, (double)c.e2z};
     double lo[3], hi[3];
     for (int k = 0; k < 3; ++k) {
@@ -602,8 +602,8 @@ __host__ __device__ __forceinline__ int sup_groups(int nsup) { return max(4, (ns
 #ifndef CG_SUP_WAVES
 #define CG_SUP_WAVES 3   // 168 VGPRs; 2 waves (182) 562 us, 4 waves (136 B scratch) 468, 3: 452 (C5, one frame; r05)
 #endif
-__global__ __launch_bounds__(256, CG_SUP_WAVES) void rt_sup_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
-                                                             const cg_tri *__restrict__ tris, BigBufs B)
+__global__ __launch_bounds__(256, CG_SUP_WAVES) void rt_sup_primary_kernel(RtFrame F, const RtGeo *__restrict__ geo,
+                                                             RtTri *__restrict__ tc_out, BigBufs B)
 {
     __shared__ float s_sb[kSupGroup][4];         // the group's super-bin bundles (x0 > x1: no pixel)
     __shared__ int s_cnt[kSupGroup][4][4];       // kept per (super-bin, triangle slot r, wave)
@@ -646,16 +646,24 @@ __global__ __launch_bounds__(256, CG_SUP_WAVES) void rt_sup_primary_kernel(RtFra
             pbc[r][0] = pbc[r][1] = kProjAll;
             const int i = base + r * 256 + (int)threadIdx.x;
             // (bundle_mask answers ~0 when its error terms are not finite: every valid bundle is tested)
+            // the frame's RtTri of triangle i, formed here from the scene's RtGeo (rt_tri_frame,
+            // bit for bit rt_tri_const) and published by the first group's workgroups for the
+            // later passes -- no separate prepare launch for large scenes
+            RtTri c{};
+            if (i < F.n_tris) {
+                c = rt_tri_frame(geo[i], F.cam);
+                if (blockIdx.y == 0) tc_out[i] = c;
+            }
             unsigned long long m = (i < F.n_tris && valid)
-                                       ? bundle_mask(tc[i], s_sb, ng, ex0, ex1, ey0, ey1, F.focal) & valid : 0ull;
+                                       ? bundle_mask(c, s_sb, ng, ex0, ex1, ey0, ey1, F.focal) & valid : 0ull;
             unsigned long long kept = 0ull;
             while (m) {
                 const int k = __builtin_ctzll(m);
                 m &= m - 1ull;
                 const float x0 = s_sb[k][0], x1 = s_sb[k][1], y0 = s_sb[k][2], y1 = s_sb[k][3];
                 PrimDet pd;
-                if (!cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd)) {
-                    const unsigned long long pb = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                if (!cull_primary(c, x0, x1, y0, y1, F.focal, &pd)) {
+                    const unsigned long long pb = proj_box16(c, pd, F.cam, F.focal);
                     if (proj_meets(pb, x0, x1, y0, y1)) {
                         if (kc[r][0] < 0) {
                             kc[r][0] = k;
@@ -707,9 +715,10 @@ __global__ __launch_bounds__(256, CG_SUP_WAVES) void rt_sup_primary_kernel(RtFra
                     } else if (kc[r][1] == k) {
                         pb = pbc[r][1];
                     } else {   // a third or later kept super-bin: the same box again
+                        const RtTri c = rt_tri_frame(geo[i], F.cam);
                         PrimDet pd;
-                        (void)cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
-                        pb = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                        (void)cull_primary(c, x0, x1, y0, y1, F.focal, &pd);
+                        pb = proj_box16(c, pd, F.cam, F.focal);
                     }
                     const int at = off + before + __popcll(b & lt);
                     B.sup_pool[at] = i;
@@ -852,7 +861,7 @@ __device__ void bin_certify_batch(const RtFrame &F, const RtTri *__restrict__ tc
             PrimDet pd;
             kept[r] = !cull_primary(tc[i], x0, x1, y0, y1, F.focal, &pd);
             if (kept[r]) {
-                unsigned long long b = proj_box16(tc[i], pd, tris[i], F.cam, F.focal);
+                unsigned long long b = proj_box16(tc[i], pd, F.cam, F.focal);
                 if (b == kProjAll && !is_bin_mask(sb)) b = sb;
                 kept[r] = proj_meets(b, x0, x1, y0, y1);
                 pbox[r] = b;
@@ -1054,7 +1063,7 @@ __global__ __launch_bounds__(256, 4) void rt_bin_count_kernel(RtFrame F, const R
                 PrimDet ph;
                 pb[h] = kProjNone;
                 if (hv[h] && !cull_primary(tc[i], hx0[h], hx1[h], hy0[h], hy1[h], F.focal, &ph))
-                    pb[h] = proj_box16(tc[i], ph, tris[i], F.cam, F.focal);
+                    pb[h] = proj_box16(tc[i], ph, F.cam, F.focal);
             }
         }
         B.flat_ent[d] = ent;
@@ -2482,8 +2491,9 @@ static void lit_bounds(BigBufs &B, const RtFrame &F, const RtGrid &G)
     B.lit_M = 0.25f * G.h;
 }
 
-hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
-                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const cg_tri *d_tris,
+hipError_t launch_rt_big(const RtFrame &F, RtTri *d_tc, const RtShade *d_shade, const RtSphere *d_sph,
+                         const RtGrid &grid, void *scratch, uint32_t *d_out, hipStream_t st, const RtGeo *d_geo,
+                         const cg_tri *d_tris,
                          int pend_cap, const BigCaps &caps, unsigned long long *h_demand, int dry)
 {
     BigBufs B = big_layout(F, caps);
@@ -2499,8 +2509,9 @@ hipError_t launch_rt_big(const RtFrame &F, const RtTri *d_tc, const RtShade *d_s
     const bool flags_fit = lat || 9 * F.n_lights <= 64;
     const dim3 bgrid((F.n_tris + kBinTris - 1) / kBinTris, bins);
     const dim3 pgrid((F.W + kRtTileW - 1) / kRtTileW, (F.rows_out + kRtTileH - 1) / kRtTileH);
+    // the first pass also writes the frame's RtTri (rt_sup_primary_kernel)
     hipLaunchKernelGGL(rt_sup_primary_kernel, dim3(bgrid.x, sup_groups(B.sups_x * B.sups_y)), dim3(256), 0, st, F,
-                       d_tc, d_tris, B);
+                       d_geo, d_tc, B);
     const int sups = B.sups_x * B.sups_y;
     hipLaunchKernelGGL(rt_chunk_scan_kernel, dim3(sups), dim3(1024), 0, st, B.sup_chunk, nullptr, B.nch, B.sup_pre,
                        B.sup_tot);

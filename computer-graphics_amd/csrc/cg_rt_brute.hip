@@ -29,7 +29,19 @@ namespace cg {
 
 namespace {
 
-constexpr int kBruteRows = 8;      // pixel rows per launch
+constexpr int kBruteRows = 32;     // pixel rows per launch (8,640 waves: enough to hide the scalar loads)
+
+// A triangle's values that do not depend on the lane's ray, formed with the
+// reference's own float ops (skeleton.cpp:283-306): e1 = v1 - v0, e2 = v2 - v0,
+// s = cameraPos - v0, detT = det(s, e1, e2), and K1 = e1.y*e2.z - e2.y*e1.z --
+// the first cofactor det3(-d, e1, e2) forms, the same operands and op for
+// every ray.  64 B: one s_load_dwordx16 per triangle in the loops below.
+struct alignas(16) BruteTri {
+    float e1x, e1y, e1z, e2x;
+    float e2y, e2z, v0x, v0y;
+    float v0z, K1, sx, sy;
+    float sz, detT, pad0, pad1;
+};
 
 // One sub-ray's closest hit: tri >= 0 a triangle, tri = -1 - k sphere k, tri =
 // INT_MIN none.
@@ -89,9 +101,35 @@ __device__ vec3 brute_dir(const RtFrame &F, int u, int v, int k)
     return v3(d.x + (0.5f * (float)i), d.y + (0.5f * (float)j), F.focal);
 }
 
+__global__ void rt_brute_tri_kernel(RtFrame F, const cg_tri *__restrict__ tris, int n, BruteTri *__restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const cg_tri T = tris[i];
+    const vec3 e1 = v3(T.v1.x - T.v0.x, T.v1.y - T.v0.y, T.v1.z - T.v0.z);   // :283
+    const vec3 e2 = v3(T.v2.x - T.v0.x, T.v2.y - T.v0.y, T.v2.z - T.v0.z);   // :284
+    const vec3 s = v3(F.cam[0] - T.v0.x, F.cam[1] - T.v0.y, F.cam[2] - T.v0.z);   // :296-297
+    BruteTri b;
+    b.e1x = e1.x; b.e1y = e1.y; b.e1z = e1.z; b.e2x = e2.x;
+    b.e2y = e2.y; b.e2z = e2.z; b.v0x = T.v0.x; b.v0y = T.v0.y;
+    b.v0z = T.v0.z; b.K1 = e1.y * e2.z - e2.y * e1.z; b.sx = s.x; b.sy = s.y;
+    b.sz = s.z; b.detT = det3(s, e1, e2); b.pad0 = 0.f; b.pad1 = 0.f;   // :305-306
+    out[i] = b;
+}
+
+// det3(-d, e1, e2) (glm determinant, cg_math.h det3) with its first cofactor K1 precomputed:
+// (c0.x*K1 - c1.x*(c0.y*c2.z - c2.y*c0.z)) + c2.x*(c0.y*c1.z - c1.y*c0.z), c0 = -d.
+__device__ __forceinline__ float brute_det(const BruteTri &b, vec3 nd)
+{
+    const float a = nd.x * b.K1;
+    const float q = b.e1x * (nd.y * b.e2z - b.e2y * nd.z);
+    const float c = b.e2x * (nd.y * b.e1z - b.e1y * nd.z);
+    return (a - q) + c;
+}
+
 // Primary rays: rows row0 .. row0 + rows - 1, one lane per sub-ray, every
 // triangle (wave-uniform, scalar loads) then every sphere.
-__global__ __launch_bounds__(256) void rt_brute_primary_kernel(RtFrame F, const cg_tri *__restrict__ tris, int n,
+__global__ __launch_bounds__(256) void rt_brute_primary_kernel(RtFrame F, const BruteTri *__restrict__ bt, int n,
                                                              const RtSphere *__restrict__ sph, int row0, int rows,
                                                              BruteHit *__restrict__ hits)
 {
@@ -105,23 +143,25 @@ __global__ __launch_bounds__(256) void rt_brute_primary_kernel(RtFrame F, const 
     const float len = length(dir);
     float best = FLT_MAX;
     int idx = INT_MIN;
-    vec3 pos = v3(0.f, 0.f, 0.f);
+    float tb = 0.f;
     for (int i = 0; i < n; ++i) {
-        const cg_tri T = tris[i];
-        const vec3 e1 = v3(T.v1.x - T.v0.x, T.v1.y - T.v0.y, T.v1.z - T.v0.z);
-        const vec3 e2 = v3(T.v2.x - T.v0.x, T.v2.y - T.v0.y, T.v2.z - T.v0.z);
-        const vec3 s = v3(start.x - T.v0.x, start.y - T.v0.y, start.z - T.v0.z);
-        const float det = det3(ndir, e1, e2);
-        const float t = det3(s, e1, e2) / det;
-        const float d = t * len;
-        if (d < 0.0f || d >= best || d > FLT_MAX) continue;     // :311-313
-        const float uu = det3(ndir, s, e2) / det, vv = det3(ndir, e1, s) / det;
-        if (uu >= 0 && vv >= 0 && (uu + vv) <= 1) {             // :328
+        const BruteTri b = bt[i];                                 // wave-uniform: scalar loads
+        const float det = brute_det(b, ndir);                     // :289, :306
+        const float t = b.detT / det;                             // :305-306
+        const float d = t * len;                                  // :307
+        if (d < 0.0f || d >= best || d > FLT_MAX) continue;       // :311-313
+        const vec3 e1 = v3(b.e1x, b.e1y, b.e1z), e2 = v3(b.e2x, b.e2y, b.e2z), s = v3(b.sx, b.sy, b.sz);
+        const float uu = det3(ndir, s, e2) / det, vv = det3(ndir, e1, s) / det;   // :317-321
+        if (uu >= 0 && vv >= 0 && (uu + vv) <= 1) {               // :328
             best = d;
             idx = i;
-            const vec3 td = dir * t;
-            pos = v3(start.x + td.x, start.y + td.y, start.z + td.z);
+            tb = t;
         }
+    }
+    vec3 pos = v3(0.f, 0.f, 0.f);
+    if (idx >= 0) {                                               // :326 position = start + t * dir
+        const vec3 td = dir * tb;
+        pos = v3(start.x + td.x, start.y + td.y, start.z + td.z);
     }
     for (int q = 0; q < F.n_sph; ++q) {
         float t;
@@ -161,7 +201,8 @@ __device__ float brute_rmag(vec3 r)
 // Shadow rays of light l: one lane per sub-ray; blocked[g] = 1 when the
 // reference's shadow test (:394-396) darkens it.  Every triangle in index
 // order until the whole wave has found a blocker, then every sphere.
-__global__ __launch_bounds__(256) void rt_brute_shadow_kernel(RtFrame F, const cg_tri *__restrict__ tris, int n,
+__global__ __launch_bounds__(256) void rt_brute_shadow_kernel(RtFrame F, const cg_tri *__restrict__ tris,
+                                                            const BruteTri *__restrict__ bt, int n,
                                                             const RtSphere *__restrict__ sph, long long total,
                                                             const BruteHit *__restrict__ hits, int l,
                                                             uint8_t *__restrict__ blocked)
@@ -187,12 +228,11 @@ __global__ __launch_bounds__(256) void rt_brute_shadow_kernel(RtFrame F, const c
     bool hit = false;
     for (int i = 0; i < n; ++i) {
         if (__ballot(live && !hit) == 0ull) break;                          // the whole wave decided
+        const BruteTri b = bt[i];                                           // uniform: scalar loads
         if (!live || hit) continue;
-        const cg_tri T = tris[i];
-        const vec3 e1 = v3(T.v1.x - T.v0.x, T.v1.y - T.v0.y, T.v1.z - T.v0.z);
-        const vec3 e2 = v3(T.v2.x - T.v0.x, T.v2.y - T.v0.y, T.v2.z - T.v0.z);
-        const vec3 s = v3(o.x - T.v0.x, o.y - T.v0.y, o.z - T.v0.z);
-        const float det = det3(ndir, e1, e2);
+        const vec3 e1 = v3(b.e1x, b.e1y, b.e1z), e2 = v3(b.e2x, b.e2y, b.e2z);
+        const vec3 s = v3(o.x - b.v0x, o.y - b.v0y, o.z - b.v0z);            // :296-297
+        const float det = brute_det(b, ndir);
         const float t = det3(s, e1, e2) / det;
         const float d = t * len;
         if (!(d >= 0.0f && d < rmag)) continue;   // a closer accepted hit than the light
@@ -256,16 +296,21 @@ hipError_t rt_render_brute(const RtFrame &F, const cg_tri *d_tris, int n, const 
     const long long per = (long long)kBruteRows * F.W * 9;
     BruteHit *hits = nullptr;
     uint8_t *blocked = nullptr;
+    BruteTri *bt = nullptr;
     hipError_t e = hipMalloc(&hits, per * sizeof(BruteHit));
     if (e == hipSuccess) e = hipMalloc(&blocked, per * (size_t)std::max(F.n_lights, 1));
+    if (e == hipSuccess) e = hipMalloc(&bt, (size_t)std::max(n, 1) * sizeof(BruteTri));
+    if (e == hipSuccess && n > 0)
+        hipLaunchKernelGGL(rt_brute_tri_kernel, dim3((n + 255) / 256), dim3(256), 0, st, F, d_tris, n, bt);
     for (int r = row0; e == hipSuccess && r < row0 + rows; r += kBruteRows) {
         const int nr = std::min(kBruteRows, row0 + rows - r);
         const long long total = (long long)nr * F.W * 9;
         const int blocks = (int)((total + 255) / 256);
-        hipLaunchKernelGGL(rt_brute_primary_kernel, dim3(blocks), dim3(256), 0, st, F, d_tris, n, d_sph, r, nr, hits);
+        hipLaunchKernelGGL(rt_brute_primary_kernel, dim3(blocks), dim3(256), 0, st, F, (const BruteTri *)bt, n, d_sph, r,
+                           nr, hits);
         for (int l = 0; l < F.n_lights; ++l)
-            hipLaunchKernelGGL(rt_brute_shadow_kernel, dim3(blocks), dim3(256), 0, st, F, d_tris, n, d_sph, total,
-                               (const BruteHit *)hits, l, blocked + (size_t)l * total);
+            hipLaunchKernelGGL(rt_brute_shadow_kernel, dim3(blocks), dim3(256), 0, st, F, d_tris, (const BruteTri *)bt, n,
+                               d_sph, total, (const BruteHit *)hits, l, blocked + (size_t)l * total);
         hipLaunchKernelGGL(rt_brute_shade_kernel, dim3((nr * F.W + 255) / 256), dim3(256), 0, st, F, d_tris, d_sph, nr,
                            (const BruteHit *)hits, (const uint8_t *)blocked, total,
                            d_out + (size_t)(r - row0) * F.W);
@@ -274,6 +319,7 @@ hipError_t rt_render_brute(const RtFrame &F, const cg_tri *d_tris, int n, const 
     }
     if (hits) (void)hipFree(hits);
     if (blocked) (void)hipFree(blocked);
+    if (bt) (void)hipFree(bt);
     return e;
 }
 

@@ -10,6 +10,26 @@
 
 namespace cg {
 
+// RtTri of a triangle for rays from camf, from its per-scene RtGeo: s =
+// cameraPos - v0 (skeleton.cpp:296-297, the xyz of rt_tri_const's vec4
+// difference), detT, K2, K3 -- bit for bit rt_tri_const's.
+__device__ __forceinline__ RtTri rt_tri_frame(const RtGeo &g, const float camf[4])
+{
+    const vec3 e1 = v3(g.e1x, g.e1y, g.e1z), e2 = v3(g.e2x, g.e2y, g.e2z);
+    const vec3 s = v3(camf[0] - g.v0x, camf[1] - g.v0y, camf[2] - g.v0z);
+    RtTri r;
+    r.e1x = e1.x; r.e1y = e1.y; r.e1z = e1.z;
+    r.e2x = e2.x; r.e2y = e2.y; r.e2z = e2.z;
+    r.sx = s.x; r.sy = s.y; r.sz = s.z;
+    r.detT = det3(s, e1, e2);                                          // :305-306
+    r.K1 = g.K1;
+    r.K2 = s.y * e2.z - e2.y * s.z;
+    r.K3 = e1.y * s.z - s.y * e1.z;
+    r.v0x = g.v0x; r.v0y = g.v0y; r.v0z = g.v0z;
+    return r;
+}
+
+
 // ---------------------------------------------------------------------------
 // Sphere::intersect + solveQuadratic (raytracer/Source/TestModelH.h:24-66).
 // The start-dependent terms come from the caller: L = start - centre (:48),

@@ -41,8 +41,9 @@ void rt_scene_box(const cg_tri *tris, int n_tris, const cg_sphere *spheres, int 
                   double hi[3]);
 void rt_box_columns(const double lo[3], const double hi[3], const cg_rt_camera *cam, int *col0, int *col1);
 size_t rt_lattice_tiles(const RtFrame &);
-hipError_t launch_rt_big(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
-                         uint32_t *, hipStream_t, const cg_tri *, int, const BigCaps &, unsigned long long *, int);
+hipError_t launch_rt_big(const RtFrame &, RtTri *, const RtShade *, const RtSphere *, const RtGrid &, void *,
+                         uint32_t *, hipStream_t, const RtGeo *, const cg_tri *, int, const BigCaps &,
+                         unsigned long long *, int);
 bool rt_big_shadow_lists(const RtFrame &);
 int rt_big_mode(const RtFrame &);
 bool rt_grid_build(const cg_tri *, int, RtGrid &, std::vector<int> &, std::vector<int> &, size_t);
@@ -835,8 +836,9 @@ static int rt_big_enqueue(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipStrea
             big.release();
         }
         CG_TRY(c, big.ensure(need), "alloc large-scene scratch");
-        CG_TRY(c, launch_rt_big(F, (const RtTri *)S.tc->p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
-                                c->grid, big.p, d_out, st, (const cg_tri *)c->tris.p, c->pend_cap, c->big_caps,
+        CG_TRY(c, launch_rt_big(F, (RtTri *)S.tc->p, (const RtShade *)c->shade.p, (const RtSphere *)c->sph.p,
+                                c->grid, big.p, d_out, st, (const RtGeo *)c->geo.p, (const cg_tri *)c->tris.p,
+                                c->pend_cap, c->big_caps,
                                 *S.demand, dry),
                "rt_big launch");
         CG_TRY(c, hipEventRecord(*S.ev, st), "pool event");
@@ -879,9 +881,10 @@ static int rt_enqueue_kernels(cg_ctx *c, const RtFrame &F, uint32_t *d_out, hipS
         const size_t nt = (size_t)std::max(c->n_tris, 1);
         CG_TRY(c, S.tc->ensure(nt * sizeof(RtTri)), "alloc tri constants");
     }
+    // large scenes: the super-bin pass forms the frame's RtTri itself (no prepare launch)
+    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st, slot);
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, (const RtGeo *)c->geo.p, c->n_tris, cams, 1,
                                 (RtTri *)S.tc->p, st, &F, (const RtSphere *)c->sph.p, lat, supm), "rt_prepare launch");
-    if (F.n_tris > 64 && F.cull_primary && F.cull_shadow) return rt_big_enqueue(c, F, d_out, st, slot);
     CG_TRY(c, launch_rt_pixels(F, (const RtTri *)c->tc.p, (const RtShade *)c->shade.p,
                                (const RtSphere *)c->sph.p, lat, um, d_out, st), "rt_pixel launch");
     return CG_OK;
