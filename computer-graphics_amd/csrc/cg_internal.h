@@ -38,6 +38,35 @@ struct LatOrder {
                              // in groups (cg_dist chunks), every frame of a group at each tile, heavy first; 0: one group
     uint8_t gs[kLatMaxGroups + 1];   // group starts (frames of the launch), gs[ngroups] = frames
 };
+struct RtGeo;
+struct RtTri;
+// Certificates beside the lattice launch instead of before it (one-light
+// lattice, whole-frame calls).  The certificate launch (rt_tile_cert_kernel,
+// on the auxiliary stream, frame-major) publishes each (frame, super-tile)
+// once its 16 tiles' masks and the frame's RtTri are stored: flags[frame *
+// units + super-tile] = gen, an agent-scope release.  A lattice workgroup waits
+// for its super-tile's word (acquire, bounded by `spin` wall-clock ticks) and
+// otherwise -- or with `force`, the test hook -- takes the uncertified path:
+// every triangle and sphere is a candidate for its primary and shadow rays (a
+// certificate only ever removes candidates that cannot change a pixel, so the
+// image is the same) and the workgroup stores the frame's RtTri itself (the
+// same values the certificate launch stores).  flags null: the certificates
+// completed before the launch (stream order), nothing to wait for.
+struct LatReady {
+    const uint32_t *flags;   // [frames][units] publication words of the launch's slot
+    uint32_t gen;            // this call's generation (words are only ever raised)
+    int units, sx;           // super-tiles per frame / per super-tile row
+    int force;               // test hook: every workgroup uncertified
+    uint32_t spin;           // wall-clock ticks (100 MHz) to wait before taking the uncertified path
+    const RtGeo *geo;        // the scene's per-triangle constants (uncertified path)
+    RtTri *tc;               // the launch's RtTri (uncertified path: written by the workgroup)
+};
+struct LatPublish {
+    uint32_t *flags;         // null: no publication (certificates complete before the lattice starts)
+    uint32_t gen;
+    int units;
+    int done;                // out (launch_rt_prepare): 1 when the launch publishes (the fused form)
+};
 struct LatFlatten {
     const uint8_t *cost;     // a recording of the launch's tile geometry
     uint32_t *flat;          // out: its counting sort

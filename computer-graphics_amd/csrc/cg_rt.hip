@@ -441,7 +441,8 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
                                                            const unsigned long long *__restrict__ sup_masks,
                                                            unsigned long long *__restrict__ lat_masks,
                                                            RtTri *__restrict__ tc_out,
-                                                           int n_prep_blocks, int frame_fast, LatFlatten Z)
+                                                           int n_prep_blocks, int frame_fast, LatFlatten Z,
+                                                           LatPublish P)
 {
     constexpr int kT = kSup * kSup;
     // frame_fast: blockIdx.x = frame (dispatched fastest), blockIdx.y = prep block, then
@@ -469,6 +470,10 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
     const int sy = (tiles_y + kSup - 1) / kSup, ud = blk - n_prep_blocks;
     const int uw = (sy - 1 - ud / sxw) * sxw + ud % sxw, unit = (uw / sxw) * sx + s0 + uw % sxw;
     lat_masks += (size_t)frame * tiles_x * tiles_y * 2;
+    // published certificates (LatPublish): the frame's RtTri stored by this workgroup too, so
+    // that a published super-tile implies a complete RtTri (every workgroup of the frame
+    // stores the same values)
+    if (P.flags && wave == 0 && lane < n) tc_out[(size_t)frame * n + lane] = rt_tri_frame(geo[lane], camf);
     __shared__ unsigned long long s_sup[2];
     if (!sup_masks) {
         if (wave == 0) {
@@ -609,6 +614,13 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
             lat_masks[2 * t] = live ? pm : 0ull;
             lat_masks[2 * t + 1] = (live && pm != 0ull) ? (sm | (s_sphsh[tl] ? (1ull << 63) : 0ull)) : 0ull;
         }
+    }
+    if (P.flags) {   // publish: every wave's stores written back, then the word (agent-scope release)
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(P.flags + (size_t)frame * P.units + unit, P.gen, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 #ifdef CG_WG_TIMING
     WGT_STAMP(wt3);
@@ -1047,7 +1059,8 @@ template <int PITCH>
 __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__restrict__ tc,
                                              const RtShade *__restrict__ shade, const RtSphere *__restrict__ sph,
                                              const unsigned long long *__restrict__ lat_masks, const RtFrameCams &cams,
-                                             size_t out_stride, uint32_t *__restrict__ out, const LatSlot &S)
+                                             size_t out_stride, uint32_t *__restrict__ out, const LatSlot &S,
+                                             const LatReady &R)
 {
     const int frame = S.frame;
     RtFrame F = F0;
@@ -1090,12 +1103,50 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     const int step1 = 128;
 #endif
     if (G.u0 + G.nu <= o.wc0 || G.u0 >= o.wc0 + o.pitch) return;   // outside the RGB24 window: whole workgroup
+    // Certificates published beside this launch (LatReady): wait for the tile's
+    // super-tile, or take the uncertified path.
+    bool certified = true;
+    if (R.flags) {
+        __shared__ int s_cert;
+        if (threadIdx.x == 0) {
+            int ok = 0;
+            if (!R.force) {
+                const uint32_t *w = R.flags + (size_t)frame * R.units + (by / kSup) * R.sx + bx / kSup;
+                const unsigned long long t0 = wall_clock64();
+                for (;;) {
+                    const uint32_t v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v == R.gen) {
+                        ok = 1;
+                        break;
+                    }
+                    if (wall_clock64() - t0 > R.spin) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            s_cert = ok;
+        }
+        __syncthreads();
+        certified = s_cert != 0;
+        if (!certified) {   // the frame's RtTri from the scene's constants, as the certificates store it
+            if ((int)threadIdx.x < F.n_tris)
+                R.tc[(size_t)frame * F.n_tris + threadIdx.x] = rt_tri_frame(R.geo[threadIdx.x], F.cam);
+            __threadfence();
+            __syncthreads();
+        }
+        // the loads of the constants and masks below stay after the acquire and the
+        // barrier (fences order them for the compiler as well).  An opaque pointer
+        // here would cost the scalar loads of RtTri (68 -> 80 VGPRs).  Scalar-cache
+        // lines of this frame's RtTri are only ever fetched after a publication (or
+        // this workgroup's own stores), and every RtTri of a frame is stored before
+        // any of its super-tiles is published, so no stale line can be read.
+    }
     // the tile's certificates (rt_prepare_kernel): primary mask (bit 63: the
     // sphere may be hit; bit 62: covered) and shadow mask for every hit the
-    // tile can produce
+    // tile can produce; uncertified: every triangle and sphere, not covered
     const size_t tix = (size_t)by * lat_tiles_x(F) + bx;
-    const unsigned long long m0 = uniform_u64(lat_masks[2 * tix]);
-    const unsigned long long s0 = uniform_u64(lat_masks[2 * tix + 1]);
+    const unsigned long long all = ((1ull << F.n_tris) - 1ull) | (F.n_sph > 0 ? (1ull << 63) : 0ull);
+    const unsigned long long m0 = certified ? uniform_u64(lat_masks[2 * tix]) : all;
+    const unsigned long long s0 = certified ? uniform_u64(lat_masks[2 * tix + 1]) : all;
     const unsigned long long mask = m0 & ~(3ull << 62), smask = s0 & ~(1ull << 63);
     const bool covered = (m0 >> 62) & 1ull;
     RtFrame Fp = F;                        // pass 1: spheres only where one may be hit
@@ -1624,14 +1675,14 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
                                                                   const unsigned long long *__restrict__ lat_masks,
                                                                   RtFrameCams cams, size_t out_stride,
                                                                   uint32_t *__restrict__ out, uint32_t *frame_done,
-                                                                  LatOrder O)
+                                                                  LatOrder O, LatReady R)
 {
 #ifdef CG_WG_TIMING
     const unsigned long long wt0 = wall_clock64();
 #endif
     const unsigned long long t_start = wall_clock64();
     const LatSlot S = lat_slot_of(O);
-    lattice_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out, S);
+    lattice_body<PITCH>(F0, tc, shade, sph, lat_masks, cams, out_stride, out, S, R);
     // the recording for the next call's order: frame 0's tiles, one class each
     if (O.cost && S.frame == 0 && threadIdx.x == 0)
         O.cost[S.by * (int)gridDim.x + S.bx] = (uint8_t)lat_cost_class(wall_clock64() - t_start);
@@ -1864,8 +1915,11 @@ hipError_t launch_rt_scene(const cg_tri *d_tris, int n, RtGeo *d_geo, RtShade *d
 // launch; on return Z->n < 0 iff it was (the other certificate paths skip it).
 hipError_t launch_rt_prepare(const cg_tri *d_tris, const RtGeo *d_geo, int n, const RtFrameCams &cams, int nframes,
                              RtTri *d_tc, hipStream_t st, const RtFrame *F, const RtSphere *d_sph,
-                             unsigned long long *d_lat_masks, unsigned long long *d_sup_masks, LatFlatten *Z)
+                             unsigned long long *d_lat_masks, unsigned long long *d_sup_masks, LatFlatten *Z,
+                             LatPublish *pub)
 {
+    const LatPublish P = pub ? *pub : LatPublish{};
+    if (pub) pub->done = 0;
     if (n <= 0) return hipSuccess;
     const int threads = kRtThreads, prep = (n + threads - 1) / threads;
     int cert = 0;
@@ -1911,11 +1965,14 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, const RtGeo *d_geo, int n, co
                                  : cnt <= (size_t)resident4 ? 256 : cnt <= 2 * (size_t)resident4 ? 128 : 64;
             const int tprep = (n + tthreads - 1) / tthreads;
             const int kt_id = KT_RT_TILE_CERT;
-            const int ff = tprep + units_w <= 65535;
+            // published certificates run beside the lattice launch: frame-major, as the lattice
+            // takes its tiles, so its first frames' super-tiles come first
+            const int ff = !P.flags && tprep + units_w <= 65535;
             const dim3 cg = ff ? dim3(nframes, tprep + units_w) : dim3(tprep + units_w, nframes);
             kt_launch(kt_id, rt_tile_cert_kernel, cg, dim3(tthreads), 0, st, d_tris, d_geo, n, cams, Fl, d_sph,
                                (const unsigned long long *)nullptr, d_lat_masks, d_tc, tprep, ff,
-                               Z ? *Z : LatFlatten{});
+                               Z ? *Z : LatFlatten{}, P);
+            if (pub) pub->done = P.flags != nullptr;
             if (Z) Z->n = -Z->n;   // done (the caller's flag: the lattice launch may use the order)
             return hipGetLastError();
         }
@@ -1934,7 +1991,7 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, const RtGeo *d_geo, int n, co
         const int ff = units <= 65535;
         kt_launch(kt_id, rt_tile_cert_kernel, ff ? dim3(nframes, units) : dim3(units, nframes), dim3(tthreads), 0, st,
                            d_tris, d_geo, n, cams, Fl, d_sph, (const unsigned long long *)d_sup_masks, d_lat_masks,
-                           (RtTri *)nullptr, 0, ff, LatFlatten{});
+                           (RtTri *)nullptr, 0, ff, LatFlatten{}, LatPublish{});
         return hipGetLastError();
     }
     if (F && d_lat_masks) {   // single-level: every tile (of the window) certified by rt_prepare_kernel
@@ -2018,19 +2075,21 @@ hipError_t launch_rt_lattice_frames(const RtFrame &F, const RtTri *d_tc, const R
                                     const RtSphere *d_sph, const unsigned long long *d_lat_masks,
                                     const unsigned long long *d_umask, const RtFrameCams &cams, int nframes,
                                     size_t out_stride, uint32_t *d_out, hipStream_t st, uint32_t *d_done,
-                                    const LatOrder *order)
+                                    const LatOrder *order, const LatReady *ready)
 {
     const LatOrder O = order ? *order : LatOrder{};
+    const LatReady R = ready ? *ready : LatReady{};
+    if (R.flags && (F.n_lights != 1 || F.n_tris > 62)) return hipErrorInvalidValue;
     const dim3 grid(F.txn ? F.txn : lat_tiles_x(F), (F.rows_out + kLatTileH - 1) / kLatTileH, nframes);
     if (F.n_lights > 1 && !d_umask) return hipErrorInvalidValue;
     if (F.txn && (F.tx0 < 0 || F.tx0 + F.txn > lat_tiles_x(F))) return hipErrorInvalidValue;
     const int kt_id = F.n_lights == 1 ? KT_RT_LATTICE : KT_RT_LATTICE_LIGHTS;
     if (F.n_lights == 1 && lat_yaw(F))
         kt_launch(kt_id, rt_lattice_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
-                           d_lat_masks, cams, out_stride, d_out, d_done, O);
+                           d_lat_masks, cams, out_stride, d_out, d_done, O, R);
     else if (F.n_lights == 1)
         kt_launch(kt_id, rt_lattice_kernel<kLatW>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph, d_lat_masks,
-                           cams, out_stride, d_out, d_done, O);
+                           cams, out_stride, d_out, d_done, O, R);
     else if (lat_yaw(F))
         kt_launch(kt_id, rt_lattice_lights_kernel<kLatWY>, grid, dim3(kRtThreads), 0, st, F, d_tc, d_shade, d_sph,
                            d_lat_masks, d_umask, cams, out_stride, d_out, d_done);
@@ -2051,7 +2110,7 @@ hipError_t launch_rt_pixels(const RtFrame &F, const RtTri *d_tc, const RtShade *
         hipError_t e = launch_rt_lattice_units(F, d_tc, d_shade, d_sph, d_lat_masks, cams, 1, d_umask, st);
         if (e != hipSuccess) return e;
         return launch_rt_lattice_frames(F, d_tc, d_shade, d_sph, d_lat_masks, d_umask, cams, 1, 0, d_out, st,
-                                        nullptr, nullptr);
+                                        nullptr, nullptr, nullptr);
     }
     const int kt_id = KT_RT_PIXEL;
     if (F.n_tris <= 64 && F.cull_primary)

@@ -22,13 +22,14 @@
 namespace cg {
 hipError_t launch_rt_prepare(const cg_tri *, const RtGeo *, int, const RtFrameCams &, int, RtTri *, hipStream_t,
                              const RtFrame *, const RtSphere *, unsigned long long *, unsigned long long *,
-                             LatFlatten * = nullptr);
+                             LatFlatten * = nullptr, LatPublish * = nullptr);
 hipError_t launch_rt_scene(const cg_tri *, int, RtGeo *, RtShade *, hipStream_t);
 hipError_t rt_render_brute(const RtFrame &, const cg_tri *, int, const RtSphere *, int, int, uint32_t *, hipStream_t);
 size_t rt_sup_units(const RtFrame &);
 hipError_t launch_rt_lattice_frames(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                     const unsigned long long *, const unsigned long long *, const RtFrameCams &,
-                                    int, size_t, uint32_t *, hipStream_t, uint32_t *, const LatOrder *);
+                                    int, size_t, uint32_t *, hipStream_t, uint32_t *, const LatOrder *,
+                                    const LatReady * = nullptr);
 hipError_t launch_rt_lattice_units(const RtFrame &, const RtTri *, const RtShade *, const RtSphere *,
                                    const unsigned long long *, const RtFrameCams &, int, unsigned long long *,
                                    hipStream_t);
@@ -201,6 +202,8 @@ struct cg_ctx {
     // of its last lattice launch (class per tile) and the order sorted for it
     DevBuf lcost[2], lflat[2];
     int umask_frames = 0;                            // light sets: frames the unit-mask slots are sized for
+    DevBuf pflag[2];                  // published-certificate words per slot (LatPublish / LatReady)
+    uint32_t cert_gen = 0u;           // generation of the latest published call
     unsigned long long lrec_key[2] = {0ull, 0ull};   // geometry key of the slot's recording (0: none)
     unsigned rt_scene_gen = 0;                       // cg_rt_set_scene count (part of the key)
     // cg_rt_render_frames (host output): chunks render into two device slots
@@ -412,7 +415,7 @@ extern "C" void cg_destroy(cg_ctx *c)
     }
     if (c->start_ev) (void)hipEventDestroy(c->start_ev);
     for (int k = 0; k < 2; ++k) {
-        c->ptc[k].release(); c->plat[k].release(); c->psup[k].release();
+        c->ptc[k].release(); c->plat[k].release(); c->pflag[k].release(); c->psup[k].release();
         c->pumask[k].release();
         if (c->ev_cert[k]) (void)hipEventDestroy(c->ev_cert[k]);
         if (c->ev_lat[k]) (void)hipEventDestroy(c->ev_lat[k]);
@@ -929,6 +932,14 @@ static unsigned long long lat_order_key(const cg_ctx *c, const RtFrame &F)
 // tile's tail), frame-major gains nothing there; both cost whole frames 1-2 % (0.920 -> 0.935 ms
 // per 20-frame lattice launch), so only launches of at most kLatOrderRounds rounds of resident
 // workgroups take the order (a band's ~13k workgroups: yes; a whole frame's 105k: no).
+// Published certificates beside the lattice launch (default on; CG_CERT_CONC=0: the
+// certificates complete first, for A/B runs).  Read per call.
+static bool cert_concurrent()
+{
+    const char *e = std::getenv("CG_CERT_CONC");
+    return !(e && e[0] == '0');
+}
+
 static int lat_order_mode()
 {
     static const int m = [] {
@@ -1037,8 +1048,6 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     // keeps them on the caller's stream -- the cross-stream wait would leave
     // the GPU idle for ~12 us between certificates and lattice.
     const bool cold = hipEventQuery(c->ev_lat[0]) == hipSuccess && hipEventQuery(c->ev_lat[1]) == hipSuccess;
-    hipStream_t cst = cold ? st : c->aux;
-    if (!cold) CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
     // Measured order (one-light lattice kernel): sort the latest complete
     // recording of this geometry -- the other slot's (the previous call) when
     // every lattice launch is done, else this slot's (two calls ago, complete:
@@ -1050,6 +1059,40 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     LatFlatten flat{};
     const bool ordered = lat_order_mode() > 0 && F.n_lights == 1 &&
                          (long long)gx * gy * nf <= kLatOrderRounds * lat_resident_wgs();
+    // Published certificates (LatReady, cg_internal.h): the one-light lattice
+    // launch starts beside its certificate launch instead of after it, each
+    // workgroup waiting only for its own super-tile (calls in the default
+    // order: whole frames; band calls keep the measured order, whose sort the
+    // certificate launch does first)
+    const bool conc = cert_concurrent() && !ordered && F.n_lights == 1 && F.n_tris <= 62 &&
+                      !rt_lattice_unit_bytes(F, nf);
+    // certificates on aux, after the slot's previous reader, so that they run
+    // beside the lattice launch still queued before them (or, published, beside
+    // this call's own).  A cold call with unpublished certificates (every
+    // earlier lattice launch of this context complete: nothing to run beside)
+    // keeps them on the caller's stream -- the cross-stream wait would leave
+    // the GPU idle for ~12 us between certificates and lattice.
+    hipStream_t cst = (cold && !conc) ? st : c->aux;
+    if (!cold) CG_TRY(c, hipStreamWaitEvent(cst, c->ev_lat[k], 0), "aux wait");
+    LatPublish pub{};
+    LatReady ready{};
+    if (conc) {
+        const size_t units = rt_sup_units(F), words = nfa * units;
+        for (int q = 0; q < 2; ++q) {
+            const size_t had = c->pflag[q].bytes;
+            CG_TRY(c, c->pflag[q].ensure(words * sizeof(uint32_t)), "alloc certificate words");
+            if (c->pflag[q].bytes != had) {   // fresh words: zero (no generation), before any launch reads them
+                CG_TRY(c, hipMemsetAsync(c->pflag[q].p, 0, c->pflag[q].bytes, st), "zero certificate words");
+                CG_TRY(c, hipStreamSynchronize(st), "zero certificate words");
+            }
+        }
+        uint32_t gen = ++c->cert_gen;
+        if (gen == 0u) gen = ++c->cert_gen;
+        pub = LatPublish{(uint32_t *)c->pflag[k].p, gen, (int)units};
+        const char *fe = std::getenv("CG_LAT_FORCE_UNCERT");   // test hook, read per call
+        ready = LatReady{(const uint32_t *)c->pflag[k].p, gen, (int)units, (lat_tiles_x_host(F) + kSup - 1) / kSup,
+                         fe && fe[0] == '1', 100000u, (const RtGeo *)c->geo.p, (RtTri *)btc.p};
+    }
     if (ordered) {
         for (int q = 0; q < 2; ++q) {
             // a reallocated cost map holds no recording: forget both slots' keys, or a later
@@ -1063,8 +1106,9 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
     }
     CG_TRY(c, launch_rt_prepare((const cg_tri *)c->tris.p, (const RtGeo *)c->geo.p, c->n_tris, fc, nf,
                                 (RtTri *)btc.p, cst, &F, (const RtSphere *)c->sph.p, lat, supm,
-                                flat.n > 0 ? &flat : nullptr),
+                                flat.n > 0 ? &flat : nullptr, conc ? &pub : nullptr),
            "rt_prepare launch");
+    if (conc && !pub.done) ready = LatReady{};   // not published (the split certificate form): nothing to wait for
     if (ordered) {
         if (flat.n < 0) order.flat = (const uint32_t *)c->lflat[k].p;   // sorted by the certificate launch
         order.cost = (uint8_t *)c->lcost[k].p;
@@ -1086,14 +1130,14 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
                                           lat, fc, nf, um, cst),
                "rt_lattice_units launch");
     }
-    if (!cold) {
-        CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
-        CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
-    }
+    if (!cold || conc) CG_TRY(c, hipEventRecord(c->ev_cert[k], cst), "aux record");
+    if (!cold && !conc) CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
     CG_TRY(c, launch_rt_lattice_frames(F, (const RtTri *)btc.p, (const RtShade *)c->shade.p,
                                        (const RtSphere *)c->sph.p, lat, um, fc, nf, stride, (uint32_t *)d_out, st,
-                                       d_done, ordered ? &order : nullptr),
+                                       d_done, ordered ? &order : nullptr, ready.flags ? &ready : nullptr),
            "rt_lattice launch");
+    // published: whatever the caller queues after this call follows the certificates too
+    if (conc) CG_TRY(c, hipStreamWaitEvent(st, c->ev_cert[k], 0), "aux wait");
     CG_TRY(c, hipEventRecord(c->ev_lat[k], st), "aux record");
     return CG_OK;
 }
