@@ -794,6 +794,7 @@ __device__ __forceinline__ vec3 lat_direct_light(const RtFrame &Fs, const RtTri 
                                                  const RtSphere *__restrict__ sph, const LatObj *s_obj,
                                                  const RtLight &Lt, int bi, vec3 pos, unsigned long long smask)
 {
+    cg_work(W_DL);
     const vec3 r = v3(Lt.x, Lt.y, Lt.z) - pos;                          // :370
     const float rmag = light_rmag(r);                                   // :371
     const vec3 normal = lat_normal(s_obj, bi, pos);                     // :377-387
@@ -865,7 +866,7 @@ template <int PITCH, class Store, int NP = 2>
 __device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__restrict__ tc,
                                             const RtSphere *__restrict__ sph, unsigned long long mask, bool covered,
                                             const LatTile &G, int p_lo, int p_hi, int lane, Store store,
-                                            int step = 128, int ray_stride = 64)
+                                            int step = 128, int ray_stride = 64, bool wc = true)
 {
     for (int p0 = p_lo; p0 < p_hi; p0 += step) {
         float X[NP], Y[NP];
@@ -887,6 +888,10 @@ __device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__re
             const RtTri c = tc[k];
 #pragma unroll
             for (int n = 0; n < NP; ++n) {
+                if (wc && live[n]) {   // the t stage of the ray's one candidate
+                    cg_work(W_RAY_PRI);
+                    cg_work(W_T_PRI);
+                }
                 const vec3 nd = -v3(X[n], Y[n], Fp.focal);
                 const float Q2 = nd.y * c.e2z - c.e2y * nd.z;
                 const float Q1 = nd.y * c.e1z - c.e1y * nd.z;
@@ -895,7 +900,7 @@ __device__ __forceinline__ void lat_closest(const RtFrame &Fp, const RtTri *__re
                 bi[n] = k;
             }
         } else {
-            closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t);   // :140
+            closest_primary_n<NP>(Fp, tc, sph, X, Y, live, mask, bi, t, wc);   // :140
         }
 #pragma unroll
         for (int n = 0; n < NP; ++n)
@@ -1324,10 +1329,11 @@ __device__ __forceinline__ bool lat_lights_tile(const RtFrame &F0, const RtTri *
         return false;
     }
     __syncthreads();                       // s_obj
+    // (work counts: the sweep's pass 1, not the units kernel's repeat of it)
     lat_closest<PITCH>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, [&](int p, float t, int bi) {
         s_t[p] = t;
         s_bi[p] = (int8_t)(bi == INT_MIN ? kLatNoHit : bi);
-    });
+    }, 128, 64, store_black);
     return true;
 }
 
@@ -2190,5 +2196,20 @@ extern "C" int cg_diag_wg_timing(void *buf, unsigned cap)
 extern "C" int cg_diag_wg_count(unsigned *n)
 {
     return hipMemcpyFromSymbol(n, HIP_SYMBOL(cg::g_wgt_n), sizeof *n) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef CG_WORK_COUNT
+// Counting build: this translation unit's work counters (cg_rt_dev.h WorkKind order); reset after reading.
+extern "C" int cg_diag_work_counts_rt(unsigned long long *out, int reset)
+{
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cg::g_work), sizeof(unsigned long long) * cg::W_KINDS) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[cg::W_KINDS] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_work), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
 }
 #endif

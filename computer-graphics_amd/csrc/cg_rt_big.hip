@@ -124,6 +124,7 @@ struct BigBufs {
 __device__ __forceinline__ void tri_closest(const RtTri &c, int k, vec3 nd, float len, float &best,
                                             float &bt, int &bi)
 {
+    cg_work(W_T_PRI);
     float Q2 = nd.y * c.e2z - c.e2y * nd.z;
     float Q1 = nd.y * c.e1z - c.e1y * nd.z;
     float det = (nd.x * c.K1 - c.e1x * Q2) + c.e2x * Q1;      // det(-d, e1, e2) :289
@@ -134,6 +135,7 @@ __device__ __forceinline__ void tri_closest(const RtTri &c, int k, vec3 nd, floa
     if (distance < 0.0f) return;                               // :311
     if (distance > best || distance > FLT_MAX) return;         // :313
     if (distance == best && k > bi) return;                    // ascending-index tie-break
+    cg_work(W_UV_PRI);
     float Q3 = nd.y * c.sz - c.sy * nd.z;
     float detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;      // :317
     float detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;      // :320
@@ -150,6 +152,7 @@ __device__ __forceinline__ void tri_closest(const RtTri &c, int k, vec3 nd, floa
 // with distance < rmag (skeleton.cpp:394-395).
 __device__ __forceinline__ bool tri_shadows(const RtTri &c, vec3 start, vec3 nd, float len, float rmag)
 {
+    cg_work(W_T_SH);
     float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
     float Q2 = nd.y * c.e2z - c.e2y * nd.z;
     float Q1 = nd.y * c.e1z - c.e1y * nd.z;
@@ -170,6 +173,7 @@ __device__ __forceinline__ bool tri_shadows(const RtTri &c, vec3 start, vec3 nd,
     float distance = t * len;
     if (distance < 0.0f) return false;
     if (distance >= rmag || distance > FLT_MAX) return false;
+    cg_work(W_UV_SH);
     float u = detU / det;
     float v = detV / det;
     return (u >= 0) && (v >= 0) && ((u + v) <= 1);
@@ -1770,9 +1774,11 @@ __device__ __forceinline__ vec3 big_direct_light(const RtFrame &F, const RtSpher
                                                  const RtLight &Lt, const ShadowRay &q, vec3 normal,
                                                  vec3 objColor, bool tri_shadow)
 {
+    cg_work(W_DL);
     bool shadow = tri_shadow;
     for (int k = 0; k < F.n_sph && !shadow; ++k) {
         float t;
+        cg_work(W_SPH_SH);
         if (sphere_intersect(sph[k], q.origin, q.r, t) && t < q.rmag) shadow = true;
     }
     if (shadow) return v3(0.0f, 0.0f, 0.0f);                             // :394-398
@@ -2748,6 +2754,21 @@ extern "C" int cg_diag_wg_timing_big(void *buf, unsigned cap)
     unsigned long long *p = (unsigned long long *)buf;
     if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgtb), &p, sizeof p) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_wgtb_cap), &cap, sizeof cap) != hipSuccess) return -1;
+    return 0;
+}
+#endif
+
+#ifdef CG_WORK_COUNT
+// Counting build: this translation unit's work counters (cg_rt_dev.h WorkKind order); reset after reading.
+extern "C" int cg_diag_work_counts_big(unsigned long long *out, int reset)
+{
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cg::g_work), sizeof(unsigned long long) * cg::W_KINDS) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[cg::W_KINDS] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(cg::g_work), z, sizeof z) != hipSuccess) return -1;
+    }
     return 0;
 }
 #endif

@@ -10,6 +10,24 @@
 
 namespace cg {
 
+// Work counters of a counting build (-DCG_WORK_COUNT; scripts/work_counts.py):
+// the reference's own per-ray operations the kernels perform, in SURVEY 8d's
+// units -- a triangle's t stage, its u, v stage (only when the distance tests
+// pass, as in the reference), a sphere test, a ray, a DirectLight -- primary
+// and shadow rays apart.  Wave-aggregated atomics into a per-translation-unit
+// array (cg_diag_work_counts_*); the product build compiles none of it.
+enum WorkKind { W_T_PRI, W_UV_PRI, W_SPH_PRI, W_RAY_PRI, W_T_SH, W_UV_SH, W_SPH_SH, W_RAY_SH, W_DL, W_KINDS };
+#ifdef CG_WORK_COUNT
+static __device__ unsigned long long g_work[W_KINDS];
+__device__ __forceinline__ void cg_work(int k)
+{
+    const unsigned long long b = __ballot(1);
+    if ((int)__lane_id() == __builtin_ctzll(b)) atomicAdd(&g_work[k], (unsigned long long)__popcll(b));
+}
+#else
+__device__ __forceinline__ void cg_work(int) {}
+#endif
+
 // RtTri of a triangle for rays from camf, from its per-scene RtGeo: s =
 // cameraPos - v0 (skeleton.cpp:296-297, the xyz of rt_tri_const's vec4
 // difference), detT, K2, K3 -- bit for bit rt_tri_const's.
@@ -711,14 +729,16 @@ __device__ __forceinline__ int uv_decide(float det, float detU, float detV)
 // divide-free whenever t_decide / uv_decide are certain.
 template <class UV>
 __device__ __forceinline__ bool tri_accept(float detT, float det, float len, float best, UV uvf, float &t_out,
-                                           float &dist_out)
+                                           float &dist_out, bool wc = true)
 {
     const float bound = FLT_MAX;
     float detU, detV;
+    if (wc) cg_work(W_T_PRI);
     const float t = detT / det;                               // :306
     const float distance = t * len;                           // :307
     if (distance < 0.0f) return false;                        // :311
     if (distance >= best || distance > bound) return false;   // :313
+    if (wc) cg_work(W_UV_PRI);
     uvf(detU, detV);
     {
         const float u = detU / det, v = detV / det;           // :317-321
@@ -744,6 +764,7 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
     float bt = 0.f;
     vec3 nd = -d;
     float len = length(d);                                   // :307
+    cg_work(W_RAY_PRI);
     for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
         int k = it;
         if (CULL) {
@@ -771,6 +792,7 @@ __device__ __forceinline__ int closest_primary(const RtFrame &F, const RtTri *__
         float t;
         const RtSphere S = sph[k];
         const vec3 L = s3 - v3(S.cx, S.cy, S.cz);             // camera-constant (:48, :51)
+        cg_work(W_SPH_PRI);
         if (sphere_intersect_pre(L, dot(L, L) - S.r2, d, t)) {
             if (t < best) {
                 best = t;
@@ -791,13 +813,15 @@ template <int N>
 __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri *__restrict__ tc,
                                                   const RtSphere *__restrict__ sph, const float (&X)[N],
                                                   const float (&Y)[N], const bool (&live)[N],
-                                                  unsigned long long mask, int (&bi)[N], float (&bt)[N])
+                                                  unsigned long long mask, int (&bi)[N], float (&bt)[N],
+                                                  bool wc = true)
 {
     const float bound = FLT_MAX;
     const float fz = F.focal;
     float best[N], len[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
+        if (wc && live[n]) cg_work(W_RAY_PRI);
         len[n] = length(v3(X[n], Y[n], fz));                  // :307
         best[n] = bound;
         bt[n] = 0.f;
@@ -820,7 +844,7 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
                 detU = (nd.x * c.K2 - c.sx * Q2) + c.e2x * Q3;    // :317
                 detV = (nd.x * c.K3 - c.e1x * Q3) + c.sx * Q1;    // :320
             };
-            if (tri_accept(c.detT, det, len[n], best[n], uvf, t, distance)) {
+            if (tri_accept(c.detT, det, len[n], best[n], uvf, t, distance, wc)) {
                 best[n] = distance;
                 bt[n] = t;
                 bi[n] = k;
@@ -835,6 +859,7 @@ __device__ __forceinline__ void closest_primary_n(const RtFrame &F, const RtTri 
 #pragma unroll
         for (int n = 0; n < N; ++n) {
             float t;
+            if (wc && live[n]) cg_work(W_SPH_PRI);
             if (live[n] && sphere_intersect_pre(L, cq, v3(X[n], Y[n], fz), t) && t < best[n]) {
                 best[n] = t;
                 bt[n] = t;
@@ -871,6 +896,7 @@ __device__ __forceinline__ void closest_primary_group(const RtFrame &F, const Rt
     for (int b = 0; b < NJ; ++b) ndy[b] = -dy[b];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
+        cg_work(W_RAY_PRI);
         len[s] = length(v3(dx[s / NJ], dy[s % NJ], fz));      // :307
         best[s] = bound;
         bt[s] = 0.f;
@@ -918,6 +944,7 @@ __device__ __forceinline__ void closest_primary_group(const RtFrame &F, const Rt
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             float t;
+            cg_work(W_SPH_PRI);
             if (sphere_intersect_pre(L, cq, v3(dx[s / NJ], dy[s % NJ], fz), t) && t < best[s]) {
                 best[s] = t;
                 bt[s] = t;
@@ -940,6 +967,7 @@ __device__ __forceinline__ void closest_primary_group(const RtFrame &F, const Rt
 // start): an accepted hit with distance < rmag (:394-395).
 __device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 nd, float len, float rmag)
 {
+    cg_work(W_T_SH);
     float sx = start.x - c.v0x, sy = start.y - c.v0y, sz = start.z - c.v0z;   // :296
     float Q2 = nd.y * c.e2z - c.e2y * nd.z;
     float Q1 = nd.y * c.e1z - c.e1y * nd.z;
@@ -951,6 +979,7 @@ __device__ __forceinline__ bool tri_shadow_hit(const RtTri &c, vec3 start, vec3 
     float distance = t * len;
     if (distance < 0.0f) return false;
     if (distance >= rmag || distance > FLT_MAX) return false;
+    cg_work(W_UV_SH);
     float Q3 = nd.y * sz - sy * nd.z;
     float K3 = c.e1y * sz - sy * c.e1z;
     float detU = (nd.x * K2 - sx * Q2) + c.e2x * Q3;
@@ -967,6 +996,7 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
 {
     vec3 nd = -d;
     float len = length(d);
+    cg_work(W_RAY_SH);
     for (int it = 0; CULL ? (mask != 0ull) : (it < F.n_tris); ++it) {
         int k = it;
         if (CULL) {
@@ -977,6 +1007,7 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
     }
     for (int k = 0; k < F.n_sph; ++k) {
         float t;
+        cg_work(W_SPH_SH);
         if (sphere_intersect(sph[k], start, d, t) && t < rmag) return true;
     }
     return false;
@@ -1012,6 +1043,7 @@ __device__ __forceinline__ vec3 direct_light(const RtFrame &F, const RtTri *__re
                                              vec3 objColor, int l, unsigned long long smask = ~0ull)
 {
     const RtLight Lt = F.lights[l];                                      // uniform: scalar loads
+    cg_work(W_DL);
     vec3 lp = v3(Lt.x, Lt.y, Lt.z);
     vec3 r = lp - pos;                                                   // :370
     float rmag = light_rmag(r);                                          // :371
