@@ -354,6 +354,7 @@ def kernel_roofline(kern, section, steps, share, kt, call_launch_ms, fpl_call):
                  "frac_profile_mean_note": (f"lane-ops per launch over the mean launch duration in profiles/{pm_file} "
                                             "(rocprofv3 --kernel-trace --stats)") if pm_file else
                                            "no committed rocprofv3 summary of this workload"})
+    roof.update(useful_roofline(section, kern, fpl, share, kms))
     roof.update({"kernel": kern, "kernel_ms": kms, "kernel_launches": kn, "frames_per_launch": fpl,
                  "kernel_ms_note": "HIP events recorded by the library around each launch of this kernel, on the "
                                    "stream it runs on, over the timed region (cg_kernel_timing): its busy time (the "
@@ -362,6 +363,38 @@ def kernel_roofline(kern, section, steps, share, kt, call_launch_ms, fpl_call):
                  "frac_call_note": "the same lane-ops over the call's HIP-event span per launch (the call's other "
                                    "kernels and gaps included)"})
     return roof
+
+
+def load_work_counts():
+    """The committed counts of the reference's own per-ray work the kernels perform
+    (scripts/work_counts.py on the counting build -> the latest profiles/rNN_work_counts.json);
+    None when absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_work_counts.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        return json.load(f), os.path.basename(paths[-1])
+
+
+def useful_roofline(workload, kernel, frames, share, launch_ms):
+    """the dominant kernel's USEFUL fraction -- the reference's own arithmetic
+    it performs (SURVEY 8d op weights times the counted t stages, u/v stages, sphere tests, rays and
+    DirectLights, profiles/rNN_work_counts.json) over its live launch time, against the same no-FMA
+    issue peak as `frac`.  Certificate FP64, masks, index math and packing count as overhead here,
+    so frac - useful_frac is what the kernel spends beyond the reference's arithmetic."""
+    wc, fname = load_work_counts()
+    w = (wc or {}).get("workloads", {}).get(workload)
+    if not w or not launch_ms or w.get("dominant_kernel") != kernel:
+        return {"useful_frac": None, "useful_note": "no committed work counts for this kernel"}
+    ops = w["useful_ops_per_frame"] * frames * share
+    t = ops / (launch_ms * 1e-3) / 1e12
+    return {"useful_frac": t / PEAK_VALU_LANE_TOPS, "useful_achieved": t, "useful_ops_per_launch": ops,
+            "useful_ops_per_frame": w["useful_ops_per_frame"], "useful_counts_per_frame": w["counts_per_frame"],
+            "useful_kinds": w["dominant_kinds"], "useful_counts_file": f"profiles/{fname}",
+            "useful_note": "the reference's own FP32/FP64 per-ray operations this kernel performs (SURVEY 8d weights: "
+                           "t stage 33, u/v stage 37, sphere 29, ray 11, DirectLight 40; counted on the "
+                           "CG_WORK_COUNT build) / its live launch time / the no-FMA issue peak"}
 
 
 def live_kernel_ms(kt, kernel):

@@ -199,3 +199,28 @@ def test_cpu_info_reports_physical_cores():
     b = _bench()
     ci = b.cpu_info()
     assert 1 <= ci["usable_cores"] <= ci["physical_cores"] <= ci["logical_cpus"]
+
+
+def test_default_line_useful_fraction_matches_counts():
+    """C2's, C4's and C5's dominant-kernel rooflines carry useful_frac, the
+    reference's own per-ray arithmetic the kernel performs over its time; its op count per frame is
+    the committed counts file's (profiles/rNN_work_counts.json, scripts/work_counts.py) recomputed
+    with SURVEY 8d's weights."""
+    import glob
+    rnd, d = _default()
+    if rnd < "r06":
+        pytest.skip("useful_frac starts with round 6's bench")
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_work_counts.json")))
+    assert paths, "no committed work counts"
+    with open(paths[-1]) as f:
+        wc = json.load(f)
+    weights = wc["weights"]
+    for name, r in (("rt", d), ("c4", d["c4"]), ("c5", d["c5"])):
+        ro, w = r["roofline"], wc["workloads"][name]
+        assert w["dominant_kernel"] == ro["kernel"]
+        ops = sum(weights[k] * w["counts_per_frame"][k] for k in w["dominant_kinds"])
+        assert ops == pytest.approx(w["useful_ops_per_frame"])
+        assert ro["useful_ops_per_frame"] == pytest.approx(ops)
+        assert ro["useful_counts_file"] == "profiles/" + os.path.basename(paths[-1])
+        assert 0 < ro["useful_frac"] <= 1
+        assert ro["useful_frac"] == pytest.approx(ro["useful_achieved"] / ro["peak"])
