@@ -939,6 +939,13 @@ static bool cert_concurrent()
     const char *e = std::getenv("CG_CERT_CONC");
     return !(e && e[0] == '0');
 }
+// How long a lattice workgroup waits for its published certificates before it renders the tile
+// uncertified: wall-clock ticks (100 MHz), default 1 ms; CG_LAT_SPIN for A/B runs (0: never wait).
+static uint32_t lat_spin_ticks()
+{
+    const char *e = std::getenv("CG_LAT_SPIN");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 100000u;
+}
 
 static int lat_order_mode()
 {
@@ -1003,7 +1010,15 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
         // back-to-back calls, but left the process's later streams sharing
         // hardware queues -- the rasteriser's overlapped frames then ran
         // serialised (C3 10.1-11.1k instead of 21.0-21.3k frames/s)
-        CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
+        {
+            // A/B knob: CG_AUX_PRIO=1 creates the auxiliary stream at the highest priority
+            const char *pe = std::getenv("CG_AUX_PRIO");
+            int lo = 0, hi = 0;
+            if (pe && pe[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+                CG_TRY(c, hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi), "aux stream");
+            else
+                CG_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking), "aux stream");
+        }
         for (int k = 0; k < 2; ++k) {
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_cert[k], hipEventDisableTiming), "aux event");
             CG_TRY(c, hipEventCreateWithFlags(&c->ev_lat[k], hipEventDisableTiming), "aux event");
@@ -1091,7 +1106,7 @@ static int rt_enqueue_lattice_batch(cg_ctx *c, const RtFrame &F0, const cg_rt_ca
         pub = LatPublish{(uint32_t *)c->pflag[k].p, gen, (int)units};
         const char *fe = std::getenv("CG_LAT_FORCE_UNCERT");   // test hook, read per call
         ready = LatReady{(const uint32_t *)c->pflag[k].p, gen, (int)units, (lat_tiles_x_host(F) + kSup - 1) / kSup,
-                         fe && fe[0] == '1', 100000u, (const RtGeo *)c->geo.p, (RtTri *)btc.p};
+                         fe && fe[0] == '1', lat_spin_ticks(), (const RtGeo *)c->geo.p, (RtTri *)btc.p};
     }
     if (ordered) {
         for (int q = 0; q < 2; ++q) {

@@ -2,7 +2,7 @@
 counting build of the library:
 
     make -C computer-graphics_amd OUT=_build_wc EXTRA=-DCG_WORK_COUNT _build_wc/libcgamd.so
-    python scripts/work_counts.py [--out profiles/r06_work_counts.json]
+    python scripts/work_counts.py [--out gpurun_out/work_counts.json]   (then copied to profiles/rNN_work_counts.json)
 
 Every triangle t stage, u/v stage (only when the distance tests pass, as in the reference), sphere
 test, ray and DirectLight the kernels execute is counted (cg_rt_dev.h WorkKind; wave-aggregated
@@ -56,7 +56,7 @@ def read(lib, reset=True):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r06_work_counts.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "work_counts.json"))
     args = ap.parse_args()
     res = {"note": __doc__.strip().splitlines()[0], "weights": WEIGHTS, "library": os.environ["CGAMD_LIB"],
            "workloads": {}}
