@@ -932,12 +932,18 @@ static unsigned long long lat_order_key(const cg_ctx *c, const RtFrame &F)
 // tile's tail), frame-major gains nothing there; both cost whole frames 1-2 % (0.920 -> 0.935 ms
 // per 20-frame lattice launch), so only launches of at most kLatOrderRounds rounds of resident
 // workgroups take the order (a band's ~13k workgroups: yes; a whole frame's 105k: no).
-// Published certificates beside the lattice launch (default on; CG_CERT_CONC=0: the
-// certificates complete first, for A/B runs).  Read per call.
+// Published certificates beside the lattice launch: CG_CERT_CONC=1 (read per call; off by
+// default).  Measured on one MI355X (profiles/r06_ab_conc.json, the driver's 20-frame C2 call):
+// 14.2-14.5k frames/s against 18.7-18.9k with the certificates first -- once the lattice launch
+// holds the CUs the certificate launch is dispatched only as its workgroups retire (its span
+// 80 -> 420 us; a high-priority auxiliary stream changes nothing), so lattice workgroups wait for
+// their words or, past the bound, render uncertified, which costs ~15x a certified tile (every
+// tile uncertified: 1.45k frames/s).  The path stays as the uncertified-path exactness test
+// (CG_LAT_FORCE_UNCERT=1, tests/test_rt_conc_gpu.py).
 static bool cert_concurrent()
 {
     const char *e = std::getenv("CG_CERT_CONC");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 // How long a lattice workgroup waits for its published certificates before it renders the tile
 // uncertified: wall-clock ticks (100 MHz), default 1 ms; CG_LAT_SPIN for A/B runs (0: never wait).

@@ -1,12 +1,15 @@
 """GPU: certificates published beside the lattice launch (cg_internal.h LatReady /
-LatPublish).  A whole-frame batched call starts its lattice
-launch beside its certificate launch; each lattice workgroup waits only for its
-own super-tile's publication word, or -- past its bound, or forced with
+LatPublish, CG_CERT_CONC=1; VERDICT r05 item 1 -- built, measured slower, off by
+default, cg_shim.hip cert_concurrent).  A whole-frame batched call starts its
+lattice launch beside its certificate launch; each lattice workgroup waits only
+for its own super-tile's publication word, or -- past its bound, or forced with
 CG_LAT_FORCE_UNCERT=1 -- renders its tile uncertified (every triangle and the
-sphere as candidates, the frame's RtTri formed by the workgroup itself).  Both
-paths must give the reference's image bit for bit: the golden 1080p frame
+sphere as candidates, the frame's RtTri formed by the workgroup itself).  Every
+path must give the reference's image bit for bit: the golden 1080p frame
 (SURVEY 8c fingerprint) for every frame of a call, and per-frame renders for
-moving and yawed cameras.  Reference: raytracer/Source/skeleton.cpp:104-169."""
+moving and yawed cameras.  The forced uncertified path is the test that the
+certificates only ever remove candidates that cannot change a pixel.
+Reference: raytracer/Source/skeleton.cpp:104-169."""
 import hashlib
 
 import numpy as np
@@ -44,10 +47,9 @@ def _call(ctx, cams, out=None):
 def test_conc_whole_calls_golden(c2, golden, monkeypatch, mode):
     """Calls of 20, 5, 32 and 20 frames back to back (both certificate slots, rising
     generations): every frame == the golden 1080p fingerprint."""
+    monkeypatch.setenv("CG_CERT_CONC", "0" if mode == "serial" else "1")
     if mode == "uncertified":
         monkeypatch.setenv("CG_LAT_FORCE_UNCERT", "1")
-    elif mode == "serial":
-        monkeypatch.setenv("CG_CERT_CONC", "0")
     want = golden["rt"]["rt_1920x1080_f1080"]["argb_sha256"]
     cam = cgamd.rt_camera(W, H, F)
     for nf in (20, 5, 32, 20):
@@ -61,6 +63,7 @@ def test_conc_whole_calls_golden(c2, golden, monkeypatch, mode):
 def test_conc_moving_cameras_equal_single_frames(c2, monkeypatch, mode, path):
     """A 20-frame call whose every frame has its own camera (cameraPos dolly, or a yaw per
     frame as the LEFT key turns it) == each frame rendered alone (cg_rt_render)."""
+    monkeypatch.setenv("CG_CERT_CONC", "1")
     if mode == "uncertified":
         monkeypatch.setenv("CG_LAT_FORCE_UNCERT", "1")
     if path == "dolly":
@@ -70,6 +73,7 @@ def test_conc_moving_cameras_equal_single_frames(c2, monkeypatch, mode, path):
         cams = [cgamd.rt_camera(W, H, F, (0.002 * k, 0.0, -3.0, 1.0), R) for k in range(20)]
     frames = _call(c2, cams)
     monkeypatch.delenv("CG_LAT_FORCE_UNCERT", raising=False)
+    monkeypatch.delenv("CG_CERT_CONC", raising=False)
     for k in range(20):
         alone = c2.rt_render(cams[k])[0]
         assert np.array_equal(frames[k], alone), f"{path}/{mode}: frame {k}"
