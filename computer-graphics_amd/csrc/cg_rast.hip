@@ -36,6 +36,7 @@ int ctx_invalid(cg_ctx *c, const char *what);
 void ctx_events(cg_ctx *c, hipEvent_t *a, hipEvent_t *b);
 
 constexpr int kSetupThreads = 256;
+constexpr int kSetupPreChunks = 16;  // input triangles counted in one round trip: < 64 * 16
 constexpr int kRastMaxRows = 4096;   // LDS rows per triangle in span setup (H <= 4096)
 
 // Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.
@@ -149,7 +150,43 @@ __global__ __launch_bounds__(kSetupThreads) void rast_setup_kernel(
     int *s_pre = (int *)(s_keys + 2 * A.H);
     int n = A.n;
     if (stage) {
-        if (threadIdx.x < 64) {                            // wave 0: exclusive prefix of the counts
+        if (n_in < 64 * kSetupPreChunks) {
+            // exclusive prefix of the counts: every count loaded at once (one round trip, all
+            // threads), each wave scans its 64-count chunks, then thread 0 offsets the chunks
+            __shared__ int s_tot[kSetupPreChunks];
+            constexpr int kQ = kSetupPreChunks / (kSetupThreads / 64);
+            const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+            int cnt[kQ];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int i = (q * (kSetupThreads / 64) + w) * 64 + lane;
+                cnt[q] = i < n_in ? counts[i] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int ch = q * (kSetupThreads / 64) + w, i = ch * 64 + lane;
+                int x = cnt[q];
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(x, o);
+                    if (lane >= o) x += y;
+                }
+                if (i <= n_in) s_pre[i] = x - cnt[q];   // exclusive within the chunk (s_pre[n_in]: its total)
+                if (lane == 63) s_tot[ch] = x;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int a = 0;
+                for (int ch = 0; ch * 64 <= n_in; ++ch) {
+                    const int t = s_tot[ch];
+                    s_tot[ch] = a;
+                    a += t;
+                }
+                s_carry = a;
+            }
+            __syncthreads();
+            for (int i = threadIdx.x; i <= n_in; i += kSetupThreads) s_pre[i] += s_tot[i / 64];
+        } else if (threadIdx.x < 64) {                     // wave 0: exclusive prefix of the counts
             const int lane = threadIdx.x;
             int carry = 0;
             for (int i0 = 0; i0 < n_in; i0 += 64) {
