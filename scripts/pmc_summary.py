@@ -42,7 +42,8 @@ for wl, kernels in DOMINANT.items():
         # frame's sizing passes (once per pass, like rt_sup_primary_kernel)
         frames = max(1, nf.get("rt_big_primary_kernel", 1))
         passes = max(1, nf.get("rt_sup_primary_kernel", frames))
-        kernels = sorted(k for k in f if k.startswith("rt_"))
+        # (rt_scene_kernel runs once per scene, at cg_rt_set_scene: not a frame's)
+        kernels = sorted(k for k in f if k.startswith("rt_") and k != "rt_scene_kernel")
         mult = {k: max(1, round(nf[k] / (passes if nf[k] > frames else frames))) for k in kernels}
     det = {k: {"fetch_kib_raw": f.get(k), "write_kib": w.get(k), "dispatches_per_frame": mult.get(k, 1),
                "hbm_bytes_corrected": (2 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024 * mult.get(k, 1)} for k in kernels}
