@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <utility>
@@ -24,6 +25,7 @@ static const char *const kKtNames[KT_COUNT] = {
 };
 
 namespace {
+constexpr size_t kKtPoolEvents = 512;   // pre-created when timing is switched on (256 timed launches)
 struct Pending {
     int id;
     hipEvent_t a, b;
@@ -31,6 +33,7 @@ struct Pending {
 struct KtState {
     std::mutex mu;
     bool on = false;
+    bool all = false;                   // also time the certificate launches (CG_KTIME_ALL=1)
     std::atomic<bool> on_fast{false};   // read without the lock: a disabled scope costs one load
     std::vector<hipEvent_t> pool;
     std::vector<Pending> pending;
@@ -94,6 +97,7 @@ struct KtState {
     }
     hipEvent_t get()
     {
+        if (pool.empty()) settle_completed();   // recycle the pairs that completed
         if (!pool.empty()) {
             hipEvent_t e = pool.back();
             pool.pop_back();
@@ -148,6 +152,9 @@ KtLaunch::KtLaunch(int id, hipStream_t st) : id_(id)
     if (!s.on_fast.load(std::memory_order_relaxed)) return;
     std::lock_guard<std::mutex> g(s.mu);
     if (!s.on || id < 0 || id >= KT_COUNT) return;
+    // the certificate launches ride untimed unless CG_KTIME_ALL=1: no roofline reads them, and a
+    // timed (profiled) dispatch costs host time in front of the lattice launch that follows
+    if (!s.all && (id == KT_RT_PREPARE || id == KT_RT_TILE_CERT || id == KT_RT_LATTICE_UNITS)) return;
     if (!s.ref_set) {   // one recorded event anchors the busy-time spans
         if (!s.ref && hipEventCreate(&s.ref) != hipSuccess) s.ref = nullptr;
         s.ref_set = s.ref && hipEventRecord(s.ref, st) == hipSuccess;
@@ -189,6 +196,21 @@ extern "C" int cg_kernel_timing(int enable)
     for (auto &v : s.spans) v.clear();
     s.ref_set = false;
     s.on = enable != 0;
+    {
+        const char *e = std::getenv("CG_KTIME_ALL");
+        s.all = e && e[0] == '1';
+    }
+    if (s.on) {
+        // every event a timed region will record, created here rather than in front of
+        // the timed launches: a hipEventCreate per event in the launch path cost ~15 us of
+        // host time per call (two launches), which a band call's second launch waited for
+        if (!s.ref && hipEventCreate(&s.ref) != hipSuccess) s.ref = nullptr;
+        while (s.pool.size() < kKtPoolEvents) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            s.pool.push_back(e);
+        }
+    }
     s.on_fast.store(s.on);
     return CG_OK;
 }

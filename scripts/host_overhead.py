@@ -1,7 +1,8 @@
 """One GPU: where a cold C2 call's wall time goes on the host side -- the API call's own time
 (t_api: cg_rt_render_frames_device returns), the synchronise after it, and the device span
 (HIP events around the call on its stream) -- for the whole frame and a 1/8 band (RGB24,
-the wire's columns).  Usage: python scripts/host_overhead.py [N] [spin]"""
+the wire's columns).  Usage: python scripts/host_overhead.py [N] [spin|ktime]
+(ktime: the library's live kernel timing on, as in bench.py's timed region)"""
 import ctypes
 import json
 import os
@@ -10,6 +11,7 @@ import sys
 import time
 
 SPIN = len(sys.argv) > 2 and sys.argv[2] == "spin"
+KTIME = len(sys.argv) > 2 and sys.argv[2] == "ktime"
 if SPIN:   # hipDeviceScheduleSpin before any HIP context exists
     hip = ctypes.CDLL("libamdhip64.so")
     assert hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0
@@ -23,7 +25,7 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 21
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 stream = torch.cuda.Stream(dev)
-res = {"spin": SPIN}
+res = {"spin": SPIN, "ktime": KTIME}
 with cgamd.Context(0) as ctx:
     tris, n, sph = cgamd.rt_scene()
     ctx.rt_set_scene(tris, n, sph, 1)
@@ -35,6 +37,7 @@ with cgamd.Context(0) as ctx:
     sp = ctypes.c_void_p(stream.cuda_stream)
     c0, c1 = cgamd.frame_columns(tris, n, sph, 1, cam)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cgamd.kernel_timing(KTIME)
 
     def one(shard, fmt):
         torch.cuda.synchronize(dev)

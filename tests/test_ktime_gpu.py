@@ -14,7 +14,7 @@ def _times(*names):
     return {k: cgamd.kernel_time(k) for k in names}
 
 
-def test_kernel_time_counts_each_timed_launch(ctx):
+def test_kernel_time_counts_each_timed_launch(ctx, monkeypatch):
     torch = pytest.importorskip("torch")
     tris, n, sph = cgamd.rt_scene()
     ctx.rt_set_scene(tris, n, sph, 1)
@@ -25,6 +25,7 @@ def test_kernel_time_counts_each_timed_launch(ctx):
     ctx.rt_render_frames_device(cams, g.data_ptr(), None, st.cuda_stream)      # warm, untimed
     st.synchronize()
     ref = g.clone()
+    monkeypatch.setenv("CG_KTIME_ALL", "1")        # the certificate launches timed too
     cgamd.kernel_timing(True)
     try:
         for _ in range(calls):
@@ -41,6 +42,16 @@ def test_kernel_time_counts_each_timed_launch(ctx):
     cert_launches = t["rt_tile_cert_kernel"][2] + t["rt_prepare_kernel"][2]
     assert calls <= cert_launches <= 2 * calls     # fused certificates: one launch per call, split: two
     assert t["rast_fill_kernel"] == (0.0, 0.0, 0)  # kernels that did not run record nothing
+    # by default only the kernels a roofline reads are timed: the certificate launches ride plain
+    monkeypatch.delenv("CG_KTIME_ALL")
+    cgamd.kernel_timing(True)
+    try:
+        ctx.rt_render_frames_device(cams, g.data_ptr(), None, st.cuda_stream)
+        st.synchronize()
+        t2 = _times("rt_lattice_kernel", "rt_tile_cert_kernel", "rt_prepare_kernel")
+    finally:
+        cgamd.kernel_timing(False)
+    assert t2["rt_lattice_kernel"][2] == 1 and t2["rt_tile_cert_kernel"][2] == 0 and t2["rt_prepare_kernel"][2] == 0
     # off: nothing is recorded
     ctx.rt_render_frames_device(cams, g.data_ptr(), None, st.cuda_stream)
     st.synchronize()
