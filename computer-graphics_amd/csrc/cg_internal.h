@@ -229,6 +229,7 @@ class KtLaunch {
 
   private:
     int id_;
+    bool ref_ = false;   // a is the session's anchor event
 };
 template <class K, class... A>
 inline void kt_launch(int id, K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, A... args)

@@ -435,7 +435,10 @@ __device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int c
 // masks round-trip through memory and no second dependent launch.
 __device__ __forceinline__ void lat_flatten(const LatFlatten &Z);   // below, with the lattice kernel
 
-__global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris,
+#ifndef CG_CERT_WAVES
+#define CG_CERT_WAVES 4   // waves per SIMD of the certificate launch (A/B: -DCG_CERT_WAVES=n)
+#endif
+__global__ __launch_bounds__(256, CG_CERT_WAVES) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris,
                                                            const RtGeo *__restrict__ geo, int n, RtFrameCams cams,
                                                            RtFrame F, const RtSphere *__restrict__ sph,
                                                            const unsigned long long *__restrict__ sup_masks,
@@ -631,7 +634,10 @@ __global__ __launch_bounds__(256, 4) void rt_tile_cert_kernel(const cg_tri *__re
 
 // Draw (skeleton.cpp:104-169), one thread per pixel.  CULL: n_tris <= 64,
 // one certificate mask per wave (lane k certifies triangle k).
-constexpr int kRtMinWaves = 6;   // waves per SIMD of rt_lattice_kernel (52 VGPRs: 8 fit)
+#ifndef CG_LAT_WAVES
+#define CG_LAT_WAVES 6    // A/B: -DCG_LAT_WAVES=n
+#endif
+constexpr int kRtMinWaves = CG_LAT_WAVES;   // waves per SIMD of rt_lattice_kernel (68 VGPRs: 7 fit)
 // The pixel kernel (rotations other than a yaw; no bench configuration) at 5
 // waves per SIMD: 96 VGPRs and no scratch -- 6 spilled 52 B per lane for ~1 %.
 constexpr int kRtPixelWaves = 5;
