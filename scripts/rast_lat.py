@@ -1,6 +1,7 @@
 """C3 single-Draw latency per kernel: cg_rast_draw_device one frame at a time
 (synchronised), for rocprofv3 --kernel-trace --stats.  Usage:
-  rocprofv3 --kernel-trace --stats --output-format csv -d OUT -o rast -- python scripts/rast_lat.py [frames]"""
+  rocprofv3 --kernel-trace --stats --output-format csv -d OUT -o rast -- python scripts/rast_lat.py [frames]
+(CG_RAST_CM=1|2: colour mode)"""
 import os
 import sys
 
@@ -14,7 +15,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 with cgamd.Context(0) as ctx:
-    p = cgamd.rast_params(W, H, F)
+    p = cgamd.rast_params(W, H, F, colour_mode=int(os.environ.get("CG_RAST_CM", "0")))
     ctx.rast_set_scene()
     argb = torch.zeros(W * H, dtype=torch.int32, device=dev)
     depth = torch.zeros(W * H, dtype=torch.float32, device=dev)
