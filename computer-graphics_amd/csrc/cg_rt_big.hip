@@ -1918,6 +1918,19 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 #ifndef CG_HINT_WAVES
 #define CG_HINT_WAVES 4   // 99-101 VGPRs, no scratch; 5: 12-16 B, 6: 68-76 B -- all the same speed (r05_ab_walk.json)
 #endif
+// The grid walks of a wave's unresolved shadow rays are deferred to the end of
+// the wave (a per-wave LDS queue, kHintQ rays) and then walked 64 at a time, one
+// per lane: inline, only the ~quarter of the lanes the cheap tests left
+// unresolved walk while the others wait (C5: 26 % of the rays, 18.5 triangle
+// tests each).  A full queue walks inline, as before.  CG_HINT_QUEUE=0: inline.
+#ifndef CG_HINT_QUEUE
+#define CG_HINT_QUEUE 1
+#endif
+constexpr int kHintQ = 128;
+struct HintQ {
+    float4 a[kHintQ], b[kHintQ];   // origin.xyz, len | r.xyz, rmag
+    int2 e[kHintQ];                // the verdict's word (pixel or lattice point), bit
+};
 template <int LM>
 __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                                      const RtShade *__restrict__ shade,
@@ -1928,7 +1941,12 @@ __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_ker
     constexpr int NS = LM == 0 ? 9 : (LM == 1 ? 5 : 7);   // ray slots per lane (lattice: owned points / 64)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int tx = blockIdx.x * (kRtTileW / 8) + wave, ty = blockIdx.y;
-    if (tx >= B.tiles_x) return;
+    if (tx >= B.tiles_x) return;   // the whole wave (the queue is per wave: no barrier)
+#if CG_HINT_QUEUE
+    __shared__ HintQ s_hq[kRtThreads / 64];
+    HintQ &hq = s_hq[wave];
+    int qn = 0;                     // wave-uniform: entries queued
+#endif
     const float m = 0.5f;
     int u = 0, L = 0, nsu = NS, n = 0;
     bool active = false;
@@ -1992,18 +2010,40 @@ __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_ker
                 have &= ~__ballot(k == kn);
                 if (ray && k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
             }
+            const int bitno = kLat ? l : s * F.n_lights + l;
+#if CG_HINT_QUEUE
+            // every lane (qn stays wave-uniform): queue the unresolved rays while the
+            // wave's queue has room for all of this step's
+            bool queued = false;
+            {
+                const bool need = ray && k < 0;
+                const unsigned long long want = __ballot(need);
+                const int nw = __popcll(want);
+                const bool fits = qn + nw <= kHintQ;
+                if (need && fits) {
+                    const int at = qn + __popcll(want & ((1ull << lane) - 1ull));
+                    hq.a[at] = make_float4(q.origin.x, q.origin.y, q.origin.z, q.len);
+                    hq.b[at] = make_float4(q.r.x, q.r.y, q.r.z, q.rmag);
+                    hq.e[at] = make_int2((int)(kLat ? id : pix), bitno);
+                }
+                if (fits) qn += nw;
+                queued = need && fits;
+            }
+#endif
             if (!ray) continue;
 #ifdef CG_WALK_STATS
             ++st_rays;
             if (k >= 0) ++st_cheap;
             const int g0 = gtests;
 #endif
+#if CG_HINT_QUEUE
+            if (queued) continue;   // its verdict comes from the deferred walk
+#endif
             if (k < 0) k = grid_blocker(B.grid, tc, q, &gtests);
 #ifdef CG_WALK_STATS
             if (gtests > g0) ++st_grid_rays;
             if (k < 0) ++st_lit;
 #endif
-            const int bitno = kLat ? l : s * F.n_lights + l;
             const unsigned long long bit = 1ull << bitno;
             if (k >= 0) {
                 shadowed |= bit;
@@ -2037,6 +2077,38 @@ __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_ker
         B.sh_bits[pix] = shadowed;
         B.pend_bits[pix] = pending;
     }
+#if CG_HINT_QUEUE
+    // The deferred grid walks, one queued ray per lane.  A verdict ORs its bit into
+    // the word this wave stored above: the wave's stores are acknowledged first
+    // (vmcnt), so the OR reaches the word after them.
+    if (qn > 0) {
+        __asm__ volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0);   // vmcnt, expcnt, lgkmcnt all 0: the stores above are done, the queue written
+        __asm__ volatile("" ::: "memory");
+        for (int j = lane; j < qn; j += 64) {
+            ShadowRay q;
+            const float4 a = hq.a[j], b = hq.b[j];
+            const int2 e = hq.e[j];
+            q.origin = v3(a.x, a.y, a.z);
+            q.len = a.w;
+            q.r = v3(b.x, b.y, b.z);
+            q.rmag = b.w;
+            q.nd = -q.r;
+            const int k = grid_blocker(B.grid, tc, q, &gtests);
+            const unsigned long long bit = 1ull << e.y;
+            if (k >= 0) {
+                atomicOr(&B.sh_bits[e.x], bit);
+            } else {
+                const int p = atomicAdd(B.pend_n, 1);
+                if (p < B.max_pend)
+                    B.pend_ray[p] = PendRay{q.origin.x, q.origin.y, q.origin.z, q.nd.x, q.nd.y, q.nd.z, q.len, q.rmag,
+                                            e.x, e.y};
+                else
+                    atomicOr(&B.pend_bits[e.x], bit);   // past the queue: rt_big_shade_kernel searches it
+            }
+        }
+    }
+#endif
     WGTB_END(4);
 }
 
