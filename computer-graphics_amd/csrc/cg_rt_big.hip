@@ -1927,6 +1927,9 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 #define CG_HINT_QUEUE 1
 #endif
 constexpr int kHintQ = 128;
+#ifndef CG_HINT_REPS
+#define CG_HINT_REPS 16   // blockers other lanes found, tried per unresolved ray before the grid
+#endif
 struct HintQ {
     float4 a[kHintQ], b[kHintQ];   // origin.xyz, len | r.xyz, rmag
     int2 e[kHintQ];                // the verdict's word (pixel or lattice point), bit
@@ -2005,7 +2008,7 @@ __global__ __launch_bounds__(kRtThreads, CG_HINT_WAVES) void rt_shadow_hints_ker
             // tri_shadows, so the verdict does not depend on which lanes
             // contributed them
             unsigned long long have = __ballot(k >= 0);
-            for (int rep = 0; rep < 16 && have != 0ull && __ballot(ray && k < 0) != 0ull; ++rep) {
+            for (int rep = 0; rep < CG_HINT_REPS && have != 0ull && __ballot(ray && k < 0) != 0ull; ++rep) {
                 const int kn = __shfl(k, __builtin_ctzll(have));
                 have &= ~__ballot(k == kn);
                 if (ray && k < 0 && tri_shadows(tc[kn], q.origin, q.nd, q.len, q.rmag)) k = kn;
