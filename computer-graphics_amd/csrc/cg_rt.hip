@@ -796,6 +796,7 @@ __device__ __forceinline__ vec3 lat_normal(const LatObj *s_obj, int bi, vec3 pos
 }
 // DirectLight (skeleton.cpp:366-415) of light Lt for a hit on bi at pos, the
 // shadow ray walking the candidates of smask (as direct_light<true>)
+template <bool SHARED = false>
 __device__ __forceinline__ vec3 lat_direct_light(const RtFrame &Fs, const RtTri *__restrict__ tc,
                                                  const RtSphere *__restrict__ sph, const LatObj *s_obj,
                                                  const RtLight &Lt, int bi, vec3 pos, unsigned long long smask)
@@ -806,7 +807,7 @@ __device__ __forceinline__ vec3 lat_direct_light(const RtFrame &Fs, const RtTri 
     const vec3 normal = lat_normal(s_obj, bi, pos);                     // :377-387
     const vec3 origin = pos + normal * 0.00001f;                        // :394
     if (shadowed<true>(Fs, tc, sph, origin, r, rmag, smask)) return v3(0.0f, 0.0f, 0.0f);   // :394-398
-    return direct_light_lit(Lt, r, rmag, normal, lat_colour(s_obj, bi));
+    return direct_light_lit<SHARED>(Lt, r, rmag, normal, lat_colour(s_obj, bi));
 }
 
 //
@@ -1591,7 +1592,7 @@ __device__ __forceinline__ void lattice_lights_body(const RtFrame &F0, const RtT
                     if (bi == kLatNoHit) return;
                     const float Y = 0.5f * (float)(ay0 + cy), t = s_t[cy * PITCH + cx];
                     const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
-                    const vec3 dl = lat_direct_light(Fu, tc, sph, s_obj, Lt, bi, pos, um);
+                    const vec3 dl = lat_direct_light<true>(Fu, tc, sph, s_obj, Lt, bi, pos, um);
                     float *b = &s_dl[step & 1][r][0][0];
                     b[l ^ lat_swz(r, 0)] = dl.x;
                     b[kLatMaxLights + (l ^ lat_swz(r, 1))] = dl.y;

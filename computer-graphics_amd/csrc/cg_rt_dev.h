@@ -1013,8 +1013,44 @@ __device__ __forceinline__ bool shadowed(const RtFrame &F, const RtTri *__restri
     return false;
 }
 
+// x / d per channel (:412's three numerators over one area), bit for bit.  The
+// compiler's IEEE f32 division is v_div_scale (denominator), v_div_scale
+// (numerator, VCC), v_rcp, two refinement FMAs, v_mul, three FMAs, v_div_fmas,
+// v_div_fixup; here d's refined reciprocal is formed once for the three and the
+// scaling and fix-up steps are dropped.  Those are identities when the operands
+// and the quotient are normal and far from the range ends: div_scale rescales
+// only a denormal or extreme-exponent operand or quotient (VCC then stays clear
+// and div_fmas is a plain FMA), div_fixup rewrites only zero, infinite or NaN
+// operands.  Taken when d is in [2^-40, 2^40], each x at least 2^-86 and their
+// sum at most 2^40 (so each quotient lies in [2^-126, 2^80], no exponent gap
+// reaches 96 and every numerator exceeds 2^-103); NaN fails the tests, and any
+// lane outside divides as before.
+// SHARED = false: the three IEEE divides.  Measured per kernel (profiles/r06_ab_session2.json):
+// the light-set sweep (C4) gains 1.6 %, the one-light lattice (C2) lost 1.7 % and the large
+// scenes' shading 0.7 %, so only the sweep takes it.
+template <bool SHARED>
+__device__ __forceinline__ vec3 div3_by(vec3 x, float d)
+{
+    if constexpr (SHARED) {
+        const bool ok = d >= 0x1p-40f && d <= 0x1p40f && x.x >= 0x1p-86f && x.y >= 0x1p-86f &&
+                        x.z >= 0x1p-86f && (x.x + x.y) + x.z <= 0x1p40f;
+        if (ok) {
+            const float r0 = __builtin_amdgcn_rcpf(d);
+            const float r = fmaf(fmaf(-d, r0, 1.0f), r0, r0);
+            auto q = [&](float n) {
+                float m = n * r;
+                m = fmaf(fmaf(-d, m, n), r, m);
+                return fmaf(fmaf(-d, m, n), r, m);
+            };
+            return v3(q(x.x), q(x.y), q(x.z));
+        }
+    }
+    return x / d;
+}
+
 // DirectLight's lit branch (skeleton.cpp:400-412): r = light - pos, rmag its
 // FP64 magnitude (:370-371), normal at the hit (:377-387).
+template <bool SHARED = false>
 __device__ __forceinline__ vec3 direct_light_lit(const RtLight &Lt, vec3 r, float rmag, vec3 normal,
                                                  vec3 objColor)
 {
@@ -1024,7 +1060,7 @@ __device__ __forceinline__ vec3 direct_light_lit(const RtLight &Lt, vec3 r, floa
     float area = (float)((double)b * ((double)rmag * (double)rmag));     // :406
     if (a <= 0) a = 0.f;                                                 // :409
     vec3 lc = v3(Lt.r, Lt.g, Lt.b);
-    return ((objColor * lc) * a) / area;                                 // :412
+    return div3_by<SHARED>((objColor * lc) * a, area);                   // :412
 }
 
 // r_magnitude (skeleton.cpp:371): the norm in FP64, rounded to float.
