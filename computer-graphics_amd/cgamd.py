@@ -128,6 +128,7 @@ _SIGS = {
                                       C.POINTER(Isect), C.POINTER(C.c_int)]),
     "cg_rt_probe_direct_light": (C.c_int, [P, C.POINTER(Isect), C.POINTER(Light), C.c_int,
                                            C.POINTER(Vec3)]),
+    "cg_rt_probe_div3_device": (C.c_int, [P, P, C.c_int, P, P]),
     "cg_rast_load_test_model": (C.c_int, [C.POINTER(RTri), C.c_int, C.POINTER(C.c_int),
                                           C.POINTER(RTri), C.c_int, C.POINTER(C.c_int)]),
     "cg_rast_prepare": (C.c_int, [C.POINTER(RastParams), C.POINTER(RTri), C.c_int, C.POINTER(RTri),
@@ -321,6 +322,13 @@ def frame_columns(tris, n, sph, n_sph, cam):
     if rc != CG_OK:
         raise RuntimeError(f"cg_rt_frame_columns failed with {rc}")
     return c0.value, c1.value
+
+
+def probe_div3_device(d_x, d_den, n, d_q, stream=None):
+    """cg_rt_probe_div3_device: d_q[3i + k] = d_x[3i + k] / d_den[i] as the light-set sweep divides
+    (device pointers; asynchronous on `stream`)."""
+    if load().cg_rt_probe_div3_device(P(d_x), P(d_den), n, P(d_q), P(stream) if stream else None) != CG_OK:
+        raise RuntimeError("cg_rt_probe_div3_device failed")
 
 
 def kernel_timing(enable: bool):

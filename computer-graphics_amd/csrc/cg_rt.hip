@@ -2206,6 +2206,30 @@ extern "C" int cg_diag_wg_count(unsigned *n)
 }
 #endif
 
+namespace cg {
+// div3_by<true> on n (numerator triple, denominator) pairs: the test of the shared-reciprocal
+// division against IEEE x / d (tests/test_rt_gpu.py)
+__global__ void rt_probe_div3_kernel(const float *__restrict__ x, const float *__restrict__ d, int n,
+                                     float *__restrict__ q)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const vec3 r = div3_by<true>(v3(x[3 * i], x[3 * i + 1], x[3 * i + 2]), d[i]);
+    q[3 * i] = r.x;
+    q[3 * i + 1] = r.y;
+    q[3 * i + 2] = r.z;
+}
+}  // namespace cg
+
+extern "C" int cg_rt_probe_div3_device(const float *d_x, const float *d_den, int n, float *d_q, void *stream)
+{
+    if (n < 0 || (n && (!d_x || !d_den || !d_q))) return CG_E_INVALID;
+    if (n == 0) return CG_OK;
+    hipLaunchKernelGGL(cg::rt_probe_div3_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_x, d_den,
+                       n, d_q);
+    return hipGetLastError() == hipSuccess ? CG_OK : CG_E_HIP;
+}
+
 #ifdef CG_WORK_COUNT
 // Counting build: this translation unit's work counters (cg_rt_dev.h WorkKind order); reset after reading.
 extern "C" int cg_diag_work_counts_rt(unsigned long long *out, int reset)

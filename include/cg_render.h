@@ -229,6 +229,11 @@ int cg_rt_probe_closest(cg_ctx *ctx, const cg_vec4 *starts, const cg_vec4 *dirs,
                         cg_isect *out, int *hit);
 int cg_rt_probe_direct_light(cg_ctx *ctx, const cg_isect *isects, const cg_light *light, int n,
                              cg_vec3 *out);
+/* DirectLight's three divides by one area (:412) as the light-set sweep performs
+ * them (a shared reciprocal inside a range guard, IEEE x / d outside it), on
+ * device arrays: d_q[3i + k] = d_x[3i + k] / d_den[i]; a test that they are
+ * IEEE-exact. */
+int cg_rt_probe_div3_device(const float *d_x, const float *d_den, int n, float *d_q, void *stream);
 /* Test hook for large scenes (n_tris > 64): capacity of the device queue of
  * shadow rays the blocker hints leave to the certified lit search (0 = the
  * default, 65536).  Rays past the queue are searched per pixel by the shading

@@ -708,3 +708,40 @@ def test_rt_edge_poses_vs_live_oracle(rt, pose):
     ref = oracle.rt_draw(mg.rt_params_of(cfg), threads=min(16, os.cpu_count() or 8))
     bad = np.flatnonzero(argb != ref)
     assert bad.size == 0, f"{pose}: {bad.size} differ, first {bad[:6]} gpu {argb[bad[:3]]} ref {ref[bad[:3]]}"
+
+
+def test_rt_div3_shared_reciprocal_is_ieee(ctx):
+    """The light-set sweep's three divides by one area (:412) through one refined reciprocal
+    (cg_rt_dev.h div3_by, inside its range guard; IEEE x / d outside) == numpy's IEEE float32
+    x / d, bit for bit: 6M quotients over C4's operand ranges (area 4 pi |r|^2 of nearby
+    lights, numerators colour x light x cos), log-uniform operands across the whole float range,
+    both ends of the guard, zeros of both signs, denormals, infinities and NaN."""
+    import torch
+    rng = np.random.default_rng(0xD1B3)
+    n = 2_000_000
+
+    def logu(k, lo, hi):
+        return np.exp2(rng.uniform(lo, hi, k)).astype(np.float32)
+
+    den = np.concatenate([logu(n // 2, -8, 12),                                   # C4-like areas
+                          logu(n // 4, -140, 127) * rng.choice([-1, 1], n // 4).astype(np.float32),
+                          np.float32(2.0) ** rng.integers(-42, 43, n // 4).astype(np.float32)])
+    x = np.concatenate([logu(3 * (n // 2), -30, 6),                               # C4-like numerators
+                        logu(3 * (n // 4), -150, 127) * rng.choice([-1, 1], 3 * (n // 4)).astype(np.float32),
+                        np.float32(2.0) ** rng.integers(-90, 43, 3 * (n // 4)).astype(np.float32)])
+    specials = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-39, np.inf, -np.inf, np.nan, 2.0 ** -86, 2.0 ** -87,
+                         2.0 ** 40, 2.0 ** 41, 2.0 ** -40, 2.0 ** -41, 3.4e38], dtype=np.float32)
+    k = len(specials)
+    den[:k * k] = np.repeat(specials, k)
+    x[:3 * k * k] = np.tile(specials, 3 * k)
+    with np.errstate(all="ignore"):
+        want = x.reshape(-1, 3) / den[:, None]
+    dx = torch.from_numpy(x).cuda()
+    dd = torch.from_numpy(den).cuda()
+    dq = torch.empty_like(dx)
+    cgamd.probe_div3_device(dx.data_ptr(), dd.data_ptr(), n, dq.data_ptr())
+    torch.cuda.synchronize()
+    got = dq.cpu().numpy().reshape(-1, 3)
+    same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+    bad = np.argwhere(~same)
+    assert bad.size == 0, f"{len(bad)} quotients differ, first {[(x.reshape(-1, 3)[i, j], den[i], got[i, j], want[i, j]) for i, j in bad[:5]]}"
