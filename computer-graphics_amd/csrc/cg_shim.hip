@@ -1699,7 +1699,17 @@ extern "C" int cg_rast_draw_frames_device(cg_ctx *c, const cg_rast_params *ps, i
             return ctx_invalid(c, "draw_frames: colour mode 0 frames of one size (modes 1-2 chain rand offsets)");
     CG_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    const int L = std::min(2, n_frames);   // lanes in flight: 2 measured faster than 3 or 4 (C3, round 1)
+    // lanes in flight (CG_RAST_LANES for A/B runs): 6 -- C3 1080p, 64 frames per call, round 6:
+    // 2 lanes 21.3-21.4k frames/s, 3 18.0k, 4 21.2k, 5 22.6-22.7k, 6 23.1-23.3k, 7 20.7-20.9k,
+    // 8 21.3-22.4k (profiles/r06_ab_session2.json; round 1 had found 2 best).  The lanes' streams
+    // share the process's 4 hardware queues, so the count sets how the frames' latency-bound
+    // kernels interleave; 6 was best both alone and inside the default bench line
+    static const int lanes = [] {
+        const char *e = std::getenv("CG_RAST_LANES");
+        const int v = e ? std::atoi(e) : 6;
+        return std::max(1, std::min(v, (int)cg_ctx::kRastLanes));
+    }();
+    const int L = std::min(lanes, n_frames);
     if (!c->start_ev) CG_TRY(c, hipEventCreateWithFlags(&c->start_ev, hipEventDisableTiming), "event");
     for (int k = 0; k < L; ++k) {
         if (!c->lanes[k]) {
