@@ -1446,7 +1446,10 @@ __device__ __forceinline__ int launder(int v)
 #ifdef CG_WALK_WAVES
 template <int LM> constexpr int walk_waves() { return CG_WALK_WAVES; }
 #else
-template <int LM> constexpr int walk_waves() { return LM == 1 ? 4 : 3; }
+// Round 6, with the hints' grid walks queued: the lattice mode at 5 (96 VGPRs, 68 B of scratch;
+// C5 210.9 -> 216.7 fps, 6 waves 216.3) and the yawed mode at 4 (C5-yaw 145.0 -> 151.2, 5 waves
+// 149.6, 6 124.9); the per-pixel mode (no bench configuration) stays at 3
+template <int LM> constexpr int walk_waves() { return LM == 1 ? 5 : LM == 2 ? 4 : 3; }
 #endif
 
 template <int LM>   // 0: per-pixel mode, 1: lattice, 2: lattice with per-pixel columns
@@ -1916,7 +1919,10 @@ __device__ __forceinline__ vec4 pixel_dir(const RtFrame &F, int u, int v)
 // light) sequence, so the wave's lanes meet at each step of the neighbour
 // exchange.
 #ifndef CG_HINT_WAVES
-#define CG_HINT_WAVES 4   // 99-101 VGPRs, no scratch; 5: 12-16 B, 6: 68-76 B -- all the same speed (r05_ab_walk.json)
+// 6 waves/SIMD: 80 VGPRs, 72-80 B of scratch.  Round 5 measured 4 (no scratch), 5 and 6 the same
+// speed; with the grid walks queued per wave (below) 6 is fastest: C5 204.5 / 208.7 / 211.7 fps and
+// C5-yaw 140.8 / 143.4 / 146 at 4 / 5 / 6, 7 and 8 slower (profiles/r06_ab_session2.json)
+#define CG_HINT_WAVES 6
 #endif
 // The grid walks of a wave's unresolved shadow rays are deferred to the end of
 // the wave (a per-wave LDS queue, kHintQ rays) and then walked 64 at a time, one
