@@ -1441,8 +1441,9 @@ __device__ __forceinline__ int launder(int v)
 #endif
 // Waves per SIMD of the walk: the lattice mode (C5) fits 4 in 123 VGPRs with
 // no scratch once its slots are parked and its wave index is uniform; the
-// yawed (7 slots) and per-pixel (9 slots) modes need 3 for no scratch.
-// CG_WALK_WAVES overrides every mode (A/B builds).
+// yawed (7 slots) and per-pixel (9 slots) modes need 3 for no scratch.  More
+// waves with some scratch are faster now (below).  CG_WALK_WAVES overrides
+// every mode (A/B builds).
 #ifdef CG_WALK_WAVES
 template <int LM> constexpr int walk_waves() { return CG_WALK_WAVES; }
 #else
