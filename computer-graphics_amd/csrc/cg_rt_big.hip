@@ -949,7 +949,10 @@ __device__ void bin_certify_batch(const RtFrame &F, const RtTri *__restrict__ tc
     __syncthreads();                                        // s_w / s_base / s_lo reused by the next batch
 }
 
-__global__ __launch_bounds__(256, 4) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
+#ifndef CG_BINP_WAVES
+#define CG_BINP_WAVES 4   // A/B: -DCG_BINP_WAVES=n
+#endif
+__global__ __launch_bounds__(256, CG_BINP_WAVES) void rt_bin_primary_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                              const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int bin = blockIdx.y;
@@ -1027,7 +1030,10 @@ __device__ __forceinline__ int depth_bucket(unsigned kbits, const BigBufs &B, in
 
 // Per bin: bucket sizes and each bucket's smallest key (workgroups stride
 // over the bin's chunks).
-__global__ __launch_bounds__(256, 4) void rt_bin_count_kernel(RtFrame F, const RtTri *__restrict__ tc,
+#ifndef CG_BINC_WAVES
+#define CG_BINC_WAVES 4   // A/B: -DCG_BINC_WAVES=n
+#endif
+__global__ __launch_bounds__(256, CG_BINC_WAVES) void rt_bin_count_kernel(RtFrame F, const RtTri *__restrict__ tc,
                                                            const cg_tri *__restrict__ tris, BigBufs B)
 {
     const int bin = blockIdx.y, nc = B.bin_nch[bin];
@@ -1280,7 +1286,12 @@ __device__ __forceinline__ void half_mask_one(const RtFrame &F, const RtTri *__r
                                               hx1, hy0, hy1, F.focal);
     B.bin_spbox[p] = mk ? (mk << 32) | kMaskTag : kProjNone;
 }
-__global__ __launch_bounds__(256) void rt_half_mask_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+#ifdef CG_HALF_WAVES   // A/B builds
+__global__ __launch_bounds__(256, CG_HALF_WAVES) void rt_half_mask_kernel(
+#else
+__global__ __launch_bounds__(256) void rt_half_mask_kernel(
+#endif
+    RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
     const long long total = (long long)min((unsigned long long)B.pool_n[kPoolSorted], (unsigned long long)B.cap_sorted);
     __shared__ long long s_q[512];
@@ -2348,7 +2359,12 @@ __device__ bool lit_blocked_lane(const RtTri *__restrict__ tc, const BigBufs &B,
 
 // One wave per unresolved shadow ray (grid-stride); a blocked ray sets its
 // verdict bit.
-__global__ __launch_bounds__(256) void rt_pending_lit_kernel(RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
+#ifdef CG_PEND_WAVES   // A/B builds
+__global__ __launch_bounds__(256, CG_PEND_WAVES) void rt_pending_lit_kernel(
+#else
+__global__ __launch_bounds__(256) void rt_pending_lit_kernel(
+#endif
+    RtFrame F, const RtTri *__restrict__ tc, BigBufs B)
 {
     const int np = min(*B.pend_n, B.max_pend);
     const int lane = threadIdx.x & 63;
@@ -2364,7 +2380,12 @@ __global__ __launch_bounds__(256) void rt_pending_lit_kernel(RtFrame F, const Rt
 // more than 7 lights in per-pixel mode each (s, l) is resolved here (grid,
 // then the bin's certified shadow list).
 template <int LM>
-__global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(RtFrame F, const RtTri *__restrict__ tc,
+#ifdef CG_SHADE_WAVES   // A/B builds
+__global__ __launch_bounds__(kRtThreads, CG_SHADE_WAVES) void rt_big_shade_kernel(
+#else
+__global__ __launch_bounds__(kRtThreads) void rt_big_shade_kernel(
+#endif
+    RtFrame F, const RtTri *__restrict__ tc,
                                                                   const RtShade *__restrict__ shade,
                                                                   const RtSphere *__restrict__ sph, BigBufs B,
                                                                   uint32_t *__restrict__ out)
