@@ -1707,7 +1707,12 @@ __global__ __launch_bounds__(kRtThreads, kRtMinWaves) void rt_lattice_kernel(RtF
 }
 
 template <int PITCH>
-__global__ __launch_bounds__(kRtThreads) void rt_lattice_units_kernel(RtFrame F0, const RtTri *__restrict__ tc,
+// 4 waves/SIMD: 128 VGPRs, 36 B of scratch (unbounded it took 137 VGPRs, 3 waves): C4 97.95 ->
+// 98.5 fps; 5 waves (136 B) the same (profiles/r06_ab_session2.json)
+#ifndef CG_UNITS_WAVES
+#define CG_UNITS_WAVES 4
+#endif
+__global__ __launch_bounds__(kRtThreads, CG_UNITS_WAVES) void rt_lattice_units_kernel(RtFrame F0, const RtTri *__restrict__ tc,
                                                                       const RtShade *__restrict__ shade,
                                                                       const RtSphere *__restrict__ sph,
                                                                       const unsigned long long *__restrict__ lat_masks,
