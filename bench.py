@@ -607,7 +607,7 @@ def main():
                     help="rt, N = 1: omit the `draw` record (the host-buffer boundary: cg_rt_render / cg_rt_render_frames)")
     ap.add_argument("--no-sub", action="store_true",
                     help="rt: omit the C3/C4/C5 sub-records (only the C2 metric line)")
-    ap.add_argument("--sub-frames", default="c4:32:3,c5:10:2",
+    ap.add_argument("--sub-frames", default="c4:32:3,c5:20:3",
                     help="rt: the build-defined sub-records as workload:steps:warmup (comma separated); "
                          "'' for none")
     ap.add_argument("--rast-batch", type=int, default=64,
