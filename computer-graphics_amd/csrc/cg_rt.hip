@@ -436,7 +436,10 @@ __device__ __forceinline__ unsigned long long seg_or(unsigned long long v, int c
 __device__ __forceinline__ void lat_flatten(const LatFlatten &Z);   // below, with the lattice kernel
 
 #ifndef CG_CERT_WAVES
-#define CG_CERT_WAVES 4   // waves per SIMD of the certificate launch (A/B: -DCG_CERT_WAVES=n)
+// waves per SIMD of the certificate launch (A/B: -DCG_CERT_WAVES=n): 3 -- 154 VGPRs and no scratch
+// (4: 128 VGPRs and 80 B of scratch): the driver-shaped call's certificates 81.8 -> 73.6 us live
+// (CG_KTIME_ALL, four runs each; profiles/r06_ab_session2.json); 5 waves (236 B of scratch) slower
+#define CG_CERT_WAVES 3
 #endif
 __global__ __launch_bounds__(256, CG_CERT_WAVES) void rt_tile_cert_kernel(const cg_tri *__restrict__ tris,
                                                            const RtGeo *__restrict__ geo, int n, RtFrameCams cams,
@@ -1947,13 +1950,13 @@ hipError_t launch_rt_prepare(const cg_tri *d_tris, const RtGeo *d_geo, int n, co
     // forces the fused kernel's threads per super-tile.
     static const int single_max = env_int("CG_CERT_SINGLE_MAX", 0);
     static const int force_threads = env_int("CG_CERT_THREADS", 0);
-    // resident 4-wave workgroups of rt_tile_cert_kernel (4 waves per SIMD: 128 VGPRs)
+    // resident 4-wave workgroups of rt_tile_cert_kernel (CG_CERT_WAVES per SIMD)
     static const int resident4 = [] {
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        return cus * 4;
+        return cus * CG_CERT_WAVES;
     }();
     const size_t wtiles = F ? (size_t)(F->txn ? F->txn : lat_tiles_x(*F)) * (rt_cert_units(*F, 0) / lat_tiles_x(*F)) : 0;
     const int sup = (d_sup_masks && !(F && wtiles * nframes < (size_t)single_max)) ? 1 : 0;
