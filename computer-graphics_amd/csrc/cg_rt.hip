@@ -758,6 +758,10 @@ constexpr int kLatW = 2 * kLatTileW + 1, kLatH = 2 * kLatTileH + 1;
 #define CG_LAT_INTERLEAVE 1   // rt_lattice_kernel's points dealt to waves in 64-point chunks (A/B: 0)
 #endif
 constexpr int kLatWY = 3 * kLatTileW;   // per-pixel columns (a yawed camera): 48 x 31 = 1488 rays
+#ifndef CG_LAT_SOA
+#define CG_LAT_SOA 1   // per-pixel-column lattice: point values and hit indices in separate LDS arrays (A/B: 0)
+#endif
+constexpr int kLatSoaNoHit = -128;   // int8 hit index of a miss (hits: -kLatMaxSph .. 62)
 
 // Shared pieces of the two lattice kernels.
 //
@@ -1093,8 +1097,14 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
     lat_store_outside(F, G, o, S.bx);
     const int ay0 = G.ay0, cols = G.cols, rows = G.rows;
     // per lattice point: .w = hit index bits (INT_MIN: no hit); .x = t after
-    // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample)
-    __shared__ float4 s_pt[PITCH * kLatH];
+    // pass 1, .xyz = DirectLight after pass 2 (one ds_read_b128 per sample).
+    // Per-pixel columns (PITCH 48, CG_LAT_SOA): the three values and the hit
+    // index (int8, kLatSoaNoHit: none) in separate arrays, 13 bytes a point
+    // instead of 16, so that seven workgroups fit a CU's LDS instead of five.
+    constexpr bool kSoA = CG_LAT_SOA && PITCH == kLatWY;
+    __shared__ float4 s_pt[kSoA ? 1 : PITCH * kLatH];
+    __shared__ float s_v[kSoA ? 3 : 1][kSoA ? PITCH * kLatH : 1];
+    __shared__ int8_t s_h[kSoA ? PITCH * kLatH : 1];
     __shared__ LatObj s_obj[kLatSphSlot + kLatMaxSph];
     __shared__ uint32_t s_px[kLatTileH * kLatTileW];
     lat_load_objs(s_obj, shade, sph, F.n_tris, F.n_sph);
@@ -1173,7 +1183,14 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
         return;                            // the whole workgroup (m0 is uniform)
     }
     __syncthreads();                       // s_obj
-    auto stt = [&](int p, float t, int bi) { s_pt[p] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi)); };
+    auto stt = [&](int p, float t, int bi) {
+        if constexpr (kSoA) {
+            s_v[0][p] = t;
+            s_h[p] = (int8_t)(bi == INT_MIN ? kLatSoaNoHit : bi);
+        } else {
+            s_pt[p] = make_float4(t, 0.0f, 0.0f, __int_as_float(bi));
+        }
+    };
     if constexpr (kNP4)
         lat_closest<PITCH, decltype(stt), 4>(Fp, tc, sph, mask, covered, G, p_lo, p_hi, lane, stt, step1, 256);
     else
@@ -1187,14 +1204,28 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
         const int p = p0 + lane;
         const int cy = p / PITCH, cx = p - cy * PITCH, idx = p;
         if (p < p_hi && cx < cols) {
-            const float4 q = s_pt[idx];
-            const int bi = __float_as_int(q.w);
+            float t;
+            int bi;
+            if constexpr (kSoA) {
+                const int h = s_h[idx];
+                bi = h == kLatSoaNoHit ? INT_MIN : h;
+                t = s_v[0][idx];
+            } else {
+                const float4 q = s_pt[idx];
+                bi = __float_as_int(q.w);
+                t = q.x;
+            }
             if (bi != INT_MIN) {
                 const float X = lat_x(F, G, cx), Y = 0.5f * (float)(ay0 + cy);
-                const float t = q.x;
                 const vec3 pos = v3(F.cam[0] + t * X, F.cam[1] + t * Y, F.cam[2] + t * F.focal);
                 const vec3 dl = lat_direct_light(Fs, tc, sph, s_obj, F.lights[0], bi, pos, smask);
-                s_pt[idx] = make_float4(dl.x, dl.y, dl.z, q.w);
+                if constexpr (kSoA) {
+                    s_v[0][idx] = dl.x;
+                    s_v[1][idx] = dl.y;
+                    s_v[2][idx] = dl.z;
+                } else {
+                    s_pt[idx] = make_float4(dl.x, dl.y, dl.z, __int_as_float(bi));
+                }
             }
         }
     }
@@ -1210,11 +1241,20 @@ __device__ __forceinline__ void lattice_body(const RtFrame &F0, const RtTri *__r
         for (int k = 0; k < 9; ++k) {
             const int i = k / 3 - 1, j = k % 3 - 1;
             const int idx = (2 * ty + 1 + j) * PITCH + ((G.yaw ? 3 : 2) * tx + 1 + i);
-            const float4 q = s_pt[idx];
-            const int bi = __float_as_int(q.w);
+            int bi;
+            vec3 dl;
+            if constexpr (kSoA) {
+                const int h = s_h[idx];
+                bi = h == kLatSoaNoHit ? INT_MIN : h;
+                dl = v3(s_v[0][idx], s_v[1][idx], s_v[2][idx]);
+            } else {
+                const float4 q = s_pt[idx];
+                bi = __float_as_int(q.w);
+                dl = v3(q.x, q.y, q.z);
+            }
             if (bi == INT_MIN) continue;
             valid = true;
-            pc = pc + v3(q.x, q.y, q.z);                                                  // :151-153
+            pc = pc + dl;                                                                 // :151-153
             pc = pc + (lat_colour(s_obj, bi) * ind);                                      // :156
         }
         px = valid ? put_pixel(div_const(pc, 9.0f, 1.0f / 9.0f)) : put_pixel(v3(0.0f, 0.0f, 0.0f));   // :160-166
